@@ -1,0 +1,73 @@
+"""In-tree builds of the native pieces (no JIT cache: the .so files travel with the repo).
+
+  _synth.so       host C corpus generator (bench/test utility)
+  _akshar_hip.so  the product: HIP kernels for gfx950 + the C-ABI declared in include/akshar.h
+  oracle/_oracle.so  the CPU restatement (test infrastructure; built by oracle/Makefile)
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("AK_OFFLOAD_ARCH", "gfx950")
+
+
+def _run(cmd, cwd=None):
+    print("+", " ".join(cmd), file=sys.stderr)
+    subprocess.check_call(cmd, cwd=cwd)
+
+
+def _stale(out, srcs):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(s) > t for s in srcs)
+
+
+def build_synth(force=False):
+    src = os.path.join(CSRC, "synth.c")
+    out = os.path.join(HERE, "_synth.so")
+    if force or _stale(out, [src]):
+        _run(["gcc", "-O2", "-fopenmp", "-fPIC", "-shared", "-o", out, src])
+    return out
+
+
+def hip_sources():
+    names = sorted(os.listdir(CSRC))
+    srcs = [os.path.join(CSRC, n) for n in names if n.endswith((".hip", ".h", ".hpp", ".cpp"))]
+    srcs += [os.path.join(CSRC, "gen", n) for n in sorted(os.listdir(os.path.join(CSRC, "gen")))]
+    srcs.append(os.path.join(ROOT, "include", "akshar.h"))
+    return srcs
+
+
+def build_hip(force=False):
+    out = os.path.join(HERE, "_akshar_hip.so")
+    srcs = [os.path.join(CSRC, n) for n in sorted(os.listdir(CSRC)) if n.endswith((".hip", ".cpp"))]
+    if force or _stale(out, hip_sources()):
+        cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH, "-O3", "-std=c++17",
+               "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"), "-I", CSRC,
+               "-Wall", "-Wno-unused-function", "-o", out] + srcs
+        _run(cmd)
+    return out
+
+
+def build_oracle(force=False):
+    oracle = os.path.join(ROOT, "oracle")
+    args = ["make", "-s", "-C", oracle]
+    if force:
+        args.append("-B")
+    _run(args)
+    return os.path.join(oracle, "_oracle.so")
+
+
+def build_all(force=False):
+    build_synth(force)
+    build_oracle(force)
+    build_hip(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
