@@ -43,14 +43,29 @@ def hip_sources():
     return srcs
 
 
-def build_hip(force=False):
+def build_hip(force=False, jobs=None):
+    """Compile each .hip TU to an object in parallel, then link the shared library."""
+    from concurrent.futures import ThreadPoolExecutor
     out = os.path.join(HERE, "_akshar_hip.so")
     srcs = [os.path.join(CSRC, n) for n in sorted(os.listdir(CSRC)) if n.endswith((".hip", ".cpp"))]
-    if force or _stale(out, hip_sources()):
-        cmd = [os.path.join(ROCM, "bin", "hipcc"), "--offload-arch=" + ARCH, "-O3", "-std=c++17",
-               "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"), "-I", CSRC,
-               "-Wall", "-Wno-unused-function", "-o", out] + srcs
-        _run(cmd)
+    if not (force or _stale(out, hip_sources())):
+        return out
+    objdir = os.path.join(ROOT, "build", "hip")
+    os.makedirs(objdir, exist_ok=True)
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    common = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include"),
+              "-I", CSRC, "-Wall", "-Wno-unused-function"]
+    objs = []
+    cmds = []
+    for src in srcs:
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmds.append(common + ["-c", "-o", obj, src])
+    jobs = jobs or min(len(cmds), max(1, (os.cpu_count() or 4)), 16)
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(_run, c) for c in cmds]:
+            f.result()
+    _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs)
     return out
 
 

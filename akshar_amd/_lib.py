@@ -1,0 +1,68 @@
+"""ctypes binding of the HIP engine's C-ABI (include/akshar.h, akshar_amd/_akshar_hip.so).
+
+There is no CPU fallback: if the library or a GPU is missing, every call raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_akshar_hip.so")
+
+AK_OK = 0
+AK_NORM_LOWER = 1
+AK_NORM_CLEAN = 2
+AK_RAW = -1
+AK_ROW_BAD_UTF8 = 1
+AK_ROW_LIMIT = 4
+
+P = ctypes.c_void_p
+U64 = ctypes.c_uint64
+I32 = ctypes.c_int
+U32 = ctypes.c_uint32
+
+_LIB = None
+
+# every symbol include/akshar.h declares, with its ctypes signature
+SIGNATURES = {
+    "ak_last_error": (ctypes.c_char_p, []),
+    "ak_version": (I32, []),
+    "ak_ws_create": (I32, [ctypes.POINTER(P)]),
+    "ak_ws_free": (None, [P]),
+    "ak_bpe_create": (I32, [U32, P, P, U32, P, U32, U32, ctypes.POINTER(P)]),
+    "ak_bpe_free": (None, [P]),
+    "ak_spm_create": (I32, [U32, P, P, P, P, ctypes.c_int32, P, ctypes.POINTER(P)]),
+    "ak_spm_free": (None, [P]),
+    "ak_normalize": (I32, [P, I32, P, P, U64, P, U64, P, P, P]),
+    "ak_segment": (I32, [P, I32, I32, P, P, U64, P, U64, P, P, P]),
+    "ak_switches": (I32, [P, I32, P, P, U64, P, P, U64, P, P, P]),
+    "ak_bpe_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
+    "ak_spm_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
+    "ak_normalize_cap": (U64, [U64, U64]),
+    "ak_segment_cap": (U64, [U64, U64]),
+    "ak_bpe_encode_cap": (U64, [U64, U64]),
+    "ak_spm_encode_cap": (U64, [U64, U64]),
+}
+
+
+class AksharError(RuntimeError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise AksharError("HIP engine not built: %s missing (run __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc, what):
+    if rc != AK_OK:
+        msg = lib().ak_last_error().decode("utf-8", "replace")
+        raise AksharError("%s failed (%d): %s" % (what, rc, msg))

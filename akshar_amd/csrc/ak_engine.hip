@@ -1,0 +1,382 @@
+// ak_engine.hip — kernels and C-ABI (include/akshar.h) of the MI355X tokenization engine.
+//
+// Execution plan of every batch call (one HIP stream, no host synchronization):
+//   1. count   (fast kernel)  one lane per row runs the fused row pipeline (ak_dev.h) and only
+//                              counts its outputs; rows whose fast-path buffers overflow are
+//                              appended to a slow list.
+//   2. count   (slow kernel)  the slow list, with large per-thread buffers in a global pool.
+//   3. scan                    u32 row counts -> u64 row offsets (out_offs[n] = total).
+//   4. emit    (fast + slow)   the same pipelines again, writing at the scanned offsets.
+// Property tables for U+0000..U+09FF and the BPE single-char ids are staged in LDS per block;
+// the BPE merge table (open addressing, 8 B entries) and the SPM double-array trie stay in
+// HBM and are served from L2.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "akshar.h"
+#include "ak_internal.h"
+#include "ak_model_build.h"
+
+using namespace ak;
+
+// ------------------------------------------------------------------------------------------
+// errors
+
+static thread_local std::string g_err;
+
+int ak::set_error(int code, const char *msg) {
+    g_err = msg;
+    return code;
+}
+
+int ak::set_hip_error(const char *expr, hipError_t e) {
+    g_err = std::string(expr) + ": " + hipGetErrorString(e);
+    return AK_ERR_HIP;
+}
+
+static int fail(int code, const char *msg) { return ak::set_error(code, msg); }
+
+extern "C" const char *ak_last_error(void) { return g_err.c_str(); }
+extern "C" int ak_version(void) { return 1; }
+
+// ------------------------------------------------------------------------------------------
+// models
+
+struct ak_bpe {
+    BpeDev dev;
+    uint64_t *d_tab = nullptr;
+    uint16_t *d_single_fast = nullptr;  // FAST_N entries
+    uint32_t *d_single_cp = nullptr;
+    uint16_t *d_single_id = nullptr;
+};
+
+struct ak_spm {
+    SpmDev dev;
+    int4 *d_trie = nullptr;
+    float *d_scores = nullptr;
+    int32_t *d_byte_ids = nullptr;
+    uint32_t n_nodes = 0;
+};
+
+extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const uint32_t *single_id,
+                             uint32_t n_merges, const uint32_t *merges, uint32_t bos, uint32_t eos,
+                             ak_bpe **out) {
+    if (!out || (n_single && (!single_cp || !single_id)) || (n_merges && !merges))
+        return fail(AK_ERR_ARG, "ak_bpe_create: null argument");
+    akb::BpeTables t;
+    const std::string err = akb::build_bpe(n_single, single_cp, single_id, n_merges, merges, t);
+    if (!err.empty()) return fail(AK_ERR_UNSUPPORTED, ("ak_bpe_create: " + err).c_str());
+    ak_bpe *m = new ak_bpe();
+    HIP_TRY(hipMalloc(&m->d_tab, t.tab.size() * sizeof(uint64_t)));
+    HIP_TRY(hipMemcpy(m->d_tab, t.tab.data(), t.tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_single_fast, FAST_N * sizeof(uint16_t)));
+    HIP_TRY(hipMemcpy(m->d_single_fast, t.fast.data(), FAST_N * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_single_cp, t.rest_cp.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(m->d_single_cp, t.rest_cp.data(), t.rest_cp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_single_id, t.rest_id.size() * sizeof(uint16_t)));
+    HIP_TRY(hipMemcpy(m->d_single_id, t.rest_id.data(), t.rest_id.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    m->dev.merge_tab = m->d_tab;
+    m->dev.tab_mask = t.mask;
+    m->dev.single_sorted_cp = m->d_single_cp;
+    m->dev.single_sorted_id = m->d_single_id;
+    m->dev.n_single = t.n_rest;
+    m->dev.bos = bos;
+    m->dev.eos = eos;
+    *out = m;
+    return AK_OK;
+}
+
+extern "C" void ak_bpe_free(ak_bpe *m) {
+    if (!m) return;
+    (void)hipFree(m->d_tab);
+    (void)hipFree(m->d_single_fast);
+    (void)hipFree(m->d_single_cp);
+    (void)hipFree(m->d_single_id);
+    delete m;
+}
+
+extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
+                             const uint8_t *types, int32_t unk_id, const int32_t *byte_ids, ak_spm **out) {
+    if (!out || !piece_offs || !scores || !types || !byte_ids || (n && !piece_bytes))
+        return fail(AK_ERR_ARG, "ak_spm_create: null argument");
+    akb::SpmTables t;
+    const std::string err = akb::build_spm(n, piece_bytes, piece_offs, scores, types, t);
+    if (!err.empty()) return fail(AK_ERR_UNSUPPORTED, ("ak_spm_create: " + err).c_str());
+    ak_spm *m = new ak_spm();
+    m->n_nodes = t.n_nodes;
+    HIP_TRY(hipMalloc(&m->d_trie, t.n_nodes * sizeof(int4)));
+    HIP_TRY(hipMemcpy(m->d_trie, t.trie.data(), t.n_nodes * sizeof(int4), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_scores, std::max<uint32_t>(n, 1) * sizeof(float)));
+    HIP_TRY(hipMemcpy(m->d_scores, scores, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_byte_ids, 256 * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(m->d_byte_ids, byte_ids, 256 * sizeof(int32_t), hipMemcpyHostToDevice));
+    m->dev.trie = m->d_trie;
+    m->dev.scores = m->d_scores;
+    m->dev.byte_ids = m->d_byte_ids;
+    m->dev.unk_id = unk_id;
+    m->dev.unk_score = t.min_score - 10.0f;
+    m->dev.max_score = t.max_score;
+    *out = m;
+    return AK_OK;
+}
+
+extern "C" void ak_spm_free(ak_spm *m) {
+    if (!m) return;
+    (void)hipFree(m->d_trie);
+    (void)hipFree(m->d_scores);
+    (void)hipFree(m->d_byte_ids);
+    delete m;
+}
+
+// ------------------------------------------------------------------------------------------
+// workspace
+
+extern "C" int ak_ws_create(ak_ws **out) {
+    if (!out) return fail(AK_ERR_ARG, "ak_ws_create: null");
+    ak_ws *w = new ak_ws();
+    HIP_TRY(hipMalloc(&w->slow_count, 64));
+    const size_t T = SLOW_THREADS;
+    const size_t bytes = T * (2 * SLOW_SEG * 4 + 8 * SLOW_SEG * 4 + SLOW_WORD * 2 + SLOW_WORD * 4 + SLOW_WORD * 4 +
+                              3 * (SLOW_WORD + 1) * 4) + 4096;
+    HIP_TRY(hipMalloc(&w->pool_mem, bytes));
+    char *p = (char *)w->pool_mem;
+    auto take = [&](size_t b) { char *r = p; p += (b + 255) & ~(size_t)255; return (void *)r; };
+    w->pool.seg = (uint32_t *)take(T * 2 * SLOW_SEG * 4);
+    w->pool.dec = (uint32_t *)take(T * 8 * SLOW_SEG * 4);
+    w->pool.wsym = (uint16_t *)take(T * SLOW_WORD * 2);
+    w->pool.wpair = (uint32_t *)take(T * SLOW_WORD * 4);
+    w->pool.vchar = (uint32_t *)take(T * SLOW_WORD * 4);
+    w->pool.vbest = (float *)take(T * (SLOW_WORD + 1) * 4);
+    w->pool.vstart = (int32_t *)take(T * (SLOW_WORD + 1) * 4);
+    w->pool.vid = (int32_t *)take(T * (SLOW_WORD + 1) * 4);
+    *out = w;
+    return AK_OK;
+}
+
+extern "C" void ak_ws_free(ak_ws *w) {
+    if (!w) return;
+    (void)hipFree(w->counts);
+    (void)hipFree(w->flags);
+    (void)hipFree(w->slow_list);
+    (void)hipFree(w->slow_count);
+    (void)hipFree(w->block_sums);
+    (void)hipFree(w->pool_mem);
+    delete w;
+}
+
+int ak::ws_reserve(AkWs *w, uint64_t n) {
+    if (n > w->cap_rows) {
+        uint64_t c = std::max<uint64_t>(n, 2 * w->cap_rows);
+        (void)hipFree(w->counts);
+        (void)hipFree(w->flags);
+        (void)hipFree(w->slow_list);
+        w->counts = nullptr; w->flags = nullptr; w->slow_list = nullptr;
+        HIP_TRY(hipMalloc(&w->counts, c * 4));
+        HIP_TRY(hipMalloc(&w->flags, c));
+        HIP_TRY(hipMalloc(&w->slow_list, c * 4));
+        w->cap_rows = c;
+    }
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE + 1;
+    if (nb > w->cap_blocks) {
+        uint64_t c = std::max<uint64_t>(nb, 2 * w->cap_blocks);
+        (void)hipFree(w->block_sums);
+        w->block_sums = nullptr;
+        HIP_TRY(hipMalloc(&w->block_sums, c * 8));
+        w->cap_blocks = c;
+    }
+    return AK_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// row kernels
+
+// ------------------------------------------------------------------------------------------
+// exclusive scan u32 counts -> u64 offsets (out[n] = total)
+
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *tmp, uint64_t &total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (int i = 0; i < SCAN_BLOCK / 64; ++i) { const uint64_t t = tmp[i]; tmp[i] = s; s += t; }
+        tmp[SCAN_BLOCK / 64] = s;
+    }
+    __syncthreads();
+    total = tmp[SCAN_BLOCK / 64];
+    const uint64_t r = x - v + tmp[wid];
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const uint32_t *c, uint64_t n, uint64_t *sums) {
+    __shared__ uint64_t tmp[SCAN_BLOCK / 64 + 1];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint64_t s = 0;
+    for (int k = 0; k < SCAN_ITEMS; ++k) if (base + k < n) s += c[base + k];
+    uint64_t tot;
+    (void)block_exclusive_scan(s, tmp, tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_sums(uint64_t *sums, uint64_t nb) {
+    __shared__ uint64_t tmp[SCAN_BLOCK / 64 + 1];
+    uint64_t carry = 0;
+    for (uint64_t base = 0; base < nb; base += SCAN_BLOCK) {
+        const uint64_t i = base + threadIdx.x;
+        const uint64_t v = i < nb ? sums[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(v, tmp, tot);
+        if (i < nb) sums[i] = ex + carry;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) sums[nb] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const uint32_t *c, uint64_t n, const uint64_t *sums,
+                                                           uint64_t nb, uint64_t *out) {
+    __shared__ uint64_t tmp[SCAN_BLOCK / 64 + 1];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint64_t s = 0;
+    for (int k = 0; k < SCAN_ITEMS; ++k) { v[k] = base + k < n ? c[base + k] : 0u; s += v[k]; }
+    uint64_t tot;
+    uint64_t x = block_exclusive_scan(s, tmp, tot) + sums[blockIdx.x];
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        if (base + k < n) out[base + k] = x;
+        x += v[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = sums[nb];
+}
+
+int ak::scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st) {
+    const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    if (nb == 0) {
+        HIP_TRY(hipMemsetAsync(out_offs, 0, 8, st));
+        return AK_OK;
+    }
+    k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, st>>>(w->counts, n, w->block_sums);
+    k_scan_sums<<<1, SCAN_BLOCK, 0, st>>>(w->block_sums, nb);
+    k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, st>>>(w->counts, n, w->block_sums, nb, out_offs);
+    HIP_TRY(hipGetLastError());
+    return AK_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// driver
+
+static int g_cus = 0;
+
+int ak::num_cus() {
+    if (!g_cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 256;
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
+        g_cus = p.multiProcessorCount;
+    }
+    return g_cus;
+}
+
+static int dispatch(int op, int flags, ak_ws *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st) {
+    switch (op) {
+        case OP_NORMALIZE: return launch_normalize(flags, w, a, out_offs, st);
+        case OP_SEGMENT: return launch_segment(flags, w, a, out_offs, st);
+        case OP_SWITCHES: return launch_switches(flags, w, a, out_offs, st);
+        case OP_BPE: return launch_bpe(flags, w, a, out_offs, st);
+        default: return launch_spm(flags, w, a, out_offs, st);
+    }
+}
+
+static int check_common(ak_ws *w, const uint8_t *in, const uint64_t *offs, uint64_t n, const void *out,
+                        uint64_t *out_offs) {
+    if (!w) return fail(AK_ERR_ARG, "null workspace");
+    if (!offs || !out_offs || (n && !in)) return fail(AK_ERR_ARG, "null buffer");
+    if (!out && n) return fail(AK_ERR_ARG, "null output buffer");
+    if (n >= 0xFFFFFFFFull) return fail(AK_ERR_ARG, "too many rows in one call (max 2^32-2)");
+    return AK_OK;
+}
+
+static RowArgs make_args(const uint8_t *in, const uint64_t *offs, uint64_t n, void *out, uint64_t cap,
+                         uint8_t *row_status) {
+    RowArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in = in;
+    a.offs = offs;
+    a.n = n;
+    a.out = out;
+    a.cap = cap;
+    a.row_status = row_status;
+    return a;
+}
+
+extern "C" int ak_normalize(ak_ws *w, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n, uint8_t *out,
+                            uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream) {
+    int rc = check_common(w, in, offs, n, out, out_offs);
+    if (rc) return rc;
+    if (flags < 0 || flags > 3) return fail(AK_ERR_ARG, "ak_normalize: flags must be 0..3");
+    RowArgs a = make_args(in, offs, n, out, cap, row_status);
+    return dispatch(OP_NORMALIZE, flags, w, a, out_offs, (hipStream_t)stream);
+}
+
+extern "C" int ak_segment(ak_ws *w, int flags, int matras, const uint8_t *in, const uint64_t *offs, uint64_t n,
+                          uint32_t *ends, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream) {
+    int rc = check_common(w, in, offs, n, ends, out_offs);
+    if (rc) return rc;
+    RowArgs a = make_args(in, offs, n, ends, cap, row_status);
+    a.matras = matras;
+    return dispatch(OP_SEGMENT, flags, w, a, out_offs, (hipStream_t)stream);
+}
+
+extern "C" int ak_switches(ak_ws *w, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n, uint32_t *ends,
+                           uint8_t *labels, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream) {
+    int rc = check_common(w, in, offs, n, ends, out_offs);
+    if (rc) return rc;
+    if (!labels && n) return fail(AK_ERR_ARG, "ak_switches: null labels");
+    RowArgs a = make_args(in, offs, n, ends, cap, row_status);
+    a.labels = labels;
+    return dispatch(OP_SWITCHES, flags, w, a, out_offs, (hipStream_t)stream);
+}
+
+extern "C" int ak_bpe_encode(const ak_bpe *m, ak_ws *w, int flags, const uint8_t *in, const uint64_t *offs,
+                             uint64_t n, uint32_t *ids, uint64_t cap, uint64_t *out_offs, uint8_t *row_status,
+                             void *stream) {
+    if (!m) return fail(AK_ERR_ARG, "ak_bpe_encode: null model");
+    int rc = check_common(w, in, offs, n, ids, out_offs);
+    if (rc) return rc;
+    if (flags != 2 && flags != 3)
+        return fail(AK_ERR_UNSUPPORTED, "ak_bpe_encode: clean_hinglish=False is not supported (HF NFKC tables cover the normalized alphabet only)");
+    RowArgs a = make_args(in, offs, n, ids, cap, row_status);
+    a.bpe = m->dev;
+    a.single_fast = m->d_single_fast;
+    return dispatch(OP_BPE, flags, w, a, out_offs, (hipStream_t)stream);
+}
+
+extern "C" int ak_spm_encode(const ak_spm *m, ak_ws *w, int flags, const uint8_t *in, const uint64_t *offs,
+                             uint64_t n, uint32_t *ids, uint64_t cap, uint64_t *out_offs, uint8_t *row_status,
+                             void *stream) {
+    if (!m) return fail(AK_ERR_ARG, "ak_spm_encode: null model");
+    int rc = check_common(w, in, offs, n, ids, out_offs);
+    if (rc) return rc;
+    if (flags < 0 || flags > 3) return fail(AK_ERR_ARG, "ak_spm_encode: flags must be 0..3");
+    RowArgs a = make_args(in, offs, n, ids, cap, row_status);
+    a.spm = m->dev;
+    return dispatch(OP_SPM, flags, w, a, out_offs, (hipStream_t)stream);
+}
+
+extern "C" uint64_t ak_normalize_cap(uint64_t n, uint64_t total_bytes) { return 3 * total_bytes + 16 + 0 * n; }
+extern "C" uint64_t ak_segment_cap(uint64_t n, uint64_t total_bytes) { return total_bytes + n + 16; }
+extern "C" uint64_t ak_bpe_encode_cap(uint64_t n, uint64_t total_bytes) { return total_bytes + 2 * n + 16; }
+extern "C" uint64_t ak_spm_encode_cap(uint64_t n, uint64_t total_bytes) { return 3 * total_bytes + 4 * n + 16; }

@@ -1,0 +1,13 @@
+// Host emulation shim: lets tests/emu compile ak_dev.h with g++ to step the exact row pipeline
+// on the CPU (debugging aid; never part of the product library).
+#pragma once
+#include <stdint.h>
+#define __device__
+#define __host__
+#define __forceinline__ inline
+struct uint2 { uint32_t x, y; };
+struct int4 { int x, y, z, w; };
+struct alignas(16) uint4 { uint32_t x, y, z, w; };
+static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
+static inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
+static inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }

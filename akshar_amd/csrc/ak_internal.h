@@ -1,0 +1,174 @@
+// ak_internal.h — engine internals shared by the C-ABI TU (ak_engine.hip) and the per-op kernel
+// TUs (ak_k_*.hip, compiled in parallel): workspace layout, error plumbing, the row kernels and
+// the count -> scan -> emit launcher.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "akshar.h"
+#include "ak_dev.h"
+#include "ak_rows.h"
+
+namespace ak {
+
+int set_error(int code, const char *msg);
+int set_hip_error(const char *expr, hipError_t e);
+
+#define HIP_TRY(x)                                           \
+    do {                                                     \
+        hipError_t e_ = (x);                                 \
+        if (e_ != hipSuccess) return ak::set_hip_error(#x, e_); \
+    } while (0)
+
+constexpr int SCAN_BLOCK = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr uint64_t SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+struct AkWs {
+    uint64_t cap_rows = 0;
+    uint32_t *counts = nullptr;
+    uint8_t *flags = nullptr;
+    uint32_t *slow_list = nullptr;
+    uint32_t *slow_count = nullptr;
+    uint64_t *block_sums = nullptr;
+    uint64_t cap_blocks = 0;
+    void *pool_mem = nullptr;
+    SlowPool pool{};
+};
+
+int ws_reserve(AkWs *w, uint64_t n);
+int scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st);
+int num_cus();
+
+__device__ __forceinline__ void stage_tables(uint2 *fast, uint16_t *sfast, const uint16_t *g_single, bool bpe) {
+    for (uint32_t i = threadIdx.x; i < FAST_N; i += blockDim.x) {
+        fast[i] = prop_global(i);
+        if (bpe) sfast[i] = g_single[i];
+    }
+    __syncthreads();
+}
+
+template <int OP, int FLAGS, bool EMIT>
+__global__ __launch_bounds__(ROW_BLOCK) void k_rows_fast(RowArgs a) {
+    __shared__ uint2 fast[FAST_N];
+    __shared__ uint16_t sfast[OP == OP_BPE ? FAST_N : 1];
+    __shared__ uint16_t wsym[OP == OP_BPE ? ROW_BLOCK * FAST_WORD : 1];
+    __shared__ uint32_t wpair[OP == OP_BPE ? ROW_BLOCK * FAST_WORD : 1];
+    stage_tables(fast, sfast, a.single_fast, OP == OP_BPE);
+
+    uint32_t seg[FAST_SEG], seg2[FAST_SEG];
+    uint32_t dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
+    uint32_t vchar[OP == OP_SPM ? FAST_VCAP : 1];
+    float vbest[OP == OP_SPM ? FAST_VCAP + 1 : 1];
+    int32_t vstart[OP == OP_SPM ? FAST_VCAP + 1 : 1];
+    int32_t vid[OP == OP_SPM ? FAST_VCAP + 1 : 1];
+    Scratch sc;
+    sc.seg = seg;
+    sc.dec = dec;
+    sc.seg2 = seg2;
+    sc.dec2 = dec2;
+    sc.seg_cap = FAST_SEG;
+    sc.wsym = wsym + (OP == OP_BPE ? threadIdx.x * FAST_WORD : 0);
+    sc.wpair = wpair + (OP == OP_BPE ? threadIdx.x * FAST_WORD : 0);
+    sc.word_cap = FAST_WORD;
+    sc.vchar = vchar;
+    sc.vbest = vbest;
+    sc.vstart = vstart;
+    sc.vid = vid;
+    sc.vcap = FAST_VCAP;
+    sc.slow_status = ST_SLOW;
+
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
+        if (EMIT && a.flags[r] != 0) continue;
+        sc.status = 0;
+        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc);
+        if (!EMIT) {
+            const bool slow = (sc.status & ST_SLOW) != 0;
+            a.counts[r] = slow ? 0u : (uint32_t)cnt;
+            a.flags[r] = slow ? 1 : 0;
+            if (slow) a.slow_list[atomicAdd(a.slow_count, 1u)] = (uint32_t)r;
+            if (a.row_status) a.row_status[r] = (uint8_t)(sc.status & ST_BAD_UTF8);
+        }
+    }
+}
+
+template <int OP, int FLAGS, bool EMIT>
+__global__ __launch_bounds__(64) void k_rows_slow(RowArgs a) {
+    __shared__ uint2 fast[FAST_N];
+    __shared__ uint16_t sfast[OP == OP_BPE ? FAST_N : 1];
+    stage_tables(fast, sfast, a.single_fast, OP == OP_BPE);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < SLOW_THREADS
+    Scratch sc;
+    sc.seg = a.pool.seg + t * 2 * SLOW_SEG;
+    sc.dec = a.pool.dec + t * 8 * SLOW_SEG;
+    sc.seg2 = sc.seg + SLOW_SEG;
+    sc.dec2 = sc.dec + 4 * SLOW_SEG;
+    sc.seg_cap = SLOW_SEG;
+    sc.wsym = a.pool.wsym + t * SLOW_WORD;
+    sc.wpair = a.pool.wpair + t * SLOW_WORD;
+    sc.word_cap = SLOW_WORD;
+    sc.vchar = a.pool.vchar + t * SLOW_WORD;
+    sc.vbest = a.pool.vbest + t * (SLOW_WORD + 1);
+    sc.vstart = a.pool.vstart + t * (SLOW_WORD + 1);
+    sc.vid = a.pool.vid + t * (SLOW_WORD + 1);
+    sc.vcap = SLOW_WORD;
+    sc.slow_status = ST_LIMIT;
+    const uint32_t ns = *a.slow_count;
+    for (uint32_t i = (uint32_t)t; i < ns; i += SLOW_THREADS) {
+        const uint64_t r = a.slow_list[i];
+        if (EMIT && a.flags[r] != 1) continue;
+        sc.status = 0;
+        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc);
+        if (!EMIT) {
+            const bool lim = (sc.status & ST_LIMIT) != 0;
+            a.counts[r] = lim ? 0u : (uint32_t)cnt;
+            if (lim) a.flags[r] = 2;
+            if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0u));
+        }
+    }
+}
+
+template <int OP, int FLAGS>
+inline int launch_rows(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_t st) {
+    if (a.n == 0) {
+        HIP_TRY(hipMemsetAsync(out_offs, 0, 8, st));
+        return AK_OK;
+    }
+    int rc = ws_reserve(w, a.n);
+    if (rc) return rc;
+    a.counts = w->counts;
+    a.flags = w->flags;
+    a.slow_list = w->slow_list;
+    a.slow_count = w->slow_count;
+    a.pool = w->pool;
+    a.out_offs = out_offs;
+    const uint64_t want = (a.n + ROW_BLOCK - 1) / ROW_BLOCK;
+    const unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)num_cus() * 8);
+    HIP_TRY(hipMemsetAsync(w->slow_count, 0, 4, st));
+    k_rows_fast<OP, FLAGS, false><<<grid, ROW_BLOCK, 0, st>>>(a);
+    k_rows_slow<OP, FLAGS, false><<<SLOW_THREADS / 64, 64, 0, st>>>(a);
+    rc = scan_counts(w, a.n, out_offs, st);
+    if (rc) return rc;
+    k_rows_fast<OP, FLAGS, true><<<grid, ROW_BLOCK, 0, st>>>(a);
+    k_rows_slow<OP, FLAGS, true><<<SLOW_THREADS / 64, 64, 0, st>>>(a);
+    HIP_TRY(hipGetLastError());
+    return AK_OK;
+}
+
+
+// per-op launchers (one TU each)
+int launch_normalize(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+int launch_segment(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+int launch_switches(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+int launch_bpe(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+int launch_spm(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+
+}  // namespace ak
+
+struct ak_ws : ak::AkWs {};

@@ -1,0 +1,170 @@
+// ak_model_build.h — host-side construction of the device model tables.
+//
+//  BPE  (HF models.BPE, tokenizer.py:96-97 / cli.py:276-299): an open-addressing hash of the
+//       merges, 8-byte entries {left << 16 | right, rank << 16 | new_id}, load factor <= 0.5;
+//       a direct single-char id table for U+0000..U+09FF plus a sorted list for the rest.
+//  SPM  (sentencepiece unigram, tokenizer.py:88-90 / cli.py:232-248): a double-array trie over
+//       the UTF-8 bytes of every NORMAL / USER_DEFINED / UNUSED piece, 16-byte nodes
+//       {check, base, value, 0} so one load serves one byte step.
+#pragma once
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace akb {
+
+constexpr uint32_t FAST_N = 0x0A00;
+
+struct BpeTables {
+    std::vector<uint64_t> tab;
+    uint32_t mask = 0;
+    std::vector<uint16_t> fast;     // FAST_N entries, 0xFFFF = not in vocab
+    std::vector<uint32_t> rest_cp;  // sorted, sentinel-terminated
+    std::vector<uint16_t> rest_id;
+    uint32_t n_rest = 0;
+};
+
+// returns "" on success, else an error message
+inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const uint32_t *single_id,
+                             uint32_t n_merges, const uint32_t *merges, BpeTables &t) {
+    if (n_merges >= 0xFFFFu) return "more than 65534 merges";
+    for (uint32_t i = 0; i < n_single; ++i)
+        if (single_id[i] >= 0xFFFFu) return "vocab id >= 65535";
+    for (uint64_t i = 0; i < 3ull * n_merges; ++i)
+        if (merges[i] >= 0xFFFFu) return "vocab id >= 65535";
+    uint32_t size = 1024;
+    while (size < 2u * n_merges + 16u) size <<= 1;
+    t.tab.assign(size, 0xFFFFFFFFull);
+    t.mask = size - 1;
+    for (uint32_t r = 0; r < n_merges; ++r) {
+        const uint32_t key = (merges[3 * r] << 16) | merges[3 * r + 1];
+        uint32_t h = (key * 0x9E3779B1u) & t.mask;
+        bool dup = false;
+        while ((uint32_t)t.tab[h] != 0xFFFFFFFFu) {
+            if ((uint32_t)t.tab[h] == key) { dup = true; break; }  // the lowest rank wins
+            h = (h + 1) & t.mask;
+        }
+        if (dup) continue;
+        t.tab[h] = (uint64_t)key | ((uint64_t)((r << 16) | merges[3 * r + 2]) << 32);
+    }
+    t.fast.assign(FAST_N, 0xFFFFu);
+    std::vector<std::pair<uint32_t, uint16_t>> rest;
+    for (uint32_t i = 0; i < n_single; ++i) {
+        if (single_cp[i] < FAST_N) t.fast[single_cp[i]] = (uint16_t)single_id[i];
+        else rest.emplace_back(single_cp[i], (uint16_t)single_id[i]);
+    }
+    std::sort(rest.begin(), rest.end());
+    t.rest_cp.assign(rest.size() + 1, 0xFFFFFFFFu);
+    t.rest_id.assign(rest.size() + 1, 0xFFFFu);
+    for (size_t i = 0; i < rest.size(); ++i) { t.rest_cp[i] = rest[i].first; t.rest_id[i] = rest[i].second; }
+    t.n_rest = (uint32_t)rest.size();
+    return "";
+}
+
+struct SpmTables {
+    std::vector<int> trie;  // 4 ints per node: check, base, value, 0
+    uint32_t n_nodes = 0;
+    float min_score = 0, max_score = 0;
+};
+
+// Double-array trie: node 0 is the root; the child of node s on byte b is t = base[s] + b + 1
+// with check[t] == s; value[t] = piece id | kind << 24 (kind 0 normal, 1 user, 2 unused) or -1.
+inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
+                             const uint8_t *types, SpmTables &out) {
+    if (n >= (1u << 24)) return "too many pieces";
+    float min_score = 3.4e38f, max_score = -3.4e38f;
+    struct P { std::string s; int val; };
+    std::vector<P> ps;
+    for (uint32_t i = 0; i < n; ++i) {
+        const int ty = types[i];
+        if (ty == 1) { min_score = std::min(min_score, scores[i]); max_score = std::max(max_score, scores[i]); }
+        if (ty != 1 && ty != 4 && ty != 5) continue;
+        const uint64_t a = piece_offs[i], b = piece_offs[i + 1];
+        if (b <= a) continue;
+        std::string s((const char *)piece_bytes + a, (size_t)(b - a));
+        // a piece holding U+2581 past its first char would break the per-word lattice split
+        if (s.find("\xe2\x96\x81", 1) != std::string::npos) return "piece with an inner U+2581";
+        const int kind = ty == 1 ? 0 : ty == 4 ? 1 : 2;
+        ps.push_back({s, (int)i | (kind << 24)});
+    }
+    std::sort(ps.begin(), ps.end(), [](const P &x, const P &y) { return x.s < y.s; });
+    struct N { std::vector<std::pair<int, int>> kids; int val = -1; };
+    std::vector<N> nodes(1);
+    for (const P &p : ps) {
+        int cur = 0;
+        for (unsigned char ch : p.s) {
+            int nxt = -1;
+            for (auto &kd : nodes[cur].kids)
+                if (kd.first == ch) { nxt = kd.second; break; }
+            if (nxt < 0) {
+                nxt = (int)nodes.size();
+                nodes[cur].kids.push_back({ch, nxt});
+                nodes.emplace_back();
+            }
+            cur = nxt;
+        }
+        if (nodes[cur].val < 0) nodes[cur].val = p.val;
+    }
+    std::vector<int> check, base, value;
+    std::vector<char> used_base;
+    auto grow = [&](size_t want) {
+        if (check.size() < want) {
+            const size_t m = std::max(want, check.size() * 2);
+            check.resize(m, -2);
+            base.resize(m, 0);
+            value.resize(m, -1);
+            used_base.resize(m, 0);
+        }
+    };
+    grow(1024);
+    std::vector<int> slot(nodes.size(), -1);
+    slot[0] = 0;
+    check[0] = -1;
+    int next_free = 1;
+    std::vector<int> queue{0};
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int u = queue[qi];
+        const int s = slot[u];
+        auto &kids = nodes[u].kids;
+        if (kids.empty()) continue;
+        std::sort(kids.begin(), kids.end());
+        int b = std::max(0, next_free - kids[0].first - 1);
+        for (;; ++b) {
+            grow((size_t)b + 258);
+            if (used_base[b]) continue;
+            bool ok = true;
+            for (auto &kd : kids)
+                if (check[b + kd.first + 1] != -2) { ok = false; break; }
+            if (ok) break;
+        }
+        used_base[b] = 1;
+        base[s] = b;
+        for (auto &kd : kids) {
+            const int t = b + kd.first + 1;
+            check[t] = s;
+            value[t] = nodes[kd.second].val;
+            slot[kd.second] = t;
+            queue.push_back(kd.second);
+        }
+        while (next_free < (int)check.size() && check[next_free] != -2) ++next_free;
+    }
+    size_t nn = check.size();
+    while (nn > 1 && check[nn - 1] == -2) --nn;
+    nn += 258;  // every base + byte + 1 probe stays in range
+    grow(nn);
+    out.trie.assign(4 * nn, 0);
+    for (size_t i = 0; i < nn; ++i) {
+        out.trie[4 * i] = check[i];
+        out.trie[4 * i + 1] = base[i];
+        out.trie[4 * i + 2] = value[i];
+    }
+    out.n_nodes = (uint32_t)nn;
+    out.min_score = min_score;
+    out.max_score = max_score;
+    return "";
+}
+
+}  // namespace akb

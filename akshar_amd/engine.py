@@ -1,0 +1,227 @@
+"""Batch API over device-resident packed rows (the engine's native data layout).
+
+Rows are packed UTF-8 in one uint8 tensor with int64 row offsets (offs[0] == 0), both on the
+GPU. Every call returns device tensors: a packed output plus int64 row offsets. Calls are
+enqueued on torch's current HIP stream; the capacity check reads out_offs[-1] back (one
+stream sync) and re-runs once with the exact size if the first estimate was short.
+
+This is the batched form of the reference's per-string API; the drop-in
+per-string classes in tokenizer.py / normalize.py / segment.py are thin wrappers over it.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import AK_NORM_CLEAN, AK_NORM_LOWER, AK_RAW, AksharError, check
+from .models import BPEModel, SPMModel
+
+_WS = {}
+
+
+def _device(dev=None):
+    if not torch.cuda.is_available():
+        raise AksharError("akshar_amd needs a ROCm GPU (torch.cuda.is_available() is False); there is no CPU path")
+    return torch.device("cuda", torch.cuda.current_device() if dev is None else dev)
+
+
+def workspace(dev=None):
+    d = _device(dev)
+    key = (d.index, torch.cuda.current_stream(d).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None:
+        with torch.cuda.device(d):
+            h = ctypes.c_void_p()
+            check(_lib.lib().ak_ws_create(ctypes.byref(h)), "ak_ws_create")
+        ws = h
+        _WS[key] = ws
+    return ws
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else ctypes.c_void_p(0)
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def flags_of(normalize_roman=True, clean_hinglish=True):
+    return (AK_NORM_LOWER if normalize_roman else 0) | (AK_NORM_CLEAN if clean_hinglish else 0)
+
+
+def pack_host(texts):
+    """list[str] -> (numpy u8 bytes padded to 16, numpy int64 offsets)."""
+    enc = [t.encode("utf-8", "surrogatepass") for t in texts]
+    offs = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        np.cumsum([len(e) for e in enc], out=offs[1:])
+    raw = b"".join(enc)
+    buf = np.zeros(((len(raw) + 15) // 16) * 16 + 16, dtype=np.uint8)
+    buf[:len(raw)] = np.frombuffer(raw, dtype=np.uint8)
+    return buf, offs
+
+
+def to_device(buf, offs, dev=None):
+    d = _device(dev)
+    b = torch.from_numpy(np.ascontiguousarray(buf)).to(d, non_blocking=False)
+    o = torch.from_numpy(np.ascontiguousarray(offs).astype(np.int64, copy=False)).to(d)
+    return b, o
+
+
+def pack(texts, dev=None):
+    """list[str] -> device (bytes uint8, offs int64)."""
+    return to_device(*pack_host(texts), dev=dev)
+
+
+def _check_inputs(buf, offs):
+    if buf.dtype != torch.uint8 or offs.dtype != torch.int64:
+        raise TypeError("rows must be uint8 bytes with int64 offsets")
+    if not (buf.is_cuda and offs.is_cuda):
+        raise TypeError("rows must be device tensors")
+    if not buf.is_contiguous() or not offs.is_contiguous():
+        raise TypeError("rows must be contiguous")
+    n = offs.numel() - 1
+    if n < 0:
+        raise ValueError("offs must have n+1 entries")
+    return n
+
+
+def _run(fn_call, n, cap, make_out, dev):
+    """Run a capacity-bounded op, re-running once with the exact size if needed."""
+    out_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    outs = make_out(cap)
+    fn_call(outs, cap, out_offs)
+    total = int(out_offs[-1].item())
+    if total > cap:
+        cap = total
+        outs = make_out(cap)
+        fn_call(outs, cap, out_offs)
+        total = int(out_offs[-1].item())
+    return outs, out_offs, total
+
+
+def normalize_batch(buf, offs, flags=3, row_status=None):
+    n = _check_inputs(buf, offs)
+    dev = buf.device
+    ws = workspace(dev.index)
+    nbytes = int(offs[-1].item()) if n else 0
+    cap = nbytes + 64 if flags & AK_NORM_CLEAN else int(_lib.lib().ak_normalize_cap(n, nbytes))
+
+    def call(out, c, oo):
+        check(_lib.lib().ak_normalize(ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
+                                      _ptr(row_status), _stream(dev)), "ak_normalize")
+
+    out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.uint8, device=dev), dev)
+    return out[:total], oo
+
+
+def segment_batch(buf, offs, flags=3, matras=False, row_status=None):
+    """flags=AK_RAW (-1) segments the raw rows; else normalizes with flags first."""
+    n = _check_inputs(buf, offs)
+    dev = buf.device
+    ws = workspace(dev.index)
+    nbytes = int(offs[-1].item()) if n else 0
+    cap = int(_lib.lib().ak_segment_cap(n, nbytes))
+
+    def call(out, c, oo):
+        check(_lib.lib().ak_segment(ws, flags, int(bool(matras)), _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
+                                    _ptr(row_status), _stream(dev)), "ak_segment")
+
+    out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev)
+    return out[:total], oo
+
+
+def switches_batch(buf, offs, flags=3, row_status=None):
+    n = _check_inputs(buf, offs)
+    dev = buf.device
+    ws = workspace(dev.index)
+    nbytes = int(offs[-1].item()) if n else 0
+    cap = int(_lib.lib().ak_segment_cap(n, nbytes))
+
+    def make(c):
+        return (torch.empty(max(c, 1), dtype=torch.int32, device=dev),
+                torch.empty(max(c, 1), dtype=torch.uint8, device=dev))
+
+    def call(out, c, oo):
+        check(_lib.lib().ak_switches(ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out[0]), _ptr(out[1]), c, _ptr(oo),
+                                     _ptr(row_status), _stream(dev)), "ak_switches")
+
+    (ends, labels), oo, total = _run(call, n, cap, make, dev)
+    return ends[:total], labels[:total], oo
+
+
+class BPE:
+    """Device-resident HF BPE model (models/akshar.json layout, cli.py:276-299)."""
+
+    def __init__(self, model, dev=None):
+        self.model = model if isinstance(model, BPEModel) else BPEModel(model)
+        self.dev = _device(dev)
+        m = self.model
+        h = ctypes.c_void_p()
+        merges = np.ascontiguousarray(m.merges, dtype=np.uint32)
+        with torch.cuda.device(self.dev):
+            check(_lib.lib().ak_bpe_create(len(m.single_cp), m.single_cp.ctypes.data, m.single_id.ctypes.data,
+                                           len(merges), merges.ctypes.data, m.bos, m.eos, ctypes.byref(h)),
+                  "ak_bpe_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            _lib.lib().ak_bpe_free(h)
+
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None):
+        n = _check_inputs(buf, offs)
+        dev = buf.device
+        ws = workspace(dev.index)
+        nbytes = int(offs[-1].item()) if n else 0
+        if cap is None:
+            cap = nbytes // 2 + 2 * n + 1024
+
+        def call(out, c, oo):
+            check(_lib.lib().ak_bpe_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
+                                           _ptr(row_status), _stream(dev)), "ak_bpe_encode")
+
+        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev)
+        return out[:total], oo
+
+
+class SPM:
+    """Device-resident SentencePiece unigram model (cli.py:232-248)."""
+
+    def __init__(self, model, dev=None):
+        self.model = model if isinstance(model, SPMModel) else SPMModel(model)
+        self.dev = _device(dev)
+        m = self.model
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.dev):
+            check(_lib.lib().ak_spm_create(len(m.pieces), m.piece_bytes.ctypes.data, m.piece_offs.ctypes.data,
+                                           m.scores.ctypes.data, m.types.ctypes.data, m.unk_id,
+                                           m.byte_ids.ctypes.data, ctypes.byref(h)), "ak_spm_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            _lib.lib().ak_spm_free(h)
+
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None):
+        n = _check_inputs(buf, offs)
+        dev = buf.device
+        ws = workspace(dev.index)
+        nbytes = int(offs[-1].item()) if n else 0
+        if cap is None:
+            cap = nbytes // 2 + 2 * n + 1024
+
+        def call(out, c, oo):
+            check(_lib.lib().ak_spm_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
+                                           _ptr(row_status), _stream(dev)), "ak_spm_encode")
+
+        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev)
+        return out[:total], oo
+
+
+__all__ = ["pack", "pack_host", "to_device", "normalize_batch", "segment_batch", "switches_batch", "BPE", "SPM",
+           "flags_of", "workspace", "AK_RAW"]

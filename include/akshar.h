@@ -1,0 +1,120 @@
+/*
+ * akshar.h — C-ABI of the MI355X batch tokenization engine (libakshar: akshar_amd/_akshar_hip.so).
+ *
+ * The reference (Bhasha-Open/Akshar, pure Python) has no FFI: its boundary is the Python API
+ * (src/akshar/tokenizer.py:18-288, src/akshar/__init__.py:12-109) plus a duck-typed engine seam
+ * `self.model.encode(str).ids` / `self.model.EncodeAsIds(str)` (tokenizer.py:153-156,190-193).
+ * Each entry point below replaces one reference interface, batched: rows are packed UTF-8 in one
+ * byte buffer with u64 row offsets, every output is a packed buffer plus u64 row offsets.
+ *
+ * Conventions
+ *  - Every call returns an int status (AK_OK or a negative AK_ERR_*); ak_last_error() returns a
+ *    thread-local message for the last failure on the calling thread.
+ *  - All array arguments of the batch calls are DEVICE pointers (hipMalloc / torch CUDA tensors)
+ *    on the current HIP device; `stream` is a hipStream_t (NULL = default stream). Batch calls
+ *    only enqueue work: results are valid after the stream is synchronized.
+ *  - Input: `in` holds offs[n] bytes (offs[0] == 0, offs non-decreasing). Each row is one string
+ *    of the reference API. The buffer must stay readable through offs[n] rounded up to 16 bytes (rows are
+ *    read in aligned 16-byte blocks).
+ *  - Output sizing: callers pass a capacity `cap` (elements). out_offs[0..n] is always written;
+ *    the total is out_offs[n]. If out_offs[n] > cap, the call still returns AK_OK but the output
+ *    elements are incomplete: re-run with cap >= out_offs[n] (the bound helpers below give caps
+ *    that are always sufficient).
+ *  - row_status (optional, u8[n], may be NULL): bit 0 = row had invalid UTF-8 (decoded as U+FFFD
+ *    per byte), bit 2 = row exceeded an engine limit (AK_LIMIT_* below; its output is empty).
+ *  - Models and workspaces are not thread-safe for concurrent calls on different streams with the
+ *    same workspace; models are immutable after creation and may be shared.
+ */
+#ifndef AKSHAR_H
+#define AKSHAR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AK_OK 0
+#define AK_ERR_ARG (-1)
+#define AK_ERR_HIP (-2)
+#define AK_ERR_UNSUPPORTED (-3)
+#define AK_ERR_NOMEM (-4)
+
+/* normalize_text flags (normalize.py:117 `normalize_text(text, normalize_roman, clean_hinglish)`) */
+#define AK_NORM_LOWER 1 /* normalize_roman=True: 'LATIN' in name(c) -> c.lower()  (normalize.py:21-45) */
+#define AK_NORM_CLEAN 2 /* clean_hinglish=True: allowlist filter + elongation collapse (:92-114) */
+#define AK_NORM_DEFAULT (AK_NORM_LOWER | AK_NORM_CLEAN)
+#define AK_RAW (-1)     /* segment/switches on the raw row (the free functions on unnormalized text) */
+
+/* per-row status bits */
+#define AK_ROW_BAD_UTF8 1u
+#define AK_ROW_LIMIT 4u
+
+/* engine limits (a row exceeding one gets AK_ROW_LIMIT and an empty output) */
+#define AK_LIMIT_SEGMENT 16384 /* code points in one NFC segment (a starter + its combining marks) */
+#define AK_LIMIT_WORD 16384    /* symbols in one BPE pre-token / chars in one SentencePiece word */
+
+typedef struct ak_bpe ak_bpe; /* device-resident BPE model (HF tokenizers models.BPE) */
+typedef struct ak_spm ak_spm; /* device-resident SentencePiece unigram model */
+typedef struct ak_ws ak_ws;   /* device scratch, grows on demand; one per stream */
+
+const char *ak_last_error(void);
+int ak_version(void);
+
+int ak_ws_create(ak_ws **out);
+void ak_ws_free(ak_ws *ws);
+
+/* Replaces Tokenizer.from_file(path) (tokenizer.py:96-97) for the model cli.py:276-299 trains:
+ * NFKC -> Whitespace -> BPE(unk_token=None) -> "<s> $A </s>".
+ * single_cp/single_id: the single-code-point vocab entries; merges: n_merges x {left, right, new}
+ * in rank order (rank = row index); bos/eos: the template's special ids. Host pointers. */
+int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const uint32_t *single_id,
+                  uint32_t n_merges, const uint32_t *merges, uint32_t bos, uint32_t eos, ak_bpe **out);
+void ak_bpe_free(ak_bpe *m);
+
+/* Replaces SentencePieceProcessor.Load(path) (tokenizer.py:88-90) for the unigram model
+ * cli.py:232-248 trains (identity normalizer, byte_fallback). pieces: n UTF-8 strings packed in
+ * piece_bytes with piece_offs[n+1]; scores float[n]; types u8[n] (sentencepiece_model.proto
+ * enum: 1 NORMAL 2 UNKNOWN 3 CONTROL 4 USER_DEFINED 5 UNUSED 6 BYTE); byte_ids[256]: ids of
+ * <0x00>..<0xFF>. Host pointers. */
+int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
+                  const uint8_t *types, int32_t unk_id, const int32_t *byte_ids, ak_spm **out);
+void ak_spm_free(ak_spm *m);
+
+/* normalize_text(text, normalize_roman, clean_hinglish) (normalize.py:117-148) per row.
+ * out: UTF-8 bytes; a sufficient cap is ak_normalize_cap(). */
+int ak_normalize(ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n, uint8_t *out,
+                 uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
+
+/* segment_akshars(text, matras) (segment.py:40-125) per row: cluster END indices (code points,
+ * relative to the row) of the normalized row (flags >= 0, as tokenize() without a model,
+ * tokenizer.py:144-151) or of the raw row (flags == AK_RAW). */
+int ak_segment(ak_ws *ws, int flags, int matras, const uint8_t *in, const uint64_t *offs, uint64_t n,
+               uint32_t *ends, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
+
+/* detect_code_switches(text) (segment.py:150-201) per row: run END indices (code points) and
+ * labels (0 other, 1 devanagari, 2 roman, 255 None = all-neutral row). */
+int ak_switches(ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n, uint32_t *ends,
+                uint8_t *labels, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
+
+/* aksharTokenizer(model, "bpe").encode(text) (tokenizer.py:167-193): normalize_text(flags) then
+ * the HF pipeline; ids include <s> ... </s>. flags must include AK_NORM_CLEAN. */
+int ak_bpe_encode(const ak_bpe *m, ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
+                  uint32_t *ids, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
+
+/* aksharTokenizer(model, "sentencepiece").encode(text) (tokenizer.py:167-193): normalize_text then
+ * EncodeAsIds (no bos/eos). */
+int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
+                  uint32_t *ids, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
+
+/* Always-sufficient output capacities (elements) for n rows of total_bytes input bytes. */
+uint64_t ak_normalize_cap(uint64_t n, uint64_t total_bytes);
+uint64_t ak_segment_cap(uint64_t n, uint64_t total_bytes);
+uint64_t ak_bpe_encode_cap(uint64_t n, uint64_t total_bytes);
+uint64_t ak_spm_encode_cap(uint64_t n, uint64_t total_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AKSHAR_H */

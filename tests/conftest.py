@@ -1,0 +1,36 @@
+import gzip
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.jsonl.gz")
+BPE_PATH = os.path.join(ROOT, "models", "akshar.json")
+SPM_PATH = os.path.join(ROOT, "models", "akshar.model")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built HIP engine")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with gzip.open(GOLDEN, "rt", encoding="utf-8") as f:
+        return [json.loads(line) for line in f]
+
+
+@pytest.fixture(scope="session")
+def bpe_model():
+    from akshar_amd.models import BPEModel
+    return BPEModel(BPE_PATH)
+
+
+@pytest.fixture(scope="session")
+def spm_model():
+    from akshar_amd.models import SPMModel
+    return SPMModel(SPM_PATH)

@@ -1,0 +1,134 @@
+// Host emulation of the engine's row kernels: ak_dev.h / ak_rows.h compiled by g++ with
+// AK_HOST_EMU, driven row by row exactly like k_rows_fast / k_rows_slow (count, scan, emit).
+// A debugging and CPU-test aid for the device pipeline code; never loaded by the product.
+#define AK_HOST_EMU 1
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../akshar_amd/csrc/ak_dev.h"
+#include "../../akshar_amd/csrc/ak_model_build.h"
+#include "../../akshar_amd/csrc/ak_rows.h"
+
+using namespace ak;
+
+struct EmuModel {
+    akb::BpeTables bpe;
+    akb::SpmTables spm;
+    BpeDev bdev{};
+    SpmDev sdev{};
+    std::vector<float> scores;
+    std::vector<int32_t> byte_ids;
+};
+
+extern "C" void *emu_bpe_create(uint32_t n_single, const uint32_t *cp, const uint32_t *id, uint32_t n_merges,
+                                const uint32_t *merges, uint32_t bos, uint32_t eos) {
+    EmuModel *m = new EmuModel();
+    if (!akb::build_bpe(n_single, cp, id, n_merges, merges, m->bpe).empty()) { delete m; return nullptr; }
+    m->bdev.merge_tab = m->bpe.tab.data();
+    m->bdev.tab_mask = m->bpe.mask;
+    m->bdev.single_sorted_cp = m->bpe.rest_cp.data();
+    m->bdev.single_sorted_id = m->bpe.rest_id.data();
+    m->bdev.n_single = m->bpe.n_rest;
+    m->bdev.bos = bos;
+    m->bdev.eos = eos;
+    return m;
+}
+
+extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t *offs, const float *scores,
+                                const uint8_t *types, int32_t unk_id, const int32_t *byte_ids) {
+    EmuModel *m = new EmuModel();
+    if (!akb::build_spm(n, bytes, offs, scores, types, m->spm).empty()) { delete m; return nullptr; }
+    m->scores.assign(scores, scores + n);
+    m->byte_ids.assign(byte_ids, byte_ids + 256);
+    m->sdev.trie = (const int4 *)m->spm.trie.data();
+    m->sdev.scores = m->scores.data();
+    m->sdev.byte_ids = m->byte_ids.data();
+    m->sdev.unk_id = unk_id;
+    m->sdev.unk_score = m->spm.min_score - 10.0f;
+    m->sdev.max_score = m->spm.max_score;
+    return m;
+}
+
+extern "C" void emu_free(void *m) { delete (EmuModel *)m; }
+
+template <int OP, int FLAGS>
+static int64_t run(RowArgs a) {
+    static uint2 fast[FAST_N];
+    for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
+    std::vector<uint32_t> seg(SLOW_SEG), dec(4 * SLOW_SEG), seg2(SLOW_SEG), dec2(4 * SLOW_SEG), wpair(SLOW_WORD), vchar(SLOW_WORD);
+    std::vector<uint16_t> wsym(SLOW_WORD);
+    std::vector<float> vbest(SLOW_WORD + 1);
+    std::vector<int32_t> vstart(SLOW_WORD + 1), vid(SLOW_WORD + 1);
+    auto scratch = [&](bool slow) {
+        Scratch sc;
+        sc.seg = seg.data(); sc.dec = dec.data(); sc.seg2 = seg2.data(); sc.dec2 = dec2.data(); sc.seg_cap = slow ? SLOW_SEG : FAST_SEG;
+        sc.wsym = wsym.data(); sc.wpair = wpair.data(); sc.word_cap = slow ? SLOW_WORD : FAST_WORD;
+        sc.vchar = vchar.data(); sc.vbest = vbest.data(); sc.vstart = vstart.data(); sc.vid = vid.data();
+        sc.vcap = slow ? SLOW_WORD : FAST_VCAP;
+        sc.slow_status = slow ? ST_LIMIT : ST_SLOW;
+        sc.status = 0;
+        return sc;
+    };
+    std::vector<uint64_t> cnt(a.n), oo(a.n + 1);
+    std::vector<int> mode(a.n);
+    for (uint64_t r = 0; r < a.n; ++r) {
+        Scratch sc = scratch(false);
+        uint64_t c = process_row<OP, FLAGS, false>(a, r, fast, a.single_fast, &sc);
+        mode[r] = 0;
+        if (sc.status & ST_SLOW) {
+            Scratch s2 = scratch(true);
+            c = process_row<OP, FLAGS, false>(a, r, fast, a.single_fast, &s2);
+            mode[r] = (s2.status & ST_LIMIT) ? 2 : 1;
+            if (mode[r] == 2) c = 0;
+        }
+        cnt[r] = c;
+    }
+    oo[0] = 0;
+    for (uint64_t r = 0; r < a.n; ++r) oo[r + 1] = oo[r] + cnt[r];
+    uint64_t *out_offs = (uint64_t *)a.out_offs;
+    memcpy(out_offs, oo.data(), (a.n + 1) * 8);
+    for (uint64_t r = 0; r < a.n; ++r) {
+        if (mode[r] == 2) continue;
+        Scratch sc = scratch(mode[r] == 1);
+        (void)process_row<OP, FLAGS, true>(a, r, fast, a.single_fast, &sc);
+    }
+    return (int64_t)oo[a.n];
+}
+
+template <int OP>
+static int64_t dispatch(int flags, RowArgs a) {
+    switch (flags) {
+        case -1: if constexpr (OP == OP_SEGMENT || OP == OP_SWITCHES) return run<OP, -1>(a); break;
+        case 0: return run<OP, 0>(a);
+        case 1: return run<OP, 1>(a);
+        case 2: return run<OP, 2>(a);
+        case 3: return run<OP, 3>(a);
+    }
+    return -1;
+}
+
+// op: 0 normalize, 1 segment, 2 switches, 3 bpe, 4 spm
+extern "C" int64_t emu_run(int op, int flags, int matras, void *model, const uint8_t *in, const uint64_t *offs,
+                           uint64_t n, void *out, uint8_t *labels, uint64_t cap, uint64_t *out_offs) {
+    RowArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in = in; a.offs = offs; a.n = n; a.out = out; a.labels = labels; a.cap = cap; a.out_offs = out_offs;
+    a.matras = matras;
+    EmuModel *m = (EmuModel *)model;
+    if (m) {
+        a.bpe = m->bdev;
+        a.single_fast = m->bpe.fast.empty() ? nullptr : m->bpe.fast.data();
+        a.spm = m->sdev;
+    }
+    switch (op) {
+        case 0: return dispatch<OP_NORMALIZE>(flags, a);
+        case 1: return dispatch<OP_SEGMENT>(flags, a);
+        case 2: return dispatch<OP_SWITCHES>(flags, a);
+        case 3: return dispatch<OP_BPE>(flags, a);
+        case 4: return dispatch<OP_SPM>(flags, a);
+    }
+    return -1;
+}

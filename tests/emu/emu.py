@@ -1,0 +1,73 @@
+"""ctypes wrapper of the host emulation of the device row pipeline (tests only)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+P = ctypes.c_void_p
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        so = os.path.join(HERE, "_emu.so")
+        srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
+                                                   ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h")]
+        if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
+            subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", so, srcs[0]], cwd=HERE)
+        L = ctypes.CDLL(so)
+        L.emu_bpe_create.restype = P
+        L.emu_bpe_create.argtypes = [ctypes.c_uint32, P, P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint32]
+        L.emu_spm_create.restype = P
+        L.emu_spm_create.argtypes = [ctypes.c_uint32, P, P, P, P, ctypes.c_int32, P]
+        L.emu_free.argtypes = [P]
+        L.emu_run.restype = ctypes.c_int64
+        L.emu_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_uint64, P, P,
+                              ctypes.c_uint64, P]
+        _L = L
+    return _L
+
+
+def pad(buf):
+    b = np.zeros(((len(buf) + 15) // 16) * 16 + 16, dtype=np.uint8)
+    b[:len(buf)] = buf
+    return b
+
+
+class Model:
+    def __init__(self, bpe=None, spm=None):
+        L = lib()
+        if bpe is not None:
+            mg = np.ascontiguousarray(bpe.merges, dtype=np.uint32)
+            self.h = L.emu_bpe_create(len(bpe.single_cp), bpe.single_cp.ctypes.data, bpe.single_id.ctypes.data,
+                                      len(mg), mg.ctypes.data, bpe.bos, bpe.eos)
+        else:
+            m = spm
+            self.h = L.emu_spm_create(len(m.pieces), m.piece_bytes.ctypes.data, m.piece_offs.ctypes.data,
+                                      m.scores.ctypes.data, m.types.ctypes.data, m.unk_id, m.byte_ids.ctypes.data)
+        assert self.h
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().emu_free(self.h)
+
+
+def run(op, flags, buf, offs, model=None, matras=False):
+    """op: 0 normalize, 1 segment, 2 switches, 3 bpe, 4 spm -> (out, [labels], out_offs)."""
+    buf = pad(buf)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    n = len(offs) - 1
+    cap = int(offs[-1]) * 3 + 4 * n + 64
+    dt = np.uint8 if op == 0 else np.uint32
+    out = np.zeros(cap, dtype=dt)
+    labels = np.zeros(cap, dtype=np.uint8)
+    oo = np.zeros(n + 1, dtype=np.uint64)
+    tot = lib().emu_run(op, flags, int(matras), model.h if model else None, buf.ctypes.data, offs.ctypes.data, n,
+                        out.ctypes.data, labels.ctypes.data, cap, oo.ctypes.data)
+    assert 0 <= tot <= cap, tot
+    if op == 2:
+        return out[:tot], labels[:tot], oo
+    return out[:tot], oo

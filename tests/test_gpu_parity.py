@@ -1,0 +1,142 @@
+"""GPU parity: the HIP engine (through its C-ABI) against the golden vectors and the oracle.
+
+Bit-exact for everything (bytes, indices, token ids). Sizes: the full golden set, then seeded
+synthetic corpora at sizes the oracle finishes in seconds, then a size-independent property
+check at a larger batch (engine == oracle on a 200k-row Hinglish batch, checked row by row).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.util import NORM_KEYS, SEG_KEYS, SW_KEYS, ends_to_lens, rows_ints, rows_runs, rows_u8
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from akshar_amd import engine
+    assert torch.cuda.is_available()
+    return engine
+
+
+@pytest.fixture(scope="module")
+def gpacked(golden, eng):
+    return eng.pack([r["text"] for r in golden])
+
+
+def _cpu(t):
+    return t.cpu().numpy()
+
+
+def _bad(golden, key, got):
+    return [(r["set"], r["i"], r["text"], g, r[key]) for r, g in zip(golden, got) if g != r[key]][:5]
+
+
+@pytest.mark.parametrize("flags,key", NORM_KEYS)
+def test_normalize_golden(golden, gpacked, eng, flags, key):
+    out, oo = eng.normalize_batch(*gpacked, flags=flags)
+    assert _bad(golden, key, rows_u8(_cpu(out), _cpu(oo))) == []
+
+
+@pytest.mark.parametrize("flags,matras,key", SEG_KEYS)
+def test_segment_golden(golden, gpacked, eng, flags, matras, key):
+    ends, oo = eng.segment_batch(*gpacked, flags=flags, matras=matras)
+    got = [ends_to_lens(e) for e in rows_ints(_cpu(ends), _cpu(oo))]
+    assert _bad(golden, key, got) == []
+
+
+@pytest.mark.parametrize("flags,key", SW_KEYS)
+def test_switches_golden(golden, gpacked, eng, flags, key):
+    ends, labels, oo = eng.switches_batch(*gpacked, flags=flags)
+    assert _bad(golden, key, rows_runs(_cpu(ends), _cpu(labels), _cpu(oo))) == []
+
+
+def test_bpe_golden(golden, gpacked, eng, bpe_model):
+    ids, oo = eng.BPE(bpe_model).encode_batch(*gpacked)
+    assert _bad(golden, "bpe", rows_ints(_cpu(ids), _cpu(oo))) == []
+
+
+def test_spm_golden(golden, gpacked, eng, spm_model):
+    ids, oo = eng.SPM(spm_model).encode_batch(*gpacked)
+    assert _bad(golden, "spm", rows_ints(_cpu(ids), _cpu(oo))) == []
+
+
+def _synth(kind, n, seed):
+    from akshar_amd import synth
+    return synth.generate(kind, n, seed=seed)
+
+
+def _to_dev(eng, buf, offs):
+    pad = np.zeros(((len(buf) + 15) // 16) * 16 + 16, dtype=np.uint8)
+    pad[:len(buf)] = buf
+    return eng.to_device(pad, offs.astype(np.int64))
+
+
+@pytest.mark.parametrize("kind,n,seed", [(0, 20000, 7), (1, 20000, 8), (2, 20000, 9)])
+def test_synthetic_vs_oracle(eng, bpe_model, spm_model, kind, n, seed):
+    buf, offs = _synth(kind, n, seed)
+    gb, go = _to_dev(eng, buf, offs)
+    ob = (buf if len(buf) else np.zeros(1, np.uint8), offs)
+    for flags in (3, 0):
+        out, oo = eng.normalize_batch(gb, go, flags=flags)
+        ref, ro = O.normalize_batch(*ob, flags=flags)
+        assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+        assert np.array_equal(_cpu(out), ref)
+    for flags, matras in ((3, False), (-1, False), (-1, True)):
+        ends, oo = eng.segment_batch(gb, go, flags=flags, matras=matras)
+        ref, ro = O.segment_batch(*ob, flags=flags, matras=matras)
+        assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+        assert np.array_equal(_cpu(ends).astype(np.uint32), ref)
+    ends, labels, oo = eng.switches_batch(gb, go, flags=3)
+    re_, rl, ro = O.switches_batch(*ob, flags=3)
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+    assert np.array_equal(_cpu(ends).astype(np.uint32), re_) and np.array_equal(_cpu(labels), rl)
+    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(*ob)
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+    assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(*ob)
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+    assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
+
+
+def test_empty_batch_and_empty_rows(eng, bpe_model, spm_model):
+    gb, go = eng.pack([])
+    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go)
+    assert oo.numel() == 1 and int(oo[0]) == 0 and ids.numel() == 0
+    gb, go = eng.pack(["", "", "  "])
+    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go)
+    assert rows_ints(_cpu(ids), _cpu(oo)) == [[2, 3], [2, 3], [2, 3]]
+    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
+    assert rows_ints(_cpu(ids), _cpu(oo)) == [[], [], []]
+
+
+def test_long_rows_take_the_slow_path(eng, bpe_model, spm_model):
+    texts = ["क" + "्क" * 200, "a" + "́" * 300 + "b", "x" * 5000, "abcdefghij" * 50,
+             "१२३४५६७८९०" * 30, "ज्ञ" * 100 + " " + "hello " * 100]
+    gb, go = eng.pack(texts)
+    ob = O.pack(texts)
+    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(*ob)
+    assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
+    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(*ob)
+    assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
+    out, oo = eng.normalize_batch(gb, go, flags=0)
+    ref, ro = O.normalize_batch(*ob, flags=0)
+    assert rows_u8(_cpu(out), _cpu(oo)) == rows_u8(ref, ro)
+
+
+def test_large_batch_property(eng, bpe_model):
+    """200k Hinglish rows: engine == oracle row by row; total ids == sum of row counts."""
+    buf, offs = _synth(1, 200000, 1234)
+    gb, go = _to_dev(eng, buf, offs)
+    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    oo = _cpu(oo).astype(np.uint64)
+    assert oo[-1] == len(ref) == ids.numel()
+    assert np.array_equal(oo, ro)
+    assert np.array_equal(_cpu(ids).astype(np.uint32), ref)

@@ -232,12 +232,14 @@ def main():
         f.write(" *                allowed:1 lower_changes:1\n")
         f.write(" * Record word 1: norm_map:16 decomp_len:3 decomp_idx:13\n */\n")
         f.write("#pragma once\n#include <stdint.h>\n\n")
+        f.write("/* AK_UT_QUAL: storage qualifier (host: static const; HIP device: __device__ static const) */\n")
+        f.write("#ifndef AK_UT_QUAL\n#define AK_UT_QUAL static const\n#endif\n\n")
         f.write("#define AK_UT_BLOCK %d\n#define AK_UT_NBLOCKS %d\n#define AK_UT_NREC %d\n"
                 "#define AK_UT_NDECOMP %d\n#define AK_UT_NCOMP %d\n\n"
                 % (BLK, len(blk_list), len(recs), len(dec_flat), len(comp_keys)))
 
         def arr(ctype, name, vals, per=16):
-            f.write("static const %s %s[%d] = {\n" % (ctype, name, len(vals)))
+            f.write("AK_UT_QUAL %s %s[%d] = {\n" % (ctype, name, len(vals)))
             for i in range(0, len(vals), per):
                 f.write("  " + ",".join(str(v) for v in vals[i:i + per]) + ",\n")
             f.write("};\n\n")
