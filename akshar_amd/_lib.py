@@ -14,6 +14,7 @@ AK_NORM_CLEAN = 2
 AK_RAW = -1
 AK_ROW_BAD_UTF8 = 1
 AK_ROW_LIMIT = 4
+AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4}
 
 P = ctypes.c_void_p
 U64 = ctypes.c_uint64
@@ -37,6 +38,9 @@ SIGNATURES = {
     "ak_switches": (I32, [P, I32, P, P, U64, P, P, U64, P, P, P]),
     "ak_bpe_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
     "ak_spm_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
+    "ak_profile_enable": (I32, [I32]),
+    "ak_profile_read": (I32, [I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
+    "ak_profile_reset": (None, []),
     "ak_normalize_cap": (U64, [U64, U64]),
     "ak_segment_cap": (U64, [U64, U64]),
     "ak_bpe_encode_cap": (U64, [U64, U64]),

@@ -475,6 +475,7 @@ struct SwitchSink {
 struct BpeDev {
     const uint64_t *merge_tab;  // open addressing: lo32 = left << 16 | right, hi32 = rank << 16 | new
     uint32_t tab_mask;
+    uint32_t tab_shift;
     const uint32_t *single_sorted_cp;  // for code points >= FAST_N
     const uint16_t *single_sorted_id;
     uint32_t n_single;
@@ -483,7 +484,7 @@ struct BpeDev {
 
 __device__ __forceinline__ uint32_t merge_lookup(const BpeDev &m, uint32_t a, uint32_t b) {
     const uint32_t key = (a << 16) | b;
-    uint32_t h = (key * 0x9E3779B1u) & m.tab_mask;
+    uint32_t h = (key * 0x9E3779B1u) >> m.tab_shift;
     for (;;) {
         const uint64_t e = m.merge_tab[h];  // L2-resident table (plain load: keep it cached)
         const uint32_t k = (uint32_t)e;

@@ -44,6 +44,65 @@ int ak::set_hip_error(const char *expr, hipError_t e) {
 static int fail(int code, const char *msg) { return ak::set_error(code, msg); }
 
 extern "C" const char *ak_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------------------
+// built-in profiler
+
+bool ak::g_prof_on = false;
+
+namespace {
+struct ProfRec { int kernel; hipEvent_t start, stop; };
+std::vector<ProfRec> g_prof_pending;
+hipEvent_t g_prof_open[AK_PROF_NKERNELS] = {};
+double g_prof_ms[AK_PROF_NKERNELS] = {};
+uint64_t g_prof_n[AK_PROF_NKERNELS] = {};
+}  // namespace
+
+void ak::prof_mark(int k, bool end, hipStream_t st) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    (void)hipEventRecord(e, st);
+    if (!end) {
+        g_prof_open[k] = e;
+    } else if (g_prof_open[k]) {
+        g_prof_pending.push_back({k, g_prof_open[k], e});
+        g_prof_open[k] = nullptr;
+    } else {
+        (void)hipEventDestroy(e);
+    }
+}
+
+static void prof_drain() {
+    for (auto &r : g_prof_pending) {
+        float ms = 0.0f;
+        if (hipEventSynchronize(r.stop) == hipSuccess && hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess) {
+            g_prof_ms[r.kernel] += ms;
+            g_prof_n[r.kernel] += 1;
+        }
+        (void)hipEventDestroy(r.start);
+        (void)hipEventDestroy(r.stop);
+    }
+    g_prof_pending.clear();
+}
+
+extern "C" int ak_profile_enable(int on) {
+    ak::g_prof_on = on != 0;
+    return AK_OK;
+}
+
+extern "C" void ak_profile_reset(void) {
+    prof_drain();
+    for (int k = 0; k < AK_PROF_NKERNELS; ++k) { g_prof_ms[k] = 0; g_prof_n[k] = 0; }
+}
+
+extern "C" int ak_profile_read(int kernel, double *total_ms, uint64_t *launches) {
+    if (kernel < 0 || kernel >= AK_PROF_NKERNELS || !total_ms || !launches)
+        return fail(AK_ERR_ARG, "ak_profile_read: bad argument");
+    prof_drain();
+    *total_ms = g_prof_ms[kernel];
+    *launches = g_prof_n[kernel];
+    return AK_OK;
+}
 extern "C" int ak_version(void) { return 1; }
 
 // ------------------------------------------------------------------------------------------
@@ -84,6 +143,7 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     HIP_TRY(hipMemcpy(m->d_single_id, t.rest_id.data(), t.rest_id.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     m->dev.merge_tab = m->d_tab;
     m->dev.tab_mask = t.mask;
+    m->dev.tab_shift = t.shift;
     m->dev.single_sorted_cp = m->d_single_cp;
     m->dev.single_sorted_id = m->d_single_id;
     m->dev.n_single = t.n_rest;

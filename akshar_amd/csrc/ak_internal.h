@@ -41,6 +41,12 @@ struct AkWs {
     SlowPool pool{};
 };
 
+// built-in kernel timing (include/akshar.h ak_profile_*): HIP events around every launch
+extern bool g_prof_on;
+void prof_mark(int kernel, bool end, hipStream_t st);
+#define AK_PROF(k, end, st) \
+    do { if (ak::g_prof_on) ak::prof_mark((k), (end), (st)); } while (0)
+
 int ws_reserve(AkWs *w, uint64_t n);
 int scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st);
 int num_cus();
@@ -151,12 +157,22 @@ inline int launch_rows(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_t st) {
     const uint64_t want = (a.n + ROW_BLOCK - 1) / ROW_BLOCK;
     const unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)num_cus() * 8);
     HIP_TRY(hipMemsetAsync(w->slow_count, 0, 4, st));
+    AK_PROF(AK_PROF_COUNT, false, st);
     k_rows_fast<OP, FLAGS, false><<<grid, ROW_BLOCK, 0, st>>>(a);
+    AK_PROF(AK_PROF_COUNT, true, st);
+    AK_PROF(AK_PROF_COUNT_SLOW, false, st);
     k_rows_slow<OP, FLAGS, false><<<SLOW_THREADS / 64, 64, 0, st>>>(a);
+    AK_PROF(AK_PROF_COUNT_SLOW, true, st);
+    AK_PROF(AK_PROF_SCAN, false, st);
     rc = scan_counts(w, a.n, out_offs, st);
     if (rc) return rc;
+    AK_PROF(AK_PROF_SCAN, true, st);
+    AK_PROF(AK_PROF_EMIT, false, st);
     k_rows_fast<OP, FLAGS, true><<<grid, ROW_BLOCK, 0, st>>>(a);
+    AK_PROF(AK_PROF_EMIT, true, st);
+    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
     k_rows_slow<OP, FLAGS, true><<<SLOW_THREADS / 64, 64, 0, st>>>(a);
+    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
     HIP_TRY(hipGetLastError());
     return AK_OK;
 }

@@ -21,6 +21,7 @@ constexpr uint32_t FAST_N = 0x0A00;
 struct BpeTables {
     std::vector<uint64_t> tab;
     uint32_t mask = 0;
+    uint32_t shift = 0;  // slot = (key * 0x9E3779B1) >> shift: the product's HIGH bits
     std::vector<uint16_t> fast;     // FAST_N entries, 0xFFFF = not in vocab
     std::vector<uint32_t> rest_cp;  // sorted, sentinel-terminated
     std::vector<uint16_t> rest_id;
@@ -39,9 +40,11 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
     while (size < 2u * n_merges + 16u) size <<= 1;
     t.tab.assign(size, 0xFFFFFFFFull);
     t.mask = size - 1;
+    t.shift = 32;
+    for (uint32_t s = size; s > 1; s >>= 1) --t.shift;
     for (uint32_t r = 0; r < n_merges; ++r) {
         const uint32_t key = (merges[3 * r] << 16) | merges[3 * r + 1];
-        uint32_t h = (key * 0x9E3779B1u) & t.mask;
+        uint32_t h = (key * 0x9E3779B1u) >> t.shift;
         bool dup = false;
         while ((uint32_t)t.tab[h] != 0xFFFFFFFFu) {
             if ((uint32_t)t.tab[h] == key) { dup = true; break; }  // the lowest rank wins

@@ -172,11 +172,12 @@ class BPE:
         if h:
             _lib.lib().ak_bpe_free(h)
 
-    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None):
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None):
         n = _check_inputs(buf, offs)
         dev = buf.device
         ws = workspace(dev.index)
-        nbytes = int(offs[-1].item()) if n else 0
+        if nbytes is None:
+            nbytes = int(offs[-1].item()) if n else 0
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
 
@@ -207,11 +208,12 @@ class SPM:
         if h:
             _lib.lib().ak_spm_free(h)
 
-    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None):
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None):
         n = _check_inputs(buf, offs)
         dev = buf.device
         ws = workspace(dev.index)
-        nbytes = int(offs[-1].item()) if n else 0
+        if nbytes is None:
+            nbytes = int(offs[-1].item()) if n else 0
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
 
@@ -225,3 +227,22 @@ class SPM:
 
 __all__ = ["pack", "pack_host", "to_device", "normalize_batch", "segment_batch", "switches_batch", "BPE", "SPM",
            "flags_of", "workspace", "AK_RAW"]
+
+
+def profile_enable(on=True):
+    _lib.lib().ak_profile_enable(1 if on else 0)
+
+
+def profile_reset():
+    _lib.lib().ak_profile_reset()
+
+
+def profile_read():
+    """{kernel class: (total device ms, launches)} since the last reset (synchronizes)."""
+    res = {}
+    for name, k in _lib.AK_PROF.items():
+        ms = ctypes.c_double()
+        n = ctypes.c_uint64()
+        check(_lib.lib().ak_profile_read(k, ctypes.byref(ms), ctypes.byref(n)), "ak_profile_read")
+        res[name] = (ms.value, n.value)
+    return res

@@ -108,6 +108,19 @@ int ak_bpe_encode(const ak_bpe *m, ak_ws *ws, int flags, const uint8_t *in, cons
 int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
                   uint32_t *ids, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
 
+/* Built-in kernel timing: when enabled, every batch call records HIP events around each of its
+ * kernel launches on the caller's stream; ak_profile_read synchronizes the pending events and
+ * returns the accumulated device time and launch count of one kernel class. */
+#define AK_PROF_COUNT 0      /* fast count pass (one lane per row) */
+#define AK_PROF_COUNT_SLOW 1 /* slow-path count pass (rows over the fast buffers) */
+#define AK_PROF_SCAN 2       /* row counts -> row offsets (three small kernels) */
+#define AK_PROF_EMIT 3       /* fast emit pass */
+#define AK_PROF_EMIT_SLOW 4  /* slow-path emit pass */
+#define AK_PROF_NKERNELS 5
+int ak_profile_enable(int on);
+int ak_profile_read(int kernel, double *total_ms, uint64_t *launches);
+void ak_profile_reset(void);
+
 /* Always-sufficient output capacities (elements) for n rows of total_bytes input bytes. */
 uint64_t ak_normalize_cap(uint64_t n, uint64_t total_bytes);
 uint64_t ak_segment_cap(uint64_t n, uint64_t total_bytes);

@@ -29,6 +29,7 @@ extern "C" void *emu_bpe_create(uint32_t n_single, const uint32_t *cp, const uin
     if (!akb::build_bpe(n_single, cp, id, n_merges, merges, m->bpe).empty()) { delete m; return nullptr; }
     m->bdev.merge_tab = m->bpe.tab.data();
     m->bdev.tab_mask = m->bpe.mask;
+    m->bdev.tab_shift = m->bpe.shift;
     m->bdev.single_sorted_cp = m->bpe.rest_cp.data();
     m->bdev.single_sorted_id = m->bpe.rest_id.data();
     m->bdev.n_single = m->bpe.n_rest;

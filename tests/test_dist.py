@@ -1,0 +1,73 @@
+"""Multi-process sharding + reassembly on CPU (gloo, world_size 2): the N > 1 path of bench.py
+and akshar_amd.dist, checked against the single-process result (oracle ids)."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from akshar_amd import dist as adist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from akshar_amd import synth
+        from akshar_amd.models import BPEModel
+        from oracle import oracle as O
+        from tests.conftest import BPE_PATH
+        buf, offs = synth.generate(synth.KIND_HINGLISH, 3000, seed=5)
+        r0, r1 = adist.shard_rows(offs.astype(np.int64), world, rank)
+        sub_offs = (offs[r0:r1 + 1] - offs[r0]).astype(np.uint64)
+        sub = buf[int(offs[r0]):int(offs[r1])]
+        ids, oo = O.OracleBPE(BPEModel(BPE_PATH)).encode_batch(sub if len(sub) else np.zeros(1, np.uint8), sub_offs)
+        all_ids, all_offs = adist.gather_ids(torch.from_numpy(ids.astype(np.int32)),
+                                             torch.from_numpy(oo.astype(np.int64)))
+        q.put((rank, r0, r1, all_ids.numpy(), all_offs.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_rows_balanced_and_complete():
+    offs = np.cumsum([0] + [10, 200, 5, 5, 5, 300, 1, 1, 1, 1]).astype(np.int64)
+    for world in (1, 2, 3, 4, 8):
+        cuts = [adist.shard_rows(offs, world, r) for r in range(world)]
+        assert cuts[0][0] == 0 and cuts[-1][1] == len(offs) - 1
+        assert all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
+
+
+def test_gloo_world2_gather_matches_single_process():
+    from akshar_amd import synth
+    from akshar_amd.models import BPEModel
+    from oracle import oracle as O
+    from tests.conftest import BPE_PATH
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    buf, offs = synth.generate(synth.KIND_HINGLISH, 3000, seed=5)
+    ref_ids, ref_offs = O.OracleBPE(BPEModel(BPE_PATH)).encode_batch(buf, offs)
+    res.sort()
+    assert res[0][2] == res[1][1] and 0 < res[0][2] < 3000
+    for _, _, _, ids, oo in res:
+        assert np.array_equal(ids.astype(np.uint32), ref_ids)
+        assert np.array_equal(oo.astype(np.uint64), ref_offs)
