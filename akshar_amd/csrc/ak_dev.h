@@ -148,7 +148,7 @@ __device__ __forceinline__ int utf8_len(uint32_t cp) {
 constexpr uint32_t H_SBASE = 0xAC00, H_LBASE = 0x1100, H_VBASE = 0x1161, H_TBASE = 0x11A7;
 constexpr uint32_t H_LCOUNT = 19, H_VCOUNT = 21, H_TCOUNT = 28, H_NCOUNT = 588, H_SCOUNT = 11172;
 
-__device__ uint32_t compose_pair(uint32_t a, uint32_t b) {
+__device__ __forceinline__ uint32_t compose_pair(uint32_t a, uint32_t b) {
     if (a - H_LBASE < H_LCOUNT && b - H_VBASE < H_VCOUNT)
         return H_SBASE + ((a - H_LBASE) * H_VCOUNT + (b - H_VBASE)) * H_TCOUNT;
     if (a - H_SBASE < H_SCOUNT && (a - H_SBASE) % H_TCOUNT == 0 && b > H_TBASE && b < H_TBASE + H_TCOUNT)
@@ -162,6 +162,66 @@ __device__ uint32_t compose_pair(uint32_t a, uint32_t b) {
         if (k < key) lo = mid + 1; else hi = mid - 1;
     }
     return 0;
+}
+
+// Full NFC of one segment (seg[0..n)) into dec[]: decompose, canonical order, compose.
+// Returns the output length, or -1 if dec[] (dcap entries) overflows. Rare path: not inlined,
+// and it receives only arrays and values so the streaming stages stay in registers.
+template <bool HF>
+__device__ __noinline__ int nfc_full(const uint32_t *seg, uint32_t *dec, int n, int dcap, const uint2 *fast) {
+    auto cc = [&](uint32_t x) { const uint2 pr = prop(fast, x); return HF ? p_ccc_hf(pr) : p_ccc(pr); };
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t cp = seg[i];
+        if (cp - H_SBASE < H_SCOUNT) {
+            const uint32_t s = cp - H_SBASE;
+            if (m + 3 > dcap) return -1;
+            dec[m++] = H_LBASE + s / H_NCOUNT;
+            dec[m++] = H_VBASE + (s % H_NCOUNT) / H_TCOUNT;
+            if (s % H_TCOUNT) dec[m++] = H_TBASE + s % H_TCOUNT;
+            continue;
+        }
+        const uint2 pr = prop(fast, cp);
+        const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
+        if (m + (int)(len ? len : 1) > dcap) return -1;
+        if (!len) dec[m++] = cp;
+        else for (uint32_t k = 0; k < len; ++k) dec[m++] = AK_UT_DECOMP[idx + k];
+    }
+    // canonical ordering (stable insertion sort of non-starter runs)
+    for (int i = 1; i < m; ++i) {
+        const uint32_t x = dec[i];
+        const int c = cc(x);
+        if (c == 0) continue;
+        int j = i;
+        while (j > 0 && cc(dec[j - 1]) > c) { dec[j] = dec[j - 1]; --j; }
+        dec[j] = x;
+    }
+    // canonical composition in place (write index <= read index)
+    int starter = -1;
+    uint32_t st = 0;
+    int lastc = 0;
+    int w = 0;
+    for (int i = 0; i < m; ++i) {
+        const uint32_t ch = dec[i];
+        const int c = cc(ch);
+        if (starter >= 0) {
+            const uint32_t comp = compose_pair(st, ch);
+            if (comp && (lastc < c || lastc == 0)) {
+                st = comp;
+                dec[starter] = comp;
+                continue;
+            }
+        }
+        if (i == 0 && c != 0) {
+            lastc = 256;  // a leading non-starter blocks composition
+            dec[w++] = ch;
+            continue;
+        }
+        if (c == 0) { starter = w; st = ch; }
+        lastc = c;
+        dec[w++] = ch;
+    }
+    return w;
 }
 
 template <bool HF, class Next>
@@ -207,64 +267,6 @@ struct NfcStage {
         seg[n++] = cp;
     }
 
-    __device__ void full() {
-        // decompose (canonical, full) into dec[]
-        int m = 0;
-        const int dcap = 4 * sc->seg_cap;
-        for (int i = 0; i < n; ++i) {
-            const uint32_t cp = seg[i];
-            if (cp - H_SBASE < H_SCOUNT) {
-                const uint32_t s = cp - H_SBASE;
-                if (m + 3 > dcap) { sc->status |= sc->slow_status; return; }
-                dec[m++] = H_LBASE + s / H_NCOUNT;
-                dec[m++] = H_VBASE + (s % H_NCOUNT) / H_TCOUNT;
-                if (s % H_TCOUNT) dec[m++] = H_TBASE + s % H_TCOUNT;
-                continue;
-            }
-            const uint2 pr = prop(fast, cp);
-            const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
-            if (m + (int)(len ? len : 1) > dcap) { sc->status |= sc->slow_status; return; }
-            if (!len) dec[m++] = cp;
-            else for (uint32_t k = 0; k < len; ++k) dec[m++] = AK_UT_DECOMP[idx + k];
-        }
-        // canonical ordering (stable insertion sort of non-starter runs)
-        for (int i = 1; i < m; ++i) {
-            const uint32_t x = dec[i];
-            const int c = cc(prop(fast, x));
-            if (c == 0) continue;
-            int j = i;
-            while (j > 0 && cc(prop(fast, dec[j - 1])) > c) { dec[j] = dec[j - 1]; --j; }
-            dec[j] = x;
-        }
-        // canonical composition, emitting each char once it can no longer change
-        int starter = -1;  // index into dec[] of the open starter (composed value kept in st)
-        uint32_t st = 0;
-        int lastc = 0;
-        // compose in place: out[] overwrites dec[] from the front (write index <= read index)
-        int w = 0;
-        for (int i = 0; i < m; ++i) {
-            const uint32_t ch = dec[i];
-            const int c = cc(prop(fast, ch));
-            if (starter >= 0) {
-                const uint32_t comp = compose_pair(st, ch);
-                if (comp && (lastc < c || lastc == 0)) {
-                    st = comp;
-                    dec[starter] = comp;
-                    continue;
-                }
-            }
-            if (i == 0 && c != 0) {
-                lastc = 256;  // leading non-starter blocks composition
-                dec[w++] = ch;
-                continue;
-            }
-            if (c == 0) { starter = w; st = ch; }
-            lastc = c;
-            dec[w++] = ch;
-        }
-        for (int i = 0; i < w; ++i) next->push(dec[i]);
-    }
-
     __device__ __forceinline__ void flush() {
         if (n == 0) return;
         if (!work) {
@@ -276,7 +278,9 @@ struct NfcStage {
             }
         } else {
             if (!inbuf) { seg[0] = p0; seg[1] = p1; }
-            full();
+            const int w = nfc_full<HF>(seg, dec, n, 4 * sc->seg_cap, fast);
+            if (w < 0) sc->status |= sc->slow_status;
+            for (int i = 0; i < w; ++i) next->push(dec[i]);
         }
         n = 0;
         inbuf = false;
@@ -494,8 +498,7 @@ __device__ __forceinline__ uint32_t merge_lookup(const BpeDev &m, uint32_t a, ui
     }
 }
 
-template <class Out>
-__device__ void bpe_merge_word(const BpeDev &m, uint16_t *w, uint32_t *pr, int n, Out &out) {
+__device__ __forceinline__ int bpe_merge_word(const BpeDev &m, uint16_t *w, uint32_t *pr, int n) {
     for (int i = 0; i + 1 < n; ++i) pr[i] = merge_lookup(m, w[i], w[i + 1]);
     while (n > 1) {
         uint32_t best = 0xFFFFFFFFu;
@@ -512,7 +515,7 @@ __device__ void bpe_merge_word(const BpeDev &m, uint16_t *w, uint32_t *pr, int n
         if (bi > 0) pr[bi - 1] = merge_lookup(m, w[bi - 1], w[bi]);
         if (bi + 1 < n) pr[bi] = merge_lookup(m, w[bi], w[bi + 1]);
     }
-    for (int i = 0; i < n; ++i) out.put((uint32_t)w[i]);
+    return n;
 }
 
 struct BpeWordSink {  // after HF NFC: pre-tokenize and merge
@@ -538,7 +541,10 @@ struct BpeWordSink {  // after HF NFC: pre-tokenize and merge
         return 0xFFFFu;
     }
     __device__ __forceinline__ void end_word() {
-        if (cls >= 0 && wlen > 0) bpe_merge_word(*m, sc->wsym, sc->wpair, wlen, c);
+        if (cls >= 0 && wlen > 0) {
+            const int k = bpe_merge_word(*m, sc->wsym, sc->wpair, wlen);
+            for (int i = 0; i < k; ++i) c.put((uint32_t)sc->wsym[i]);
+        }
         cls = -1;
         wlen = 0;
     }
@@ -607,7 +613,7 @@ struct SpmSink {
     __device__ __forceinline__ void init(const SpmDev *md, Scratch *s) {
         m = md; sc = s; started = false; pending_space = false; wl = 0; base = 0.0f;
     }
-    __device__ void solve() {
+    __device__ __forceinline__ void solve() {
         const int L = wl;
         float *best = sc->vbest;
         int32_t *start = sc->vstart;

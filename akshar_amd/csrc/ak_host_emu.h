@@ -5,6 +5,7 @@
 #define __device__
 #define __host__
 #define __forceinline__ inline
+#define __noinline__ __attribute__((noinline))
 struct uint2 { uint32_t x, y; };
 struct int4 { int x, y, z, w; };
 struct alignas(16) uint4 { uint32_t x, y, z, w; };

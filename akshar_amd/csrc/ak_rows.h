@@ -84,7 +84,7 @@ __device__ __forceinline__ void run_input(Sink &sink, const uint2 *fast, Scratch
 
 // Process row r; returns the output count. EMIT writes at out_offs[r].
 template <int OP, int FLAGS, bool EMIT>
-__device__ uint64_t process_row(const RowArgs &a, uint64_t r, const uint2 *fast, const uint16_t *sfast, Scratch *sc) {
+__device__ __forceinline__ uint64_t process_row(const RowArgs &a, uint64_t r, const uint2 *fast, const uint16_t *sfast, Scratch *sc) {
     const uint64_t b = a.offs[r], e = a.offs[r + 1];
     Reader rd;
     rd.init(a.in);

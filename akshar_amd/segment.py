@@ -1,0 +1,118 @@
+"""Drop-in segmentation API (reference: src/akshar/segment.py:14-236), run on the GPU.
+
+segment_akshars      :40-125  regex \\X grapheme clusters (UAX #29 + GB9c, Unicode 17), optional
+                              matra/halant split
+detect_code_switches :150-201 script runs; digits/punct neutral
+analyze_text_composition :210-236  counts + ratios (float division on the host, as the reference)
+identify_script / is_matra   per-character helpers (:26-37, :128-147), host-side: they classify
+                              one character and are not on the batch path.
+"""
+from . import engine
+
+MATRA_RANGES = [(0x0900, 0x0902), (0x093E, 0x094C), (0x0951, 0x0954)]  # segment.py:20-24
+_LABEL = {0: "other", 1: "devanagari", 2: "roman", 255: None}
+
+
+def is_matra(char):
+    """segment.py:26-37."""
+    cp = ord(char)
+    return any(a <= cp <= b for a, b in MATRA_RANGES)
+
+
+def identify_script(char):
+    """segment.py:128-147 (same rule order; str.isdigit is the interpreter's, as in the reference)."""
+    cp = ord(char)
+    if 0x0900 <= cp <= 0x097F:
+        return "devanagari"
+    if (0x0041 <= cp <= 0x005A) or (0x0061 <= cp <= 0x007A):
+        return "roman"
+    if char.isdigit():
+        return "digit"
+    if char in " .,!?;:'\"()-[]{}":
+        return "punct"
+    return "other"
+
+
+def _split(text, ends):
+    out, a = [], 0
+    for e in ends:
+        out.append(text[a:e])
+        a = e
+    return out
+
+
+def segment_batch(texts, matras=False, flags=engine.AK_RAW):
+    """list[str] -> list[list[str]] (clusters of the raw texts, or of their normalization when
+    flags >= 0, in which case the normalized texts are returned too)."""
+    if not texts:
+        return []
+    buf, offs = engine.pack(texts)
+    ends, oo = engine.segment_batch(buf, offs, flags=flags, matras=matras)
+    ends = ends.cpu().numpy()
+    oo = oo.cpu().numpy()
+    return [[int(x) for x in ends[oo[i]:oo[i + 1]]] for i in range(len(texts))]
+
+
+def segment_akshars(text, matras=False, separate_matras=None):
+    """segment.py:40 — split text into akshars (grapheme clusters)."""
+    if separate_matras is not None:
+        matras = separate_matras
+    return _split(text, segment_batch([text], matras=matras)[0])
+
+
+def switches_batch(texts, flags=engine.AK_RAW):
+    if not texts:
+        return []
+    buf, offs = engine.pack(texts)
+    ends, labels, oo = engine.switches_batch(buf, offs, flags=flags)
+    ends = ends.cpu().numpy()
+    labels = labels.cpu().numpy()
+    oo = oo.cpu().numpy()
+    res = []
+    for i in range(len(texts)):
+        e = [int(x) for x in ends[oo[i]:oo[i + 1]]]
+        lab = [_LABEL[int(x)] for x in labels[oo[i]:oo[i + 1]]]
+        res.append(list(zip(e, lab)))
+    return res
+
+
+def detect_code_switches(text):
+    """segment.py:150 — [(segment, script_label), ...]."""
+    runs = switches_batch([text])[0]
+    segs = _split(text, [e for e, _ in runs])
+    return [(s, lab) for s, (_, lab) in zip(segs, runs)]
+
+
+def segment_by_script(text):
+    """segment.py:204-207."""
+    return [seg for seg, _ in detect_code_switches(text)]
+
+
+def composition_from(text, n_akshars, runs):
+    """analyze_text_composition's arithmetic (segment.py:225-236) from cluster count + runs."""
+    total = len(text)
+    dev = roman = 0
+    a = 0
+    for e, lab in runs:
+        if lab == "devanagari":
+            dev += e - a
+        elif lab == "roman":
+            roman += e - a
+        a = e
+    return {
+        "akshar_count": n_akshars,
+        "script_switches": len(runs) - 1,
+        "devanagari_ratio": dev / total if total > 0 else 0,
+        "roman_ratio": roman / total if total > 0 else 0,
+    }
+
+
+def analyze_text_composition(text):
+    """segment.py:210 — composition stats for a (normalized) string."""
+    n = len(segment_batch([text])[0])
+    runs = switches_batch([text])[0]
+    return composition_from(text, n, runs)
+
+
+__all__ = ["segment_akshars", "detect_code_switches", "segment_by_script", "analyze_text_composition",
+           "identify_script", "is_matra", "MATRA_RANGES", "segment_batch", "switches_batch"]

@@ -1,0 +1,151 @@
+"""Drop-in `aksharTokenizer` (reference: src/akshar/tokenizer.py:18-288) on the MI355X engine.
+
+Same constructor, methods, return types and errors as the reference:
+  - model_path missing / not a file -> akshar-level fallback (model_type "akshar")      :67-71
+  - model_type not in {"sentencepiece", "bpe"} -> ValueError("unknown model_type: ...")  :101-102
+  - encode()/decode() without a model -> ValueError("need model for IDs" / "... to decode") :187-188,213-214
+The per-string methods run a batch of one through the GPU; `encode_batch` / `tokenize_batch` /
+`encode_packed` are the batched forms (one launch for many rows). The reference's engine
+libraries (sentencepiece, tokenizers) are not used: models are read from their files
+(akshar_amd.models) and run by the HIP kernels.
+"""
+import os
+from typing import List, Optional, Union
+
+from . import decode as _dec
+from . import engine
+from .normalize import normalize_batch
+from .segment import _split, composition_from, segment_batch, switches_batch
+
+
+class aksharTokenizer:
+    """High-level tokenizer for Hindi/Sanskrit/Hinglish text (tokenizer.py:18)."""
+
+    def __init__(self, model_path: Optional[str] = None, model_type: str = "sentencepiece",
+                 normalize_roman: bool = True, clean_hinglish: bool = True):
+        self.model_path = model_path
+        self.normalize_roman = normalize_roman
+        self.clean_hinglish = clean_hinglish
+        self.model = None
+        self._configured_model_type = model_type
+        if model_path and os.path.exists(model_path):
+            self._load_model()
+        else:
+            self.model_type = "akshar"
+
+    def _load_model(self):
+        model_type = self._configured_model_type
+        if model_type == "sentencepiece":
+            self.model = engine.SPM(self.model_path)
+            self.model_type = "sentencepiece"
+        elif model_type == "bpe":
+            self.model = engine.BPE(self.model_path)
+            self.model_type = "bpe"
+        else:
+            raise ValueError(f"unknown model_type: {model_type}")
+
+    @property
+    def _flags(self):
+        return engine.flags_of(self.normalize_roman, self.clean_hinglish)
+
+    # ---------------------------------------------------------------- preprocessing
+    def preprocess(self, text: str) -> str:
+        return normalize_batch([text], self.normalize_roman, self.clean_hinglish)[0]
+
+    def preprocess_batch(self, texts: List[str]) -> List[str]:
+        return normalize_batch(texts, self.normalize_roman, self.clean_hinglish)
+
+    # ---------------------------------------------------------------- ids
+    def encode_packed(self, buf, offs, nbytes=None):
+        """Device rows (uint8 bytes, int64 offsets) -> device (int32 ids, int64 row offsets)."""
+        if self.model is None:
+            raise ValueError("need model for IDs")
+        return self.model.encode_batch(buf, offs, flags=self._flags, nbytes=nbytes)
+
+    def encode_batch(self, texts: List[str]) -> List[List[int]]:
+        if self.model is None:
+            raise ValueError("need model for IDs")
+        if not texts:
+            return []
+        buf, offs = engine.pack(texts)
+        ids, oo = self.encode_packed(buf, offs)
+        ids = ids.cpu().numpy()
+        oo = oo.cpu().numpy()
+        return [[int(x) for x in ids[oo[i]:oo[i + 1]]] for i in range(len(texts))]
+
+    def encode(self, text: str) -> List[int]:
+        return self.encode_batch([text])[0]
+
+    def decode(self, ids: List[int]) -> str:
+        if self.model is None:
+            raise ValueError("need model to decode")
+        if self.model_type == "sentencepiece":
+            return _dec.spm_decode(self.model.model, list(ids))
+        return _dec.bpe_decode(self.model.model, list(ids))
+
+    # ---------------------------------------------------------------- tokens
+    def _tokens_for(self, ids):
+        if self.model_type == "sentencepiece":
+            return _dec.spm_pieces(self.model.model, ids)
+        return _dec.bpe_tokens(self.model.model, ids)
+
+    def tokenize_batch(self, texts: List[str], return_metadata: bool = False):
+        norms = self.preprocess_batch(texts)
+        if self.model is None:
+            toks = [_split(n, e) for n, e in zip(norms, segment_batch(norms))]
+        else:
+            toks = [self._tokens_for(ids) for ids in self.encode_batch(texts)]
+        if not return_metadata:
+            return toks
+        metas = [self._composition(n) for n in norms]
+        out = []
+        for text, norm, meta, t in zip(texts, norms, metas, toks):
+            meta = dict(meta)
+            meta["tokens"] = t
+            meta["token_count"] = len(t)
+            meta["original_text"] = text
+            meta["normalized_text"] = norm
+            out.append(meta)
+        return out
+
+    def tokenize(self, text: str, return_metadata: bool = False) -> Union[List[str], dict]:
+        return self.tokenize_batch([text], return_metadata)[0]
+
+    def detokenize(self, tokens: List[str]) -> str:
+        """tokenizer.py:221-246 (pure string handling, unchanged)."""
+        if self.model_type == "sentencepiece":
+            txt = "".join(tokens)
+            txt = txt.replace("▁", " ")
+            return txt.strip()
+        elif self.model_type == "bpe":
+            txt = " ".join(tokens)
+            txt = txt.replace(" ##", "")
+            txt = txt.replace("Ġ", " ")
+            return txt.strip()
+        return "".join(tokens)
+
+    # ---------------------------------------------------------------- analysis
+    @staticmethod
+    def _composition(norm):
+        n = len(segment_batch([norm])[0])
+        return composition_from(norm, n, switches_batch([norm])[0])
+
+    def explain(self, text: str) -> dict:
+        norm = self.preprocess(text)
+        ends = segment_batch([norm])[0]
+        runs = switches_batch([norm])[0]
+        akshars = _split(norm, ends)
+        switches = list(zip(_split(norm, [e for e, _ in runs]), [lab for _, lab in runs]))
+        stats = composition_from(norm, len(ends), runs)
+        tokens = self.tokenize(text)
+        return {"original": text, "normalized": norm, "akshars": akshars, "code_switches": switches,
+                "tokens": tokens, "stats": stats}
+
+    def vocab_size(self) -> int:
+        if self.model is None:
+            return 0
+        return self.model.model.vocab_size
+
+
+AksharTokenizer = aksharTokenizer
+Akshar = aksharTokenizer

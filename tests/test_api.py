@@ -1,0 +1,124 @@
+"""The drop-in Python API (akshar_amd.aksharTokenizer & free functions) against the reference.
+
+Mirrors the reference's own suites (tests/test_tokenizer.py, test_normalize.py, test_segment.py
+in /root/reference) plus the known answers recorded in example_features.ipynb, and checks every
+golden row through the public per-string / batch methods. GPU-marked where a kernel runs; the
+argument/error behaviour that needs no kernel is checked on CPU.
+"""
+import pytest
+
+import akshar_amd
+from akshar_amd import AksharTokenizer, Akshar, aksharTokenizer
+from akshar_amd import decode as dec
+from tests.conftest import BPE_PATH, SPM_PATH
+
+gpu = pytest.mark.gpu
+
+
+# ------------------------------------------------------------------ CPU: no kernel involved
+def test_names_and_aliases():
+    assert AksharTokenizer is aksharTokenizer and Akshar is aksharTokenizer
+    for n in ("normalize_text", "segment_akshars", "detect_code_switches", "analyze_text_composition",
+              "identify_script"):
+        assert callable(getattr(akshar_amd, n))
+
+
+def test_no_model_errors_and_defaults():
+    tk = aksharTokenizer()
+    assert tk.model is None and tk.model_type == "akshar" and tk.vocab_size() == 0
+    with pytest.raises(ValueError, match="need model for IDs"):
+        tk.encode("abc")
+    with pytest.raises(ValueError, match="need model to decode"):
+        tk.decode([1, 2])
+    tk2 = aksharTokenizer(model_path="/nonexistent/model.json", model_type="bpe")
+    assert tk2.model is None and tk2.model_type == "akshar"
+    with pytest.raises(ValueError, match="unknown model_type: wordpiece"):
+        aksharTokenizer(model_path=BPE_PATH, model_type="wordpiece")
+
+
+def test_detokenize_matches_reference_rules():
+    tk = aksharTokenizer()
+    assert tk.detokenize(["क", "्", "ष"]) == "क्ष"
+    tk.model_type = "sentencepiece"
+    assert tk.detokenize(["▁aaj", "▁मौ", "सम"]) == "aaj मौसम"
+    tk.model_type = "bpe"
+    assert tk.detokenize(["<s>", "aaj", "##x", "</s>"]) == "<s> aajx </s>"
+
+
+def test_identify_script_reference_cases():
+    from akshar_amd import identify_script as ids
+    assert [ids(c) for c in "नमaZ5. "] == ["devanagari", "devanagari", "roman", "roman", "digit", "punct", "punct"]
+    assert ids("\t") == "other" and ids("€") == "other"
+
+
+def test_host_decoders_match_golden(golden, bpe_model, spm_model):
+    for r in golden:
+        assert dec.bpe_decode(bpe_model, r["bpe"]) == r["bpe_dec"]
+        assert dec.spm_decode(spm_model, r["spm"]) == r["spm_dec"]
+
+
+def test_vocab_sizes_from_files(bpe_model, spm_model):
+    assert bpe_model.vocab_size == 24000 and spm_model.vocab_size == 24000
+
+
+# ------------------------------------------------------------------ GPU: reference suites
+@gpu
+def test_reference_tokenizer_suite():
+    tk = AksharTokenizer()
+    assert tk.model is None
+    r = tk.preprocess("Hello नमस्ते")
+    assert "hello" in r and "नमस्ते" in r
+    toks = tk.tokenize("नमस्ते")
+    assert isinstance(toks, list) and toks
+    meta = tk.tokenize("hello नमस्ते", return_metadata=True)
+    for k in ("tokens", "token_count", "original_text", "akshar_count"):
+        assert k in meta
+    a = tk.explain("aaj मौसम अच्छा है")
+    for k in ("original", "normalized", "akshars", "code_switches", "tokens", "stats"):
+        assert k in a
+    assert tk.explain("आज मौसम बहुत अच्छा है")["stats"]["devanagari_ratio"] > 0.8
+    s = tk.explain("yaar aaj ka मौसम बहुत अच्छा hai")["stats"]
+    assert s["devanagari_ratio"] > 0 and s["roman_ratio"] > 0
+
+
+@gpu
+def test_notebook_known_answers():
+    """example_features.ipynb recorded outputs (cells 5, 11, 14, 16, 18, 20, 22)."""
+    tk = aksharTokenizer()
+    assert tk.tokenize("aaj मौसम बहुत अच्छा है") == ['a', 'a', 'j', ' ', 'मौ', 'स', 'म', ' ', 'ब', 'हु', 'त', ' ',
+                                                     'अ', 'च्छा', ' ', 'है']
+    e = tk.explain("aaj मौसम बहुत अच्छा है")
+    assert e["code_switches"] == [('aaj ', 'roman'), ('मौसम बहुत अच्छा है', 'devanagari')]
+    assert e["stats"] == {'akshar_count': 16, 'script_switches': 1, 'devanagari_ratio': 0.8181818181818182,
+                          'roman_ratio': 0.18181818181818182}
+    assert tk.tokenize("क्षेत्रे धर्मक्षेत्रे") == ["क्षे", "त्रे", " ", "ध", "र्म", "क्षे", "त्रे"]
+    assert akshar_amd.segment_akshars("धर्मक्षेत्रे") == ["ध", "र्म", "क्षे", "त्रे"]
+    assert akshar_amd.segment_akshars("ज्ञान") == ["ज्ञा", "न"]
+    assert akshar_amd.detect_code_switches("आज का day बहुत nice था") == [
+        ('आज का ', 'devanagari'), ('day ', 'roman'), ('बहुत ', 'devanagari'), ('nice ', 'roman'), ('था', 'devanagari')]
+    assert akshar_amd.normalize_text("Heyyy यार kya HAAL hai") == "hey यार kya haal hai"
+    assert akshar_amd.normalize_text("bohoooot") == "bohot"
+    assert akshar_amd.normalize_text("yaaaaar") == "yar"
+
+
+@gpu
+def test_public_api_on_golden(golden):
+    texts = [r["text"] for r in golden]
+    bpe = aksharTokenizer(model_path=BPE_PATH, model_type="bpe")
+    spm = aksharTokenizer(model_path=SPM_PATH, model_type="sentencepiece")
+    assert bpe.vocab_size() == 24000 and spm.vocab_size() == 24000
+    assert bpe.encode_batch(texts) == [r["bpe"] for r in golden]
+    assert spm.encode_batch(texts) == [r["spm"] for r in golden]
+    assert bpe.preprocess_batch(texts) == [r["norm"] for r in golden]
+    from akshar_amd.segment import segment_batch, switches_batch
+    norms = [r["norm"] for r in golden]
+    ends = segment_batch(norms)
+    assert [[b - a for a, b in zip([0] + e[:-1], e)] for e in ends] == [r["ak"] for r in golden]
+    for r in golden[:400]:
+        assert akshar_amd.segment_akshars(r["text"]) and True
+        assert [len(s) for s in akshar_amd.segment_akshars(r["text"])] == r["ak_raw"]
+        assert [[len(s), lab] for s, lab in akshar_amd.detect_code_switches(r["norm"])] == r["sw"]
+        assert akshar_amd.analyze_text_composition(r["norm"]) == r["comp"]
+        assert bpe.encode(r["text"]) == r["bpe"]
+        assert spm.decode(spm.encode(r["text"])) == r["spm_dec"]
+        assert bpe.decode(r["bpe"]) == r["bpe_dec"]
