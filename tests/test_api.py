@@ -115,7 +115,6 @@ def test_public_api_on_golden(golden):
     ends = segment_batch(norms)
     assert [[b - a for a, b in zip([0] + e[:-1], e)] for e in ends] == [r["ak"] for r in golden]
     for r in golden[:400]:
-        assert akshar_amd.segment_akshars(r["text"]) and True
         assert [len(s) for s in akshar_amd.segment_akshars(r["text"])] == r["ak_raw"]
         assert [[len(s), lab] for s, lab in akshar_amd.detect_code_switches(r["norm"])] == r["sw"]
         assert akshar_amd.analyze_text_composition(r["norm"]) == r["comp"]
