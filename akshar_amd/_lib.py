@@ -14,7 +14,7 @@ AK_NORM_CLEAN = 2
 AK_RAW = -1
 AK_ROW_BAD_UTF8 = 1
 AK_ROW_LIMIT = 4
-AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4}
+AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4, "tiles": 5}
 
 P = ctypes.c_void_p
 U64 = ctypes.c_uint64
@@ -29,6 +29,8 @@ SIGNATURES = {
     "ak_version": (I32, []),
     "ak_ws_create": (I32, [ctypes.POINTER(P)]),
     "ak_ws_free": (None, [P]),
+    "ak_ws_set_tiling": (I32, [P, I32, I32]),
+    "ak_ws_check": (I32, [P]),
     "ak_bpe_create": (I32, [U32, P, P, U32, P, U32, U32, ctypes.POINTER(P)]),
     "ak_bpe_free": (None, [P]),
     "ak_spm_create": (I32, [U32, P, P, P, P, ctypes.c_int32, P, ctypes.POINTER(P)]),

@@ -220,8 +220,26 @@ extern "C" int ak_ws_create(ak_ws **out) {
     return AK_OK;
 }
 
+extern "C" int ak_ws_set_tiling(ak_ws *w, int bpe_path, int tile_rows) {
+    if (!w || bpe_path < 0 || bpe_path > 1 || tile_rows < 1 || tile_rows > 16)
+        return fail(AK_ERR_ARG, "ak_ws_set_tiling: bpe_path in {0,1}, tile_rows in [1,16]");
+    w->bpe_path = bpe_path;
+    w->tile_rows = tile_rows;
+    return AK_OK;
+}
+
+extern "C" int ak_ws_check(ak_ws *w) {
+    if (!w) return fail(AK_ERR_ARG, "null workspace");
+    if (!w->tile_misc) return AK_OK;
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, w->tile_misc + 1, 4, hipMemcpyDeviceToHost));
+    return err ? fail(AK_ERR_HIP, "tile look-back gave up waiting (device timeout)") : AK_OK;
+}
+
 extern "C" void ak_ws_free(ak_ws *w) {
     if (!w) return;
+    (void)hipFree(w->tile_status);
+    (void)hipFree(w->tile_misc);
     (void)hipFree(w->counts);
     (void)hipFree(w->flags);
     (void)hipFree(w->slow_list);
@@ -355,7 +373,8 @@ static int dispatch(int op, int flags, ak_ws *w, const RowArgs &a, uint64_t *out
         case OP_NORMALIZE: return launch_normalize(flags, w, a, out_offs, st);
         case OP_SEGMENT: return launch_segment(flags, w, a, out_offs, st);
         case OP_SWITCHES: return launch_switches(flags, w, a, out_offs, st);
-        case OP_BPE: return launch_bpe(flags, w, a, out_offs, st);
+        case OP_BPE:
+            return w->bpe_path == 1 ? launch_bpe_tiles(flags, w, a, out_offs, st) : launch_bpe(flags, w, a, out_offs, st);
         default: return launch_spm(flags, w, a, out_offs, st);
     }
 }

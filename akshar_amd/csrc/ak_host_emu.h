@@ -12,3 +12,10 @@ struct alignas(16) uint4 { uint32_t x, y, z, w; };
 static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 static inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
 static inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
+#define __HIP_MEMORY_SCOPE_AGENT 0
+template <class T>
+static inline T __hip_atomic_exchange(T *p, T v, int, int) { return __atomic_exchange_n(p, v, __ATOMIC_SEQ_CST); }
+template <class T>
+static inline void __hip_atomic_store(T *p, T v, int, int) { __atomic_store_n(p, v, __ATOMIC_SEQ_CST); }
+template <class T>
+static inline T __hip_atomic_load(const T *p, int, int) { return __atomic_load_n(p, __ATOMIC_SEQ_CST); }

@@ -39,6 +39,12 @@ struct AkWs {
     uint64_t cap_blocks = 0;
     void *pool_mem = nullptr;
     SlowPool pool{};
+    // tile-cooperative BPE path
+    uint64_t *tile_status = nullptr;
+    uint64_t cap_tiles = 0;
+    uint32_t *tile_misc = nullptr;  // [0] ticket, [1] err, [64..64+SLOW_THREADS) pool locks
+    int tile_rows = 8;
+    int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (v1)
 };
 
 // built-in kernel timing (include/akshar.h ak_profile_*): HIP events around every launch
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_rows_fast(RowArgs a) {
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
         if (EMIT && a.flags[r] != 0) continue;
         sc.status = 0;
-        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc);
+        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc, EMIT ? a.out_offs[r] : 0);
         if (!EMIT) {
             const bool slow = (sc.status & ST_SLOW) != 0;
             a.counts[r] = slow ? 0u : (uint32_t)cnt;
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(64) void k_rows_slow(RowArgs a) {
         const uint64_t r = a.slow_list[i];
         if (EMIT && a.flags[r] != 1) continue;
         sc.status = 0;
-        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc);
+        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc, EMIT ? a.out_offs[r] : 0);
         if (!EMIT) {
             const bool lim = (sc.status & ST_LIMIT) != 0;
             a.counts[r] = lim ? 0u : (uint32_t)cnt;
@@ -183,6 +189,7 @@ int launch_normalize(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, h
 int launch_segment(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_switches(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_bpe(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_spm(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 
 }  // namespace ak

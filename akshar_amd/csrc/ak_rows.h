@@ -84,11 +84,12 @@ __device__ __forceinline__ void run_input(Sink &sink, const uint2 *fast, Scratch
 
 // Process row r; returns the output count. EMIT writes at out_offs[r].
 template <int OP, int FLAGS, bool EMIT>
-__device__ __forceinline__ uint64_t process_row(const RowArgs &a, uint64_t r, const uint2 *fast, const uint16_t *sfast, Scratch *sc) {
+__device__ __forceinline__ uint64_t process_row(const RowArgs &a, uint64_t r, const uint2 *fast, const uint16_t *sfast,
+                                               Scratch *sc, uint64_t emit_base) {
     const uint64_t b = a.offs[r], e = a.offs[r + 1];
     Reader rd;
     rd.init(a.in);
-    const uint64_t base = EMIT ? a.out_offs[r] : 0;
+    const uint64_t base = EMIT ? emit_base : 0;
     if constexpr (OP == OP_NORMALIZE) {
         Utf8Sink s;
         s.c = Cursor<uint8_t>{(uint8_t *)a.out, base, a.cap, EMIT};

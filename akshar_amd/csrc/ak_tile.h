@@ -1,0 +1,574 @@
+// ak_tile.h — tile-cooperative BPE encode (the bench path).
+//
+// One wave64 owns one tile of R consecutive rows at a time. The tile's bytes are staged into LDS
+// with coalesced 16-byte loads, then the wave runs the reference pipeline as data-parallel passes
+// over LDS arrays (positions on lanes, ballot / prefix-sum compaction between passes):
+//   D  decode + NFC + normalize_text map/filter       bytes -> V (u16 code points, row sentinels)
+//      (NFC segments whose marks could change are resolved by their leader lane with nfc_full)
+//   E  remove_elongations (runs >= 3, '\n' exempt)    V -> W
+//   H  HF NFKC: compat spaces -> ' ', HF-ccc segments checked by their leader
+//   P  Whitespace pre-tokenizer: word starts -> V, word-end tags on W, spaces -> DEAD
+//   B  lane per word: cps -> ids, merge_all (lowest rank, leftmost) in place in W
+//   F  weighted compaction W -> ids (B -> <s>, E -> </s>), decoupled look-back for the tile's
+//      output base, row offsets written from the sentinels' positions
+// Rows that cannot take the cooperative path (invalid UTF-8, an NFC segment over T_SEG code points,
+// a changed HF segment, or bytes beyond the tile buffer) run the sequential row pipeline
+// (ak_dev.h, process_row) in one lane of the same wave, so every row is computed exactly once.
+// Reference semantics: normalize.py:117-148, tokenizer.py:167-193, cli.py:276-299.
+#pragma once
+#include "ak_dev.h"
+#include "ak_rows.h"
+#include "ak_wave.h"
+
+namespace ak {
+
+constexpr int T_BCAP = 2048;  // staged bytes per tile (rows past it fall back)
+constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
+constexpr int T_E = T_BCAP + 2 * T_MAXR + 64;
+constexpr int T_SEG = 16;     // NFC segment length handled in the cooperative pass
+constexpr int T_TPB = 8;      // tiles per ticket
+constexpr int T_FBSEG = 16;   // fallback lane buffers (private); larger rows use the locked pool
+constexpr int T_FBWORD = 64;
+
+constexpr uint16_t V_FB = 0xFFFC;    // B sentinel of a fallback row (weight = its token count)
+constexpr uint16_t V_DEAD = 0xFFFD;
+constexpr uint16_t V_B = 0xFFFE;
+constexpr uint16_t V_E = 0xFFFF;
+constexpr uint16_t V_SPECIAL = 0xFFFC;  // values >= this are sentinels / dead
+constexpr uint16_t WEND = 0x8000;       // word-end tag on a code point (all are <= U+3000)
+
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_MASK = (1ull << 62) - 1;
+
+struct TileWaveMem {
+    alignas(16) uint8_t bytes[T_BCAP + 32];
+    uint16_t v[T_E];
+    uint16_t w[T_E];
+    uint64_t fbbase[T_MAXR];
+    uint32_t fbcount[T_MAXR];
+    uint8_t fbrow[T_MAXR];    // slot -> row index in tile
+    uint8_t fbslot[T_MAXR];   // coop row -> slot (0xFF none)
+    uint8_t fbstat[T_MAXR];
+    uint8_t hfbad[T_MAXR];
+    uint16_t wrow[T_MAXR + 1];  // W index of each coop row's B / FB sentinel
+};
+
+struct TileArgs {
+    RowArgs ra;           // in, offs, n, out (ids), cap, out_offs, row_status, bpe, single_fast
+    uint64_t *status;     // look-back words, one per tile, zeroed before the launch
+    uint32_t *ticket;     // tile ticket counter, zeroed before the launch
+    uint32_t *locks;      // SLOW_THREADS pool-region locks (zeroed once)
+    uint32_t *err;        // set if a look-back spin gave up
+    uint64_t ntiles;
+    int rows;             // R
+};
+
+__device__ __forceinline__ uint32_t lds_decode(const uint8_t *B, int p, int e, int &len) {
+    const uint32_t c = B[p];
+    if (c < 0x80u) { len = 1; return c; }
+    const int l = c >= 0xF0u ? 4 : c >= 0xE0u ? 3 : c >= 0xC0u ? 2 : 0;
+    len = 1;
+    if (l == 0 || c > 0xF4u || p + l > e) return 0xFFFFFFFFu;
+    uint32_t cp = c & (0x7Fu >> l);
+    for (int k = 1; k < l; ++k) {
+        const uint32_t b = B[p + k];
+        if ((b & 0xC0u) != 0x80u) return 0xFFFFFFFFu;
+        cp = (cp << 6) | (b & 0x3Fu);
+    }
+    const uint32_t mn = l == 2 ? 0x80u : l == 3 ? 0x800u : 0x10000u;
+    if (cp < mn || cp > 0x10FFFFu) return 0xFFFFFFFFu;
+    len = l;
+    return cp;
+}
+
+template <int FLAGS>
+__device__ __forceinline__ uint32_t map_cp(const uint2 *fast, uint32_t cp) {
+    const uint2 pr = prop(fast, cp);
+    if (FLAGS == 3) return p_normmap(pr);
+    return p_allowed(pr) ? cp : 0u;  // FLAGS == 2
+}
+
+__device__ __forceinline__ bool hf_stable(const uint2 *fast, uint32_t x) {
+    const uint2 pr = prop(fast, x);
+    return p_ccc_hf(pr) == 0 && !p_second(pr);
+}
+
+__device__ __forceinline__ uint32_t single_id_of(const BpeDev &m, const uint16_t *sfast, uint32_t cp) {
+    if (cp < FAST_N) return sfast[cp];
+    int lo = 0, hi = (int)m.n_single - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t k = m.single_sorted_cp[mid];
+        if (k == cp) return m.single_sorted_id[mid];
+        if (k < cp) lo = mid + 1; else hi = mid - 1;
+    }
+    return 0xFFFFu;
+}
+
+// BPE merge_all on W[st .. st+n) in place; returns the final symbol count. Pair ranks are looked
+// up in batches of 8 independent loads so one L2 round trip serves up to 8 pairs.
+__device__ __forceinline__ int bpe_merge_lds(const BpeDev &m, uint16_t *W, int st, int n) {
+    while (n > 1) {
+        uint32_t best = 0xFFFFFFFFu;
+        int bi = -1;
+        for (int i0 = 0; i0 + 1 < n; i0 += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int i = i0 + q;
+                v[q] = i + 1 < n ? merge_lookup(m, W[st + i], W[st + i + 1]) : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (v[q] < best) { best = v[q]; bi = i0 + q; }
+        }
+        if (bi < 0) break;
+        W[st + bi] = (uint16_t)(best & 0xFFFFu);
+        for (int i = bi + 1; i + 1 < n; ++i) W[st + i] = W[st + i + 1];
+        W[st + n - 1] = V_DEAD;
+        --n;
+    }
+    return n;
+}
+
+// sequential fallback for one row (count or emit), private buffers first, then the locked pool
+template <int FLAGS, bool EMIT>
+__device__ __noinline__ uint64_t fallback_row(const TileArgs &ta, uint64_t r, const uint2 *fast, const uint16_t *sfast,
+                                 uint64_t emit_base, uint32_t wave_gid, uint32_t &status) {
+    uint32_t seg[T_FBSEG], dec[4 * T_FBSEG], seg2[T_FBSEG], dec2[4 * T_FBSEG];
+    uint16_t wsym[T_FBWORD];
+    uint32_t wpair[T_FBWORD];
+    Scratch sc;
+    sc.seg = seg; sc.dec = dec; sc.seg2 = seg2; sc.dec2 = dec2; sc.seg_cap = T_FBSEG;
+    sc.wsym = wsym; sc.wpair = wpair; sc.word_cap = T_FBWORD;
+    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
+    sc.slow_status = ST_SLOW;
+    sc.status = 0;
+    uint64_t cnt = process_row<OP_BPE, FLAGS, EMIT>(ta.ra, r, fast, sfast, &sc, emit_base);
+    if (sc.status & ST_SLOW) {
+        const uint32_t region = wave_gid % SLOW_THREADS;
+        while (__hip_atomic_exchange(ta.locks + region, 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u)
+            w_sleep();
+        const SlowPool &P = ta.ra.pool;
+        const uint64_t t = region;
+        sc.seg = P.seg + t * 2 * SLOW_SEG;
+        sc.dec = P.dec + t * 8 * SLOW_SEG;
+        sc.seg2 = sc.seg + SLOW_SEG;
+        sc.dec2 = sc.dec + 4 * SLOW_SEG;
+        sc.seg_cap = SLOW_SEG;
+        sc.wsym = P.wsym + t * SLOW_WORD;
+        sc.wpair = P.wpair + t * SLOW_WORD;
+        sc.word_cap = SLOW_WORD;
+        sc.slow_status = ST_LIMIT;
+        sc.status = 0;
+        cnt = process_row<OP_BPE, FLAGS, EMIT>(ta.ra, r, fast, sfast, &sc, emit_base);
+        __hip_atomic_store(ta.locks + region, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (sc.status & ST_LIMIT) cnt = 0;
+    }
+    status = (sc.status & ST_BAD_UTF8) | (sc.status & ST_LIMIT);
+    return cnt;
+}
+
+// Decoupled look-back: returns the exclusive prefix (tokens before tile t).
+__device__ __forceinline__ uint64_t tile_lookback(const TileArgs &ta, uint64_t t, uint64_t total) {
+    const int lane = w_lane();
+    if (t == 0) {
+        if (lane == 0) w_atomic_store64(ta.status, LB_INC | total);
+        return 0;
+    }
+    if (lane == 0) w_atomic_store64(ta.status + t, LB_AGG | total);
+    uint64_t prefix = 0;
+    int64_t j = (int64_t)t - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t q = j - lane;
+        const uint64_t s = q >= 0 ? w_atomic_load64(ta.status + q) : LB_INC;
+        const uint64_t flag = s & ~LB_MASK;
+        const uint64_t inc = w_ballot(flag == LB_INC);
+        const uint64_t zero = w_ballot(flag == 0);
+        const int first_inc = inc ? __builtin_ctzll(inc) : 64;
+        const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
+        if (zero & upto) {  // a predecessor before the nearest inclusive has not published yet
+            if (++spins > (1u << 26)) {
+                if (lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            w_sleep();
+            continue;
+        }
+        const uint64_t mine = (uint64_t)lane <= (uint64_t)first_inc ? (s & LB_MASK) : 0ull;
+        const uint64_t lsum = w_sum64(mine);
+        prefix += lsum;
+        if (first_inc < 64) break;
+        j -= 64;
+    }
+    if (lane == 0) w_atomic_store64(ta.status + t, LB_INC | ((prefix + total) & LB_MASK));
+    return prefix;
+}
+
+template <int FLAGS>
+__device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, const uint16_t *sfast, TileWaveMem &M,
+                         uint32_t wave_gid) {
+    const int lane = w_lane();
+    const uint64_t lt = w_lanemask_lt();
+    const RowArgs &a = ta.ra;
+    const BpeDev &m = a.bpe;
+    const uint64_t r0 = t * (uint64_t)ta.rows;
+    const uint64_t r1 = r0 + (uint64_t)ta.rows < a.n ? r0 + (uint64_t)ta.rows : a.n;
+    const int nr = (int)(r1 - r0);
+    const uint64_t myoff = lane <= nr ? a.offs[r0 + lane] : 0ull;
+    const uint64_t S0 = w_shfl(myoff, 0);
+    const bool fits = lane >= 1 && lane <= nr && (myoff - S0) <= (uint64_t)T_BCAP;
+    const int k = w_popc(w_ballot(fits));  // rows 0..k-1 take the cooperative path
+    const uint64_t S1 = w_shfl(myoff, k);
+    const uint64_t a0 = S0 & ~15ull;
+    {
+        const uint64_t nblk = (S1 - a0 + 15) / 16;
+        const uint4 *src = (const uint4 *)(a.in) + a0 / 16;
+        uint4 *dst = (uint4 *)M.bytes;
+        for (uint64_t b = (uint64_t)lane; b < nblk; b += 64) dst[b] = src[b];
+    }
+    if (lane < T_MAXR) { M.fbslot[lane] = 0xFF; M.hfbad[lane] = 0; }
+    w_sync();
+
+    // ---------------- pass D: decode + NFC + map/filter -> V
+    uint8_t *FL = (uint8_t *)M.w;  // NFC leader flags by byte position (W is free until pass E)
+    uint32_t vpos = 0;
+    uint32_t nfb = 0;
+    for (int i = 0; i < k; ++i) {
+        const int s = (int)(w_shfl(myoff, i) - a0), e = (int)(w_shfl(myoff, i + 1) - a0);
+        const uint32_t vstart = vpos;
+        if (lane == 0) M.v[vpos] = V_B;
+        ++vpos;
+        bool rowbad = false;
+        for (int base = s; base < e; base += 64) {
+            const int p = base + lane;
+            const bool in = p < e;
+            const uint32_t byte = in ? M.bytes[p] : 0u;
+            const bool lead = in && (byte & 0xC0u) != 0x80u;
+            bool bad = in && p == s && !lead;
+            uint32_t cp = 0;
+            int len = 1;
+            uint2 pr = make_uint2(0, 0);
+            if (lead) {
+                cp = lds_decode(M.bytes, p, e, len);
+                if (cp == 0xFFFFFFFFu) bad = true;
+                else pr = prop(fast, cp);
+            }
+            const bool ok = lead && !bad;
+            const bool segstart = ok && (p == s || p_stable(pr));
+            bool changed = false;
+            int nout = 0;
+            uint32_t outs[4 * T_SEG];
+            bool need = false;
+            if (segstart) {
+                need = !p_stable(pr);  // a row-initial non-stable char (e.g. U+0958) is its own segment
+                if (!need && p + len < e) {
+                    int l2;
+                    const uint32_t c2 = lds_decode(M.bytes, p + len, e, l2);
+                    need = c2 != 0xFFFFFFFFu && !p_stable(prop(fast, c2));
+                }
+            }
+            {
+                if (need) {
+                    uint32_t seg[T_SEG], dec[4 * T_SEG];
+                    int n = 0;
+                    seg[n++] = cp;
+                    int q = p + len;
+                    while (q < e) {
+                        int lq;
+                        const uint32_t c = lds_decode(M.bytes, q, e, lq);
+                        if (c == 0xFFFFFFFFu || p_stable(prop(fast, c))) break;
+                        if (n == T_SEG) { bad = true; break; }
+                        seg[n++] = c;
+                        q += lq;
+                    }
+                    if (!bad) {
+                        const int wn = nfc_full<false>(seg, dec, n, 4 * T_SEG, fast);
+                        if (wn < 0) bad = true;
+                        else {
+                            changed = wn != n;
+                            for (int j = 0; j < wn && !changed; ++j) changed = dec[j] != seg[j];
+                            if (changed)
+                                for (int j = 0; j < wn; ++j) {
+                                    const uint32_t mv = map_cp<FLAGS>(fast, dec[j]);
+                                    if (mv) outs[nout++] = mv;
+                                }
+                        }
+                    }
+                }
+            }
+            if (segstart) FL[p] = changed ? 1 : 0;
+            if (w_ballot(bad)) { rowbad = true; break; }
+            w_sync();
+            bool inchg = false;
+            if (ok && !segstart) {
+                int q = p;
+                for (;;) {
+                    --q;
+                    while (q > s && (M.bytes[q] & 0xC0u) == 0x80u) --q;
+                    int lq;
+                    const uint32_t c = lds_decode(M.bytes, q, e, lq);
+                    if (q <= s || (c != 0xFFFFFFFFu && p_stable(prop(fast, c)))) break;
+                }
+                inchg = FL[q] != 0;
+            }
+            uint32_t cnt = 0, mval = 0;
+            if (ok) {
+                if (segstart && changed) cnt = (uint32_t)nout;
+                else if (!inchg) { mval = map_cp<FLAGS>(fast, cp); cnt = mval ? 1u : 0u; }
+            }
+            uint32_t tot;
+            const uint32_t ex = w_exscan(cnt, &tot);
+            if (cnt) {
+                if (segstart && changed) for (int j = 0; j < nout; ++j) M.v[vpos + ex + j] = (uint16_t)outs[j];
+                else M.v[vpos + ex] = (uint16_t)mval;
+            }
+            vpos += tot;
+        }
+        if (rowbad) {
+            vpos = vstart;
+            if (lane == 0) { M.v[vpos] = V_FB; M.fbrow[nfb] = (uint8_t)i; M.fbslot[i] = (uint8_t)nfb; }
+            ++vpos;
+            ++nfb;
+        } else {
+            if (lane == 0) M.v[vpos] = V_E;
+            ++vpos;
+        }
+        w_sync();
+    }
+    const uint32_t vlen = vpos;
+    w_sync();
+
+    // ---------------- pass E: remove_elongations V -> W (+ row sentinel positions)
+    uint32_t wlen = 0, rows_seen = 0;
+    for (uint32_t base = 0; base < vlen; base += 64) {
+        const uint32_t kk = base + lane;
+        const bool in = kk < vlen;
+        const uint16_t x = in ? M.v[kk] : V_DEAD;
+        const uint16_t pa = in && kk >= 1 ? M.v[kk - 1] : V_DEAD;
+        const uint16_t pb = in && kk >= 2 ? M.v[kk - 2] : V_DEAD;
+        const uint16_t nx = in && kk + 1 < vlen ? M.v[kk + 1] : V_DEAD;
+        const bool drop = in && x < V_SPECIAL && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
+        const bool keep = in && !drop;
+        const uint64_t km = w_ballot(keep);
+        const uint32_t pos = wlen + (uint32_t)w_popc(km & lt);
+        const bool isrow = in && (x == V_B || x == V_FB);
+        const uint64_t rm = w_ballot(isrow);
+        if (keep) M.w[pos] = x;
+        if (isrow) M.wrow[rows_seen + w_popc(rm & lt)] = (uint16_t)pos;
+        wlen += (uint32_t)w_popc(km);
+        rows_seen += (uint32_t)w_popc(rm);
+    }
+    if (lane == 0) M.wrow[rows_seen] = (uint16_t)wlen;
+    w_sync();
+
+    // ---------------- pass H: HF NFKC (compat spaces -> ' ', HF-ccc segments checked)
+    for (uint32_t base = 0; base < wlen; base += 64) {
+        const uint32_t kk = base + lane;
+        if (kk < wlen) {
+            const uint16_t x = M.w[kk];
+            if (x < V_SPECIAL && p_hfspace(prop(fast, x))) M.w[kk] = 0x20;
+        }
+    }
+    w_sync();
+    for (uint32_t base = 0; base < wlen; base += 64) {
+        const uint32_t kk = base + lane;
+        bool bad = false;
+        if (kk + 1 < wlen) {
+            const uint16_t x = M.w[kk];
+            const uint16_t y = M.w[kk + 1];
+            const bool lead = x < V_SPECIAL && (hf_stable(fast, x) || kk == 0 || M.w[kk - 1] >= V_SPECIAL);
+            if (lead && y < V_SPECIAL && !hf_stable(fast, y)) {
+                uint32_t seg[T_SEG], dec[4 * T_SEG];
+                int n = 0;
+                seg[n++] = x;
+                uint32_t q = kk + 1;
+                while (q < wlen && M.w[q] < V_SPECIAL && !hf_stable(fast, M.w[q])) {
+                    if (n == T_SEG) { bad = true; break; }
+                    seg[n++] = M.w[q++];
+                }
+                if (!bad) {
+                    const int wn = nfc_full<true>(seg, dec, n, 4 * T_SEG, fast);
+                    bool changed = wn != n;
+                    for (int j = 0; j < wn && !changed; ++j) changed = dec[j] != seg[j];
+                    bad = changed || wn < 0;
+                }
+            }
+        }
+        if (bad) {
+            int ri = 0;
+            while (ri + 1 < (int)rows_seen && M.wrow[ri + 1] <= kk) ++ri;
+            M.hfbad[ri] = 1;
+        }
+    }
+    w_sync();
+    for (int ri = 0; ri < (int)rows_seen; ++ri) {
+        if (!M.hfbad[ri]) continue;  // uniform (LDS value)
+        const uint32_t b = M.wrow[ri], e2 = M.wrow[ri + 1];
+        for (uint32_t q = b + 1 + lane; q < e2; q += 64) M.w[q] = V_DEAD;
+        if (lane == 0) { M.w[b] = V_FB; M.fbrow[nfb] = (uint8_t)ri; M.fbslot[ri] = (uint8_t)nfb; }
+        ++nfb;
+        w_sync();
+    }
+    // rows past the tile buffer
+    for (int i = k; i < nr; ++i) {
+        if (lane == 0) M.fbrow[nfb] = (uint8_t)i;
+        ++nfb;
+    }
+    w_sync();
+
+    // ---------------- pass P: Whitespace pre-tokenizer (\w+ | [^\w\s]+)
+    uint32_t nw = 0;
+    for (uint32_t base = 0; base < wlen; base += 64) {
+        const uint32_t kk = base + lane;
+        const bool in = kk < wlen;
+        auto cls = [&](uint16_t x) -> int {
+            if (x >= V_SPECIAL) return HF_S;
+            return p_hfclass(prop(fast, (uint32_t)(x & 0x7FFF)));
+        };
+        const uint16_t x = in ? M.w[kk] : V_DEAD;
+        const int c0 = cls(x);
+        const int cp_ = in && kk >= 1 ? cls(M.w[kk - 1]) : HF_S;
+        const int cn = in && kk + 1 < wlen ? cls(M.w[kk + 1]) : HF_S;
+        const bool isstart = in && c0 != HF_S && c0 != cp_;
+        const bool isend = in && c0 != HF_S && c0 != cn;
+        const uint64_t sm = w_ballot(isstart);
+        w_sync();
+        if (in && x < V_SPECIAL && c0 == HF_S) M.w[kk] = V_DEAD;
+        if (isend) M.w[kk] = (uint16_t)(x | WEND);
+        if (isstart) M.v[nw + w_popc(sm & lt)] = (uint16_t)kk;
+        nw += (uint32_t)w_popc(sm);
+        w_sync();
+    }
+
+    // ---------------- pass B: lane per word, merge_all in place
+    for (uint32_t wb = 0; wb < nw; wb += 64) {
+        const uint32_t j = wb + lane;
+        if (j < nw) {
+            const int st = M.v[j];
+            int n = 0, q = st;
+            for (;;) {
+                const uint16_t x = M.w[q];
+                const uint32_t id = single_id_of(m, sfast, (uint32_t)(x & 0x7FFF));
+                if (id != 0xFFFFu) M.w[st + n++] = (uint16_t)id;
+                ++q;
+                if (x & WEND) break;
+            }
+            for (int z = st + n; z < q; ++z) M.w[z] = V_DEAD;
+            (void)bpe_merge_lds(m, M.w, st, n);
+        }
+    }
+    w_sync();
+
+    // ---------------- fallback rows: count
+    uint32_t fbst = 0;
+    uint64_t fbcnt = 0;
+    if ((uint32_t)lane < nfb) fbcnt = fallback_row<FLAGS, false>(ta, r0 + M.fbrow[lane], fast, sfast, 0, wave_gid, fbst);
+    if ((uint32_t)lane < nfb) { M.fbcount[lane] = (uint32_t)fbcnt; M.fbstat[lane] = (uint8_t)fbst; }
+    w_sync();
+
+    // ---------------- pass F1: tile total
+    auto weight = [&](uint16_t x, uint32_t ridx) -> uint32_t {
+        if (x == V_FB) return M.fbcount[M.fbslot[ridx]];
+        return x == V_DEAD ? 0u : 1u;
+    };
+    uint64_t T = 0;
+    rows_seen = 0;
+    for (uint32_t base = 0; base < wlen; base += 64) {
+        const uint32_t kk = base + lane;
+        const bool in = kk < wlen;
+        const uint16_t x = in ? M.w[kk] : V_DEAD;
+        const bool isrow = in && (x == V_B || x == V_FB);
+        const uint64_t rm = w_ballot(isrow);
+        const uint32_t ridx = rows_seen + (uint32_t)w_popc(rm & lt);
+        uint32_t tot;
+        (void)w_exscan(in ? weight(x, ridx) : 0u, &tot);
+        T += tot;
+        rows_seen += (uint32_t)w_popc(rm);
+    }
+    const uint64_t Tcoop = T;
+    {
+        uint32_t tail = 0;
+        if ((uint32_t)lane < nfb && M.fbrow[lane] >= k) tail = M.fbcount[lane];
+        uint32_t tt;
+        (void)w_exscan(tail, &tt);
+        T += tt;
+    }
+
+    // ---------------- look-back
+    const uint64_t base_out = tile_lookback(ta, t, T);
+
+    // ---------------- pass F2: write ids + row offsets
+    uint64_t *oo = const_cast<uint64_t *>(a.out_offs);
+    uint64_t pos = base_out;
+    rows_seen = 0;
+    for (uint32_t base = 0; base < wlen; base += 64) {
+        const uint32_t kk = base + lane;
+        const bool in = kk < wlen;
+        const uint16_t x = in ? M.w[kk] : V_DEAD;
+        const bool isrow = in && (x == V_B || x == V_FB);
+        const uint64_t rm = w_ballot(isrow);
+        const uint32_t ridx = rows_seen + (uint32_t)w_popc(rm & lt);
+        const uint32_t wgt = in ? weight(x, ridx) : 0u;
+        uint32_t tot;
+        const uint32_t ex = w_exscan(wgt, &tot);
+        const uint64_t op = pos + ex;
+        uint32_t* ids = (uint32_t *)a.out;
+        if (x == V_B) {
+            if (op < a.cap) ids[op] = m.bos;
+            oo[r0 + ridx] = op;
+        } else if (x == V_FB) {
+            oo[r0 + ridx] = op;
+            M.fbbase[M.fbslot[ridx]] = op;
+        } else if (x == V_E) {
+            if (op < a.cap) ids[op] = m.eos;
+        } else if (in && x != V_DEAD) {
+            if (op < a.cap) ids[op] = x;
+        }
+        pos += tot;
+        rows_seen += (uint32_t)w_popc(rm);
+    }
+    {
+        uint32_t tail = 0;
+        const bool istail = (uint32_t)lane < nfb && M.fbrow[lane] >= k;
+        if (istail) tail = M.fbcount[lane];
+        uint32_t tt;
+        const uint32_t ex = w_exscan(tail, &tt);
+        if (istail) {
+            const uint64_t op = base_out + Tcoop + ex;
+            M.fbbase[lane] = op;
+            oo[r0 + M.fbrow[lane]] = op;
+        }
+    }
+    if (lane == 0 && r1 == a.n) oo[a.n] = base_out + T;
+    w_sync();
+
+    // ---------------- fallback rows: emit
+    if ((uint32_t)lane < nfb) {
+        uint32_t st2;
+        (void)fallback_row<FLAGS, true>(ta, r0 + M.fbrow[lane], fast, sfast, M.fbbase[lane], wave_gid, st2);
+    }
+    if (a.row_status && lane < nr) {
+        uint8_t st3 = 0;
+        for (uint32_t j = 0; j < nfb; ++j)
+            if (M.fbrow[j] == lane) st3 = M.fbstat[j];
+        a.row_status[r0 + lane] = st3;
+    }
+    w_sync();
+}
+
+template <int FLAGS>
+__device__ void bpe_tiles_wave(const TileArgs &ta, const uint2 *fast, const uint16_t *sfast, TileWaveMem &M,
+                               uint32_t wave_gid) {
+    const int lane = w_lane();
+    for (;;) {
+        uint32_t t0 = 0;
+        if (lane == 0) t0 = w_atomic_add32(ta.ticket, (uint32_t)T_TPB);
+        t0 = w_shfl(t0, 0);
+        if ((uint64_t)t0 >= ta.ntiles) break;
+        const uint64_t t1 = (uint64_t)t0 + T_TPB < ta.ntiles ? (uint64_t)t0 + T_TPB : ta.ntiles;
+        for (uint64_t t = t0; t < t1; ++t) bpe_tile<FLAGS>(ta, t, fast, sfast, M, wave_gid);
+    }
+}
+
+}  // namespace ak

@@ -1,0 +1,123 @@
+// ak_wave.h — wave64 primitives used by the tile-cooperative kernels.
+//
+// On gfx950 they map to the hardware: lane id via mbcnt, __ballot (64-bit mask), __shfl, a
+// 6-step shuffle scan, and a wavefront fence + wave barrier for LDS hand-offs between lanes of one
+// wave. Under AK_HOST_EMU (tests/emu) each lane is a host thread and every primitive is a
+// rendezvous of the 64 threads, so the same kernel source runs lane-for-lane on the CPU.
+// Primitives must be called in wave-uniform control flow.
+#pragma once
+#include <stdint.h>
+
+#ifdef AK_HOST_EMU
+#include <atomic>
+#include <barrier>
+
+namespace ak {
+struct EmuWave {
+    std::barrier<> bar{64};
+    uint64_t slot[64];
+};
+extern thread_local int t_lane;
+extern thread_local EmuWave *t_wave;
+
+inline int w_lane() { return t_lane; }
+inline void w_sync() { t_wave->bar.arrive_and_wait(); }
+inline uint64_t w_ballot(bool p) {
+    t_wave->slot[t_lane] = p ? 1 : 0;
+    w_sync();
+    uint64_t m = 0;
+    for (int i = 0; i < 64; ++i) m |= (t_wave->slot[i] & 1ull) << i;
+    w_sync();
+    return m;
+}
+template <typename T>
+inline T w_shfl(T v, int src) {
+    static_assert(sizeof(T) <= 8, "");
+    uint64_t x = 0;
+    __builtin_memcpy(&x, &v, sizeof(T));
+    t_wave->slot[t_lane] = x;
+    w_sync();
+    uint64_t y = t_wave->slot[src & 63];
+    w_sync();
+    T r;
+    __builtin_memcpy(&r, &y, sizeof(T));
+    return r;
+}
+// exclusive prefix sum over lanes; *total gets the wave sum
+inline uint32_t w_exscan(uint32_t v, uint32_t *total) {
+    t_wave->slot[t_lane] = v;
+    w_sync();
+    uint32_t ex = 0, tot = 0;
+    for (int i = 0; i < 64; ++i) {
+        if (i < t_lane) ex += (uint32_t)t_wave->slot[i];
+        tot += (uint32_t)t_wave->slot[i];
+    }
+    w_sync();
+    *total = tot;
+    return ex;
+}
+inline uint64_t w_atomic_load64(const uint64_t *p) {
+    return reinterpret_cast<const std::atomic<uint64_t> *>(p)->load(std::memory_order_relaxed);
+}
+inline void w_atomic_store64(uint64_t *p, uint64_t v) {
+    reinterpret_cast<std::atomic<uint64_t> *>(p)->store(v, std::memory_order_relaxed);
+}
+inline uint32_t w_atomic_add32(uint32_t *p, uint32_t v) {
+    return reinterpret_cast<std::atomic<uint32_t> *>(p)->fetch_add(v, std::memory_order_relaxed);
+}
+inline void w_sleep() {}
+}  // namespace ak
+
+#else
+#include <hip/hip_runtime.h>
+
+namespace ak {
+__device__ __forceinline__ int w_lane() {
+    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+// LDS written by some lanes is read by others after this (same wave)
+__device__ __forceinline__ void w_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ uint64_t w_ballot(bool p) { return (uint64_t)__ballot(p); }
+template <typename T>
+__device__ __forceinline__ T w_shfl(T v, int src) { return __shfl(v, src, 64); }
+__device__ __forceinline__ uint32_t w_exscan(uint32_t v, uint32_t *total) {
+    const int lane = w_lane();
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
+__device__ __forceinline__ uint64_t w_atomic_load64(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void w_atomic_store64(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t w_atomic_add32(uint32_t *p, uint32_t v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void w_sleep() { __builtin_amdgcn_s_sleep(2); }
+}  // namespace ak
+#endif
+
+namespace ak {
+__device__ __forceinline__ uint64_t w_lanemask_lt() {
+    const int l = w_lane();
+    return l == 0 ? 0ull : (~0ull >> (64 - l));
+}
+__device__ __forceinline__ int w_popc(uint64_t m) { return __builtin_popcountll(m); }
+// wave-wide 64-bit sum (butterfly), every lane gets the total
+__device__ __forceinline__ uint64_t w_sum64(uint64_t x) {
+    const int l = w_lane();
+    for (int d = 32; d >= 1; d >>= 1) x += w_shfl(x, l ^ d);
+    return x;
+}
+}  // namespace ak

@@ -152,6 +152,20 @@ def switches_batch(buf, offs, flags=3, row_status=None):
     return ends[:total], labels[:total], oo
 
 
+import os as _os
+
+# 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (v1); AK_BPE_PATH overrides
+BPE_PATH = int(_os.environ.get("AK_BPE_PATH", "1"))
+TILE_BYTES = 1100  # target bytes of text per wave-tile (the tile buffer holds 2048)
+
+
+def tile_rows_for(n, nbytes):
+    if n == 0:
+        return 8
+    avg = max(nbytes / n, 1.0)
+    return int(min(16, max(1, round(TILE_BYTES / avg))))
+
+
 class BPE:
     """Device-resident HF BPE model (models/akshar.json layout, cli.py:276-299)."""
 
@@ -172,7 +186,7 @@ class BPE:
         if h:
             _lib.lib().ak_bpe_free(h)
 
-    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None):
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, path=None):
         n = _check_inputs(buf, offs)
         dev = buf.device
         ws = workspace(dev.index)
@@ -180,12 +194,16 @@ class BPE:
             nbytes = int(offs[-1].item()) if n else 0
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
+        path = BPE_PATH if path is None else path
+        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows_for(n, nbytes)), "ak_ws_set_tiling")
 
         def call(out, c, oo):
             check(_lib.lib().ak_bpe_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
                                            _ptr(row_status), _stream(dev)), "ak_bpe_encode")
 
         out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev)
+        if path == 1:
+            check(_lib.lib().ak_ws_check(ws), "ak_ws_check")
         return out[:total], oo
 
 

@@ -64,6 +64,12 @@ int ak_version(void);
 
 int ak_ws_create(ak_ws **out);
 void ak_ws_free(ak_ws *ws);
+/* BPE kernel choice for this workspace: bpe_path 1 = tile-cooperative single pass (default;
+ * tile_rows rows per wave-tile, 1..16, default 8 — pick ~1.1 KB of text per tile), 0 = one lane
+ * per row (count/scan/emit). */
+int ak_ws_set_tiling(ak_ws *ws, int bpe_path, int tile_rows);
+/* Synchronous health check after a batch: AK_ERR_HIP if a device-side wait timed out. */
+int ak_ws_check(ak_ws *ws);
 
 /* Replaces Tokenizer.from_file(path) (tokenizer.py:96-97) for the model cli.py:276-299 trains:
  * NFKC -> Whitespace -> BPE(unk_token=None) -> "<s> $A </s>".
@@ -116,7 +122,8 @@ int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, cons
 #define AK_PROF_SCAN 2       /* row counts -> row offsets (three small kernels) */
 #define AK_PROF_EMIT 3       /* fast emit pass */
 #define AK_PROF_EMIT_SLOW 4  /* slow-path emit pass */
-#define AK_PROF_NKERNELS 5
+#define AK_PROF_TILES 5      /* tile-cooperative BPE kernel (single pass) */
+#define AK_PROF_NKERNELS 6
 int ak_profile_enable(int on);
 int ak_profile_read(int kernel, double *total_ms, uint64_t *launches);
 void ak_profile_reset(void);

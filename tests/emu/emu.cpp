@@ -11,6 +11,9 @@
 #include "../../akshar_amd/csrc/ak_dev.h"
 #include "../../akshar_amd/csrc/ak_model_build.h"
 #include "../../akshar_amd/csrc/ak_rows.h"
+#include "../../akshar_amd/csrc/ak_tile.h"
+
+#include <thread>
 
 using namespace ak;
 
@@ -77,11 +80,11 @@ static int64_t run(RowArgs a) {
     std::vector<int> mode(a.n);
     for (uint64_t r = 0; r < a.n; ++r) {
         Scratch sc = scratch(false);
-        uint64_t c = process_row<OP, FLAGS, false>(a, r, fast, a.single_fast, &sc);
+        uint64_t c = process_row<OP, FLAGS, false>(a, r, fast, a.single_fast, &sc, 0);
         mode[r] = 0;
         if (sc.status & ST_SLOW) {
             Scratch s2 = scratch(true);
-            c = process_row<OP, FLAGS, false>(a, r, fast, a.single_fast, &s2);
+            c = process_row<OP, FLAGS, false>(a, r, fast, a.single_fast, &s2, 0);
             mode[r] = (s2.status & ST_LIMIT) ? 2 : 1;
             if (mode[r] == 2) c = 0;
         }
@@ -94,7 +97,7 @@ static int64_t run(RowArgs a) {
     for (uint64_t r = 0; r < a.n; ++r) {
         if (mode[r] == 2) continue;
         Scratch sc = scratch(mode[r] == 1);
-        (void)process_row<OP, FLAGS, true>(a, r, fast, a.single_fast, &sc);
+        (void)process_row<OP, FLAGS, true>(a, r, fast, a.single_fast, &sc, a.out_offs[r]);
     }
     return (int64_t)oo[a.n];
 }
@@ -132,4 +135,47 @@ extern "C" int64_t emu_run(int op, int flags, int matras, void *model, const uin
         case 4: return dispatch<OP_SPM>(flags, a);
     }
     return -1;
+}
+
+// ------------------------------------------------------------------------------------------
+// tile-cooperative BPE kernel: one emulated wave (64 host threads in lockstep) walks every tile
+
+namespace ak {
+thread_local int t_lane;
+thread_local EmuWave *t_wave;
+}  // namespace ak
+
+extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
+                                 uint32_t *out, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, int rows) {
+    EmuModel *m = (EmuModel *)model;
+    static uint2 fast[FAST_N];
+    for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
+    TileArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = out; ta.ra.cap = cap; ta.ra.out_offs = out_offs;
+    ta.ra.row_status = row_status; ta.ra.bpe = m->bdev; ta.ra.single_fast = m->bpe.fast.data();
+    std::vector<uint32_t> seg(2 * SLOW_SEG), dec(8 * SLOW_SEG), wpair(SLOW_WORD), vchar(SLOW_WORD);
+    std::vector<uint16_t> wsym(SLOW_WORD);
+    ta.ra.pool.seg = seg.data(); ta.ra.pool.dec = dec.data(); ta.ra.pool.wsym = wsym.data();
+    ta.ra.pool.wpair = wpair.data(); ta.ra.pool.vchar = vchar.data();
+    const uint64_t ntiles = (n + rows - 1) / rows;
+    std::vector<uint64_t> status(ntiles + 1, 0);
+    uint32_t ticket = 0, err = 0;
+    std::vector<uint32_t> locks(SLOW_THREADS, 0);
+    ta.status = status.data(); ta.ticket = &ticket; ta.locks = locks.data(); ta.err = &err;
+    ta.ntiles = ntiles; ta.rows = rows;
+    if (n == 0) { out_offs[0] = 0; return 0; }
+    TileWaveMem *M = new TileWaveMem();
+    EmuWave W;
+    std::vector<std::thread> th;
+    for (int lane = 0; lane < 64; ++lane)
+        th.emplace_back([&, lane] {
+            t_lane = lane;
+            t_wave = &W;
+            if (flags == 3) bpe_tiles_wave<3>(ta, fast, m->bpe.fast.data(), *M, 0);
+            else bpe_tiles_wave<2>(ta, fast, m->bpe.fast.data(), *M, 0);
+        });
+    for (auto &x : th) x.join();
+    delete M;
+    return err ? -1 : (int64_t)out_offs[n];
 }

@@ -1,0 +1,54 @@
+"""The tile-cooperative BPE kernel (ak_tile.h) on one emulated wave (tests/emu: 64 host threads in
+lockstep per wave primitive) against the golden vectors and the oracle, including every fallback
+route: invalid UTF-8, NFC segments longer than the cooperative cap, rows larger than the tile
+buffer, words past the private fallback buffers."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.emu import emu
+from tests.util import rows_ints
+
+
+@pytest.fixture(scope="module")
+def em(bpe_model):
+    return emu.Model(bpe=bpe_model)
+
+
+def test_golden(golden, em):
+    packed = O.pack([r["text"] for r in golden])
+    ids, oo, st = emu.bpe_tiles(em, *packed, rows=8)
+    bad = [(r["set"], r["text"]) for r, g in zip(golden, rows_ints(ids, oo)) if g != r["bpe"]]
+    assert bad == []
+    assert not st.any()
+
+
+def _raw_rows(rows):
+    offs = np.zeros(len(rows) + 1, dtype=np.uint64)
+    np.cumsum([len(r) for r in rows], out=offs[1:])
+    buf = np.frombuffer(b"".join(rows) or b"\0", dtype=np.uint8).copy()
+    return buf, offs
+
+
+@pytest.mark.parametrize("rows", [1, 4, 16])
+def test_fallback_rows_match_oracle(em, bpe_model, rows):
+    texts = ["क" + "्क" * 200, "a" + "́" * 300 + "b", "x" * 5000, "abcdefghij" * 50, "१२३४५६७८९०" * 30,
+             "ज्ञ" * 100 + " " + "hello " * 100, "ऩ" + "़" * 40 + "्" * 40, "Ḱ" + "̣" * 20, "", "ok",
+             "न€़ ে€া", "क" + "॑" * 20 + "़", "ড়" * 3, "aaj मौसम", "x" * 2047, "y" * 2048, "z" * 2049]
+    raw = [t.encode("utf-8") for t in texts]
+    raw += [b"\xff\xfeabc", b"ok \xe0\xa4", b"\xc3(", b"\xed\xa0\x80 x", b"\x80lead", b"mid\xf4\x90\x80\x80end"]
+    buf, offs = _raw_rows(raw)
+    ids, oo, st = emu.bpe_tiles(em, buf, offs, rows=rows)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)
+    # invalid UTF-8 flagged; the surrogate form ED A0 80 decodes (as the oracle, cf. surrogatepass)
+    assert st[len(texts):].tolist() == [1, 1, 1, 0, 1, 1]
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_synthetic_vs_oracle(em, bpe_model, kind):
+    from akshar_amd import synth
+    buf, offs = synth.generate(kind, 1500, seed=300 + kind)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
