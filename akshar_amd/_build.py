@@ -5,6 +5,7 @@
   oracle/_oracle.so  the CPU restatement (test infrastructure; built by oracle/Makefile)
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -43,8 +44,25 @@ def hip_sources():
     return srcs
 
 
+def _deps(src, seen=None):
+    """src plus every quoted #include it reaches (include dirs: csrc/, include/)."""
+    seen = set() if seen is None else seen
+    if src in seen or not os.path.exists(src):
+        return seen
+    seen.add(src)
+    with open(src, errors="replace") as f:
+        for inc in re.findall(r'#include\s+"([^"]+)"', f.read()):
+            for d in (os.path.dirname(src), CSRC, os.path.join(ROOT, "include")):
+                cand = os.path.join(d, inc)
+                if os.path.exists(cand):
+                    _deps(cand, seen)
+                    break
+    return seen
+
+
 def build_hip(force=False, jobs=None):
-    """Compile each .hip TU to an object in parallel, then link the shared library."""
+    """Compile each stale .hip TU (own source or any header it reaches changed) to an object in
+    parallel, then link the shared library."""
     from concurrent.futures import ThreadPoolExecutor
     out = os.path.join(HERE, "_akshar_hip.so")
     srcs = [os.path.join(CSRC, n) for n in sorted(os.listdir(CSRC)) if n.endswith((".hip", ".cpp"))]
@@ -60,8 +78,9 @@ def build_hip(force=False, jobs=None):
     for src in srcs:
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        cmds.append(common + ["-c", "-o", obj, src])
-    jobs = jobs or min(len(cmds), max(1, (os.cpu_count() or 4)), 16)
+        if force or _stale(obj, sorted(_deps(src))):
+            cmds.append(common + ["-c", "-o", obj, src])
+    jobs = jobs or min(max(len(cmds), 1), max(1, (os.cpu_count() or 4)), 16)
     with ThreadPoolExecutor(jobs) as ex:
         for f in [ex.submit(_run, c) for c in cmds]:
             f.result()

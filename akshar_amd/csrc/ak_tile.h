@@ -145,7 +145,10 @@ __device__ __noinline__ uint64_t fallback_row(const TileArgs &ta, uint64_t r, co
     sc.status = 0;
     uint64_t cnt = process_row<OP_BPE, FLAGS, EMIT>(ta.ra, r, fast, sfast, &sc, emit_base);
     if (sc.status & ST_SLOW) {
-        const uint32_t region = wave_gid % SLOW_THREADS;
+        // one region per (wave, lane): lanes of one wave never wait on each other (a divergent spin
+        // on a lock held by a sibling lane would never converge); SLOW_THREADS is a multiple of 64
+        static_assert(SLOW_THREADS % 64 == 0, "pool regions must tile whole waves");
+        const uint32_t region = (wave_gid * 64u + (uint32_t)w_lane()) % SLOW_THREADS;
         while (__hip_atomic_exchange(ta.locks + region, 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u)
             w_sleep();
         const SlowPool &P = ta.ra.pool;

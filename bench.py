@@ -135,18 +135,21 @@ def main():
     toks = job_ids * args.steps / elapsed
 
     # dominant kernel: per-launch algorithmic bytes / its average launch duration
-    kern = max(("count", "emit"), key=lambda k: prof[k][0])
+    kern = max(("count", "emit", "tiles"), key=lambda k: prof[k][0])
     k_ms, k_n = prof[kern]
     avg_s = k_ms / max(k_n, 1) / 1e3
     read_bytes = nbytes + 8 * (rows + 1)
+    # count pass writes a u32 per row; emit / single-pass tiles write ids + row offsets
     write_bytes = 4 * rows if kern == "count" else 4 * n_ids + 8 * (rows + 1)
     algo = read_bytes + write_bytes
     achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
+    kname = {"count": "k_rows_fast<OP_BPE,3,false> (count pass)", "emit": "k_rows_fast<OP_BPE,3,true> (emit pass)",
+             "tiles": "k_bpe_tiles<3> (tile-cooperative single pass)"}[kern]
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                "kernel": "k_rows_fast<OP_BPE,3,%s> (%s pass)" % ("true" if kern == "emit" else "false", kern),
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": kname,
                 "kernel_avg_ms": round(avg_s * 1e3, 3), "algorithmic_bytes_per_launch": int(algo),
-                "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in prof.items()}}
+                "read_frac": round(read_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0,
+                "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in prof.items() if v[1]}}
 
     cpu = None
     if rank == 0 and not args.no_cpu:

@@ -53,8 +53,10 @@ def test_switches_golden(golden, gpacked, eng, flags, key):
     assert _bad(golden, key, rows_runs(_cpu(ends), _cpu(labels), _cpu(oo))) == []
 
 
-def test_bpe_golden(golden, gpacked, eng, bpe_model):
-    ids, oo = eng.BPE(bpe_model).encode_batch(*gpacked)
+@pytest.mark.parametrize("path", [1, 0])
+def test_bpe_golden(golden, gpacked, eng, bpe_model, path):
+    """path 1 = tile-cooperative single-pass kernel, 0 = one lane per row (count/scan/emit)."""
+    ids, oo = eng.BPE(bpe_model).encode_batch(*gpacked, path=path)
     assert _bad(golden, "bpe", rows_ints(_cpu(ids), _cpu(oo))) == []
 
 
@@ -93,10 +95,11 @@ def test_synthetic_vs_oracle(eng, bpe_model, spm_model, kind, n, seed):
     re_, rl, ro = O.switches_batch(*ob, flags=3)
     assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
     assert np.array_equal(_cpu(ends).astype(np.uint32), re_) and np.array_equal(_cpu(labels), rl)
-    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(*ob)
-    assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
-    assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    for path in (1, 0):
+        ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, path=path)
+        assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+        assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
     ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
     ref, ro = O.OracleSPM(spm_model).encode_batch(*ob)
     assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
@@ -119,9 +122,10 @@ def test_long_rows_take_the_slow_path(eng, bpe_model, spm_model):
              "१२३४५६७८९०" * 30, "ज्ञ" * 100 + " " + "hello " * 100]
     gb, go = eng.pack(texts)
     ob = O.pack(texts)
-    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(*ob)
-    assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
+    for path in (1, 0):
+        ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, path=path)
+        assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
     ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
     ref, ro = O.OracleSPM(spm_model).encode_batch(*ob)
     assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
