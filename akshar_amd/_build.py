@@ -73,6 +73,8 @@ def build_hip(force=False, jobs=None):
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     common = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include"),
               "-I", CSRC, "-Wall", "-Wno-unused-function"]
+    if os.environ.get("AK_HIP_REMARKS"):  # per-kernel VGPR / SGPR / LDS / scratch / occupancy report
+        common.append("-Rpass-analysis=kernel-resource-usage")
     objs = []
     cmds = []
     for src in srcs:

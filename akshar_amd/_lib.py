@@ -14,7 +14,9 @@ AK_NORM_CLEAN = 2
 AK_RAW = -1
 AK_ROW_BAD_UTF8 = 1
 AK_ROW_LIMIT = 4
-AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4, "tiles": 5}
+AK_TILE_PASSES = ("stage", "decode_nfc_map", "elongation", "hf_nfkc", "pretok", "bpe_merge", "fallback_count",
+                  "compact_ids", "fallback_emit", "loop")
+AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4, "tiles": 5, "copy": 6}
 
 P = ctypes.c_void_p
 U64 = ctypes.c_uint64
@@ -27,6 +29,7 @@ _LIB = None
 SIGNATURES = {
     "ak_last_error": (ctypes.c_char_p, []),
     "ak_version": (I32, []),
+    "ak_selftest": (I32, []),
     "ak_ws_create": (I32, [ctypes.POINTER(P)]),
     "ak_ws_free": (None, [P]),
     "ak_ws_set_tiling": (I32, [P, I32, I32]),
@@ -43,6 +46,7 @@ SIGNATURES = {
     "ak_profile_enable": (I32, [I32]),
     "ak_profile_read": (I32, [I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
     "ak_profile_reset": (None, []),
+    "ak_profile_tile_passes": (I32, [P, ctypes.POINTER(U64), I32]),
     "ak_normalize_cap": (U64, [U64, U64]),
     "ak_segment_cap": (U64, [U64, U64]),
     "ak_bpe_encode_cap": (U64, [U64, U64]),

@@ -233,13 +233,28 @@ extern "C" int ak_ws_check(ak_ws *w) {
     if (!w->tile_misc) return AK_OK;
     uint32_t err = 0;
     HIP_TRY(hipMemcpy(&err, w->tile_misc + 1, 4, hipMemcpyDeviceToHost));
-    return err ? fail(AK_ERR_HIP, "tile look-back gave up waiting (device timeout)") : AK_OK;
+    return err ? fail(AK_ERR_HIP, "tile staging slot overflow (a row produced more ids than bytes + 2)") : AK_OK;
+}
+
+namespace ak { int selftest_wave(); }
+extern "C" int ak_selftest(void) { return ak::selftest_wave(); }
+
+extern "C" int ak_profile_tile_passes(ak_ws *w, uint64_t *cycles, int n) {
+    if (!w || !cycles || n < 0) return fail(AK_ERR_ARG, "ak_profile_tile_passes: bad argument");
+    memset(cycles, 0, sizeof(uint64_t) * (size_t)n);
+    if (!w->tile_passprof) return 0;
+    const int k = std::min(n, (int)AK_TILE_NPASS);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(cycles, w->tile_passprof, (size_t)k * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(w->tile_passprof, 0, AK_TILE_NPASS * 8));
+    return k;
 }
 
 extern "C" void ak_ws_free(ak_ws *w) {
     if (!w) return;
-    (void)hipFree(w->tile_status);
+    (void)hipFree(w->stage);
     (void)hipFree(w->tile_misc);
+    (void)hipFree(w->tile_passprof);
     (void)hipFree(w->counts);
     (void)hipFree(w->flags);
     (void)hipFree(w->slow_list);
@@ -374,7 +389,7 @@ static int dispatch(int op, int flags, ak_ws *w, const RowArgs &a, uint64_t *out
         case OP_SEGMENT: return launch_segment(flags, w, a, out_offs, st);
         case OP_SWITCHES: return launch_switches(flags, w, a, out_offs, st);
         case OP_BPE:
-            return w->bpe_path == 1 ? launch_bpe_tiles(flags, w, a, out_offs, st) : launch_bpe(flags, w, a, out_offs, st);
+            return w->bpe_path == 1 && flags == 3 ? launch_bpe_tiles(flags, w, a, out_offs, st) : launch_bpe(flags, w, a, out_offs, st);
         default: return launch_spm(flags, w, a, out_offs, st);
     }
 }

@@ -40,9 +40,10 @@ struct AkWs {
     void *pool_mem = nullptr;
     SlowPool pool{};
     // tile-cooperative BPE path
-    uint64_t *tile_status = nullptr;
-    uint64_t cap_tiles = 0;
-    uint32_t *tile_misc = nullptr;  // [0] ticket, [1] err, [64..64+SLOW_THREADS) pool locks
+    uint32_t *stage = nullptr;      // staged ids, slot of row r at offs[r] + 2 r
+    uint64_t cap_stage = 0;
+    uint32_t *tile_misc = nullptr;  // [1] slot-overflow flag, [64..64+SLOW_THREADS) pool locks
+    uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 8;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (v1)
 };

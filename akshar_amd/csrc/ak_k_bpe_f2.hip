@@ -1,12 +1,15 @@
-// ak_k_bpe.hip — kernel instantiations for one op (a separate TU so hipcc builds ops in parallel).
+// ak_k_bpe_f2.hip — one-lane-per-row BPE kernels for flags 2 (normalize_roman=False) and the
+// flags dispatcher for the row path.
 #include "ak_internal.h"
 
 namespace ak {
 
+int launch_bpe_f3(AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+
 int launch_bpe(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st) {
     switch (flags) {
         case 2: return launch_rows<OP_BPE, 2>(w, a, out_offs, st);
-        case 3: return launch_rows<OP_BPE, 3>(w, a, out_offs, st);
+        case 3: return launch_bpe_f3(w, a, out_offs, st);
         default: break;
     }
     return set_error(AK_ERR_UNSUPPORTED, "bpe: unsupported flags");

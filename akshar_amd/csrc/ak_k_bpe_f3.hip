@@ -1,0 +1,11 @@
+// ak_k_bpe_f3.hip — one-lane-per-row BPE kernels for flags 3 (normalize_text defaults). Each
+// (op, flags) instantiation is its own TU so hipcc builds them in parallel.
+#include "ak_internal.h"
+
+namespace ak {
+
+int launch_bpe_f3(AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st) {
+    return launch_rows<OP_BPE, 3>(w, a, out_offs, st);
+}
+
+}  // namespace ak

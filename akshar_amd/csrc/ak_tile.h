@@ -9,8 +9,13 @@
 //   H  HF NFKC: compat spaces -> ' ', HF-ccc segments checked by their leader
 //   P  Whitespace pre-tokenizer: word starts -> V, word-end tags on W, spaces -> DEAD
 //   B  lane per word: cps -> ids, merge_all (lowest rank, leftmost) in place in W
-//   F  weighted compaction W -> ids (B -> <s>, E -> </s>), decoupled look-back for the tile's
-//      output base, row offsets written from the sentinels' positions
+//   F  weighted compaction W -> ids (B -> <s>, E -> </s>) into the tile's staging slot, per-row
+//      token counts from the sentinels' positions
+// Tiles never wait on each other: tile t stages its ids contiguously at stage[offs[r0] + 2 r0]
+// (a row's ids never exceed its bytes + 2, so the slots cannot overlap) and writes per-row
+// counts; the launcher then scans the counts into row offsets and a copy kernel moves each
+// tile's ids to their final place (ak_k_bpe_tiles.hip). No look-back, no ticket: on MI355X every
+// inter-tile hop would be a cross-XCD L2 round trip.
 // Rows that cannot take the cooperative path (invalid UTF-8, an NFC segment over T_SEG code points,
 // a changed HF segment, or bytes beyond the tile buffer) run the sequential row pipeline
 // (ak_dev.h, process_row) in one lane of the same wave, so every row is computed exactly once.
@@ -22,11 +27,10 @@
 
 namespace ak {
 
-constexpr int T_BCAP = 2048;  // staged bytes per tile (rows past it fall back)
+constexpr int T_BCAP = 1024;  // staged bytes per tile (rows past it fall back); sized for 4 blocks/CU
 constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
 constexpr int T_E = T_BCAP + 2 * T_MAXR + 64;
 constexpr int T_SEG = 16;     // NFC segment length handled in the cooperative pass
-constexpr int T_TPB = 8;      // tiles per ticket
 constexpr int T_FBSEG = 16;   // fallback lane buffers (private); larger rows use the locked pool
 constexpr int T_FBWORD = 64;
 
@@ -36,8 +40,6 @@ constexpr uint16_t V_B = 0xFFFE;
 constexpr uint16_t V_E = 0xFFFF;
 constexpr uint16_t V_SPECIAL = 0xFFFC;  // values >= this are sentinels / dead
 constexpr uint16_t WEND = 0x8000;       // word-end tag on a code point (all are <= U+3000)
-
-constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_MASK = (1ull << 62) - 1;
 
 struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
@@ -50,17 +52,64 @@ struct TileWaveMem {
     uint8_t fbstat[T_MAXR];
     uint8_t hfbad[T_MAXR];
     uint16_t wrow[T_MAXR + 1];  // W index of each coop row's B / FB sentinel
+    uint32_t rowop[T_MAXR + 1]; // tile-relative output position of each row's first id
 };
 
 struct TileArgs {
-    RowArgs ra;           // in, offs, n, out (ids), cap, out_offs, row_status, bpe, single_fast
-    uint64_t *status;     // look-back words, one per tile, zeroed before the launch
-    uint32_t *ticket;     // tile ticket counter, zeroed before the launch
+    RowArgs ra;           // in, offs, n, row_status, bpe, single_fast; out = stage (u32), cap = its size
+    uint32_t *counts;     // per-row token counts (incl. <s> </s>)
     uint32_t *locks;      // SLOW_THREADS pool-region locks (zeroed once)
-    uint32_t *err;        // set if a look-back spin gave up
+    uint32_t *err;        // set if a tile's ids exceeded its staging slot (cannot happen: checked)
+    uint64_t *passprof;   // optional: device cycles per pass, summed over waves (T_NPASS entries)
     uint64_t ntiles;
     int rows;             // R
 };
+
+// pass profile slots (ak_profile_tile_passes)
+enum { TP_STAGE, TP_D, TP_E, TP_H, TP_P, TP_B, TP_FBC, TP_F, TP_FBE, TP_LOOP, T_NPASS };
+
+struct PassClock {  // wave-uniform; lane 0 flushes once per wave
+    uint64_t acc[T_NPASS];
+    uint64_t last;
+    bool on;
+    __device__ __forceinline__ void init(bool enabled) {
+        on = enabled;
+        for (int i = 0; i < T_NPASS; ++i) acc[i] = 0;
+        last = on ? clock64() : 0;
+    }
+    __device__ __forceinline__ void mark(int k) {
+        if (!on) return;
+        const uint64_t now = clock64();
+        acc[k] += now - last;
+        last = now;
+    }
+    __device__ __forceinline__ void flush(uint64_t *dst) {
+        if (!on || w_lane() != 0) return;
+        for (int i = 0; i < T_NPASS; ++i) atomicAdd((unsigned long long *)(dst + i), (unsigned long long)acc[i]);
+    }
+};
+
+// Hot per-code-point word for the cooperative passes (LDS, cp < FAST_N; built from the full
+// property record by hot_of): normalize_text map + the NFC / HF-NFC quick-check bits + HF classes.
+constexpr uint32_t H_STABLE = 1u << 16;  // NFC-stable: ccc 0, NFC(c) == c, never a composition second
+constexpr uint32_t H_DECOMP = 1u << 17;  // has a canonical decomposition
+constexpr uint32_t H_NT = 1u << 18;      // composition second or ccc 0 (a mark that is one triggers NFC)
+constexpr uint32_t H_HFST = 1u << 19;    // HF-stable: HF ccc 0 and never a composition second
+constexpr uint32_t H_HNT = 1u << 20;     // composition second or HF ccc 0
+constexpr uint32_t H_HFSPACE = 1u << 21; // HF NFKC maps it to U+0020
+constexpr int H_CLS_SHIFT = 22;          // HF pre-tokenizer class (2 bits)
+
+__device__ __forceinline__ uint32_t hot_of(uint2 pr) {
+    return p_normmap(pr) | (p_stable(pr) ? H_STABLE : 0u) | (p_decomp(pr) ? H_DECOMP : 0u) |
+           ((p_second(pr) || p_ccc(pr) == 0) ? H_NT : 0u) | ((p_ccc_hf(pr) == 0 && !p_second(pr)) ? H_HFST : 0u) |
+           ((p_second(pr) || p_ccc_hf(pr) == 0) ? H_HNT : 0u) | (p_hfspace(pr) ? H_HFSPACE : 0u) |
+           ((uint32_t)p_hfclass(pr) << H_CLS_SHIFT);
+}
+__device__ __forceinline__ uint32_t hot(const uint32_t *H, uint32_t cp) {
+    return cp < FAST_N ? H[cp] : hot_of(prop_global(cp));
+}
+
+__device__ __forceinline__ int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }
 
 __device__ __forceinline__ uint32_t lds_decode(const uint8_t *B, int p, int e, int &len) {
     const uint32_t c = B[p];
@@ -171,46 +220,9 @@ __device__ __noinline__ uint64_t fallback_row(const TileArgs &ta, uint64_t r, co
     return cnt;
 }
 
-// Decoupled look-back: returns the exclusive prefix (tokens before tile t).
-__device__ __forceinline__ uint64_t tile_lookback(const TileArgs &ta, uint64_t t, uint64_t total) {
-    const int lane = w_lane();
-    if (t == 0) {
-        if (lane == 0) w_atomic_store64(ta.status, LB_INC | total);
-        return 0;
-    }
-    if (lane == 0) w_atomic_store64(ta.status + t, LB_AGG | total);
-    uint64_t prefix = 0;
-    int64_t j = (int64_t)t - 1;
-    uint32_t spins = 0;
-    for (;;) {
-        const int64_t q = j - lane;
-        const uint64_t s = q >= 0 ? w_atomic_load64(ta.status + q) : LB_INC;
-        const uint64_t flag = s & ~LB_MASK;
-        const uint64_t inc = w_ballot(flag == LB_INC);
-        const uint64_t zero = w_ballot(flag == 0);
-        const int first_inc = inc ? __builtin_ctzll(inc) : 64;
-        const uint64_t upto = first_inc >= 63 ? ~0ull : ((2ull << first_inc) - 1);
-        if (zero & upto) {  // a predecessor before the nearest inclusive has not published yet
-            if (++spins > (1u << 26)) {
-                if (lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            w_sleep();
-            continue;
-        }
-        const uint64_t mine = (uint64_t)lane <= (uint64_t)first_inc ? (s & LB_MASK) : 0ull;
-        const uint64_t lsum = w_sum64(mine);
-        prefix += lsum;
-        if (first_inc < 64) break;
-        j -= 64;
-    }
-    if (lane == 0) w_atomic_store64(ta.status + t, LB_INC | ((prefix + total) & LB_MASK));
-    return prefix;
-}
-
 template <int FLAGS>
-__device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, const uint16_t *sfast, TileWaveMem &M,
-                         uint32_t wave_gid) {
+__device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, const uint32_t *H, const uint16_t *sfast,
+                         TileWaveMem &M, uint32_t wave_gid, PassClock &pc) {
     const int lane = w_lane();
     const uint64_t lt = w_lanemask_lt();
     const RowArgs &a = ta.ra;
@@ -219,10 +231,10 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     const uint64_t r1 = r0 + (uint64_t)ta.rows < a.n ? r0 + (uint64_t)ta.rows : a.n;
     const int nr = (int)(r1 - r0);
     const uint64_t myoff = lane <= nr ? a.offs[r0 + lane] : 0ull;
-    const uint64_t S0 = w_shfl(myoff, 0);
+    const uint64_t S0 = w_bcast(myoff, 0);
     const bool fits = lane >= 1 && lane <= nr && (myoff - S0) <= (uint64_t)T_BCAP;
     const int k = w_popc(w_ballot(fits));  // rows 0..k-1 take the cooperative path
-    const uint64_t S1 = w_shfl(myoff, k);
+    const uint64_t S1 = w_bcast(myoff, k);
     const uint64_t a0 = S0 & ~15ull;
     {
         const uint64_t nblk = (S1 - a0 + 15) / 16;
@@ -233,17 +245,62 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     if (lane < T_MAXR) { M.fbslot[lane] = 0xFF; M.hfbad[lane] = 0; }
     w_sync();
 
+    pc.mark(TP_STAGE);
     // ---------------- pass D: decode + NFC + map/filter -> V
     uint8_t *FL = (uint8_t *)M.w;  // NFC leader flags by byte position (W is free until pass E)
     uint32_t vpos = 0;
     uint32_t nfb = 0;
     for (int i = 0; i < k; ++i) {
-        const int s = (int)(w_shfl(myoff, i) - a0), e = (int)(w_shfl(myoff, i + 1) - a0);
+        const int s = (int)(w_bcast(myoff, i) - a0), e = (int)(w_bcast(myoff, i + 1) - a0);
         const uint32_t vstart = vpos;
         if (lane == 0) M.v[vpos] = V_B;
         ++vpos;
         bool rowbad = false;
-        for (int base = s; base < e; base += 64) {
+        // Fast path: if no code point of the row trips the NFC quick check (a decomposable char, or
+        // a non-stable char that is a composition second / a starter / follows another non-stable
+        // char or the row start), NFC is the identity on the row (no NFD change, no reordering,
+        // nothing composes) and every char maps on its own: one ballot-compacted write per lane.
+        bool complex = false;
+        {
+            bool carry_ns = true;  // the char before the first one: the row start blocks like a mark
+            for (int base = s; base < e; base += 64) {
+                const int p = base + lane;
+                const bool in = p < e;
+                const uint32_t byte = in ? M.bytes[p] : 0u;
+                const bool lead = in && (byte & 0xC0u) != 0x80u;
+                bool bad = in && p == s && !lead;
+                uint32_t h = 0;
+                if (lead) {
+                    int len;
+                    const uint32_t cp = lds_decode(M.bytes, p, e, len);
+                    if (cp == 0xFFFFFFFFu) bad = true;
+                    else h = hot(H, cp);
+                }
+                if (w_ballot(bad)) { rowbad = true; break; }
+                const uint64_t LEADS = w_ballot(lead);
+                const uint64_t NS = w_ballot(lead && !(h & H_STABLE));
+                const uint64_t pm = LEADS & lt;
+                const bool prev_ns = pm ? ((NS >> msb64(pm)) & 1ull) != 0 : carry_ns;
+                bool trig = lead && !(h & H_STABLE) && ((h & H_NT) || prev_ns || (h & H_DECOMP));
+                if (lead && (h & H_STABLE) && (h & H_DECOMP)) {
+                    // a decomposable starter (e.g. U+0929) is its own NFC image unless marks follow
+                    int len1, l2;
+                    (void)lds_decode(M.bytes, p, e, len1);
+                    if (p + len1 < e) {
+                        const uint32_t c2 = lds_decode(M.bytes, p + len1, e, l2);
+                        trig = c2 == 0xFFFFFFFFu || !(hot(H, c2) & H_STABLE);
+                    }
+                }
+                if (w_ballot(trig)) { complex = true; break; }
+                if (LEADS) carry_ns = ((NS >> msb64(LEADS)) & 1ull) != 0;
+                const uint32_t mv = h & 0xFFFFu;
+                const uint64_t KM = w_ballot(mv != 0u);
+                if (mv) M.v[vpos + (uint32_t)w_popc(KM & lt)] = (uint16_t)mv;
+                vpos += (uint32_t)w_popc(KM);
+            }
+        }
+        if (complex) vpos = vstart + 1;
+        for (int base = s; complex && base < e; base += 64) {
             const int p = base + lane;
             const bool in = p < e;
             const uint32_t byte = in ? M.bytes[p] : 0u;
@@ -342,6 +399,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     const uint32_t vlen = vpos;
     w_sync();
 
+    pc.mark(TP_D);
     // ---------------- pass E: remove_elongations V -> W (+ row sentinel positions)
     uint32_t wlen = 0, rows_seen = 0;
     for (uint32_t base = 0; base < vlen; base += 64) {
@@ -365,16 +423,35 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     if (lane == 0) M.wrow[rows_seen] = (uint16_t)wlen;
     w_sync();
 
-    // ---------------- pass H: HF NFKC (compat spaces -> ' ', HF-ccc segments checked)
-    for (uint32_t base = 0; base < wlen; base += 64) {
-        const uint32_t kk = base + lane;
-        if (kk < wlen) {
-            const uint16_t x = M.w[kk];
-            if (x < V_SPECIAL && p_hfspace(prop(fast, x))) M.w[kk] = 0x20;
+    pc.mark(TP_E);
+    // ---------------- pass H: HF NFKC (compat spaces -> ' ', then the HF-NFC quick check; the full
+    // per-segment check only runs on tiles where some char trips it)
+    bool hf_any = false;
+    {
+        bool carry_b = true;
+        for (uint32_t base = 0; base < wlen; base += 64) {
+            const uint32_t kk = base + lane;
+            const bool in = kk < wlen;
+            const uint16_t x = in ? M.w[kk] : V_DEAD;
+            const bool special = x >= V_SPECIAL;
+            uint32_t h = special ? 0u : hot(H, x);
+            if (in && !special && (h & H_HFSPACE)) { M.w[kk] = 0x20; h = hot(H, 0x20); }
+            const bool nst = in && !special && !(h & H_HFST);
+            const uint64_t B = w_ballot(in && (special || nst));
+            const bool prev_b = lane ? ((B >> (lane - 1)) & 1ull) != 0 : carry_b;
+            bool trig = nst && ((h & H_HNT) || prev_b || (h & H_DECOMP));
+            if (in && !special && !nst && (h & H_DECOMP) && kk + 1 < wlen) {
+                // a decomposable HF-starter is unchanged unless an HF-non-starter follows it
+                const uint16_t y = M.w[kk + 1];
+                const uint32_t hy = y < V_SPECIAL ? hot(H, y) : H_HFST;  // compat spaces become ' '
+                trig = !(hy & (H_HFST | H_HFSPACE));
+            }
+            if (w_ballot(trig)) hf_any = true;
+            carry_b = ((B >> 63) & 1ull) != 0;
         }
     }
     w_sync();
-    for (uint32_t base = 0; base < wlen; base += 64) {
+    for (uint32_t base = 0; hf_any && base < wlen; base += 64) {
         const uint32_t kk = base + lane;
         bool bad = false;
         if (kk + 1 < wlen) {
@@ -405,7 +482,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         }
     }
     w_sync();
-    for (int ri = 0; ri < (int)rows_seen; ++ri) {
+    for (int ri = 0; hf_any && ri < (int)rows_seen; ++ri) {
         if (!M.hfbad[ri]) continue;  // uniform (LDS value)
         const uint32_t b = M.wrow[ri], e2 = M.wrow[ri + 1];
         for (uint32_t q = b + 1 + lane; q < e2; q += 64) M.w[q] = V_DEAD;
@@ -420,6 +497,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     }
     w_sync();
 
+    pc.mark(TP_H);
     // ---------------- pass P: Whitespace pre-tokenizer (\w+ | [^\w\s]+)
     uint32_t nw = 0;
     for (uint32_t base = 0; base < wlen; base += 64) {
@@ -427,7 +505,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         const bool in = kk < wlen;
         auto cls = [&](uint16_t x) -> int {
             if (x >= V_SPECIAL) return HF_S;
-            return p_hfclass(prop(fast, (uint32_t)(x & 0x7FFF)));
+            return (int)((hot(H, (uint32_t)(x & 0x7FFF)) >> H_CLS_SHIFT) & 3u);
         };
         const uint16_t x = in ? M.w[kk] : V_DEAD;
         const int c0 = cls(x);
@@ -444,6 +522,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         w_sync();
     }
 
+    pc.mark(TP_P);
     // ---------------- pass B: lane per word, merge_all in place
     for (uint32_t wb = 0; wb < nw; wb += 64) {
         const uint32_t j = wb + lane;
@@ -463,6 +542,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     }
     w_sync();
 
+    pc.mark(TP_B);
     // ---------------- fallback rows: count
     uint32_t fbst = 0;
     uint64_t fbcnt = 0;
@@ -470,40 +550,16 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     if ((uint32_t)lane < nfb) { M.fbcount[lane] = (uint32_t)fbcnt; M.fbstat[lane] = (uint8_t)fbst; }
     w_sync();
 
-    // ---------------- pass F1: tile total
+    pc.mark(TP_FBC);
+    // ---------------- pass F: weighted compaction W -> staged ids, row start positions
     auto weight = [&](uint16_t x, uint32_t ridx) -> uint32_t {
         if (x == V_FB) return M.fbcount[M.fbslot[ridx]];
         return x == V_DEAD ? 0u : 1u;
     };
-    uint64_t T = 0;
-    rows_seen = 0;
-    for (uint32_t base = 0; base < wlen; base += 64) {
-        const uint32_t kk = base + lane;
-        const bool in = kk < wlen;
-        const uint16_t x = in ? M.w[kk] : V_DEAD;
-        const bool isrow = in && (x == V_B || x == V_FB);
-        const uint64_t rm = w_ballot(isrow);
-        const uint32_t ridx = rows_seen + (uint32_t)w_popc(rm & lt);
-        uint32_t tot;
-        (void)w_exscan(in ? weight(x, ridx) : 0u, &tot);
-        T += tot;
-        rows_seen += (uint32_t)w_popc(rm);
-    }
-    const uint64_t Tcoop = T;
-    {
-        uint32_t tail = 0;
-        if ((uint32_t)lane < nfb && M.fbrow[lane] >= k) tail = M.fbcount[lane];
-        uint32_t tt;
-        (void)w_exscan(tail, &tt);
-        T += tt;
-    }
-
-    // ---------------- look-back
-    const uint64_t base_out = tile_lookback(ta, t, T);
-
-    // ---------------- pass F2: write ids + row offsets
-    uint64_t *oo = const_cast<uint64_t *>(a.out_offs);
-    uint64_t pos = base_out;
+    const uint64_t sbase = S0 + 2 * r0;  // this tile's staging slot
+    const uint64_t scap = (S1 - S0) + 2 * (uint64_t)k + (w_bcast(myoff, nr) - S1) + 2 * (uint64_t)(nr - k);
+    uint32_t *stage = (uint32_t *)a.out + sbase;
+    uint32_t pos = 0;
     rows_seen = 0;
     for (uint32_t base = 0; base < wlen; base += 64) {
         const uint32_t kk = base + lane;
@@ -514,40 +570,41 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         const uint32_t ridx = rows_seen + (uint32_t)w_popc(rm & lt);
         const uint32_t wgt = in ? weight(x, ridx) : 0u;
         uint32_t tot;
-        const uint32_t ex = w_exscan(wgt, &tot);
-        const uint64_t op = pos + ex;
-        uint32_t* ids = (uint32_t *)a.out;
+        const uint32_t op = pos + w_exscan(wgt, &tot);
+        const bool fits = op < scap;
+        if (isrow) M.rowop[ridx] = op;
         if (x == V_B) {
-            if (op < a.cap) ids[op] = m.bos;
-            oo[r0 + ridx] = op;
+            if (fits) stage[op] = m.bos;
         } else if (x == V_FB) {
-            oo[r0 + ridx] = op;
-            M.fbbase[M.fbslot[ridx]] = op;
+            M.fbbase[M.fbslot[ridx]] = sbase + op;
         } else if (x == V_E) {
-            if (op < a.cap) ids[op] = m.eos;
+            if (fits) stage[op] = m.eos;
         } else if (in && x != V_DEAD) {
-            if (op < a.cap) ids[op] = x;
+            if (fits) stage[op] = x;
         }
         pos += tot;
         rows_seen += (uint32_t)w_popc(rm);
     }
-    {
+    {   // rows past the tile buffer follow the cooperative rows
         uint32_t tail = 0;
         const bool istail = (uint32_t)lane < nfb && M.fbrow[lane] >= k;
         if (istail) tail = M.fbcount[lane];
         uint32_t tt;
         const uint32_t ex = w_exscan(tail, &tt);
         if (istail) {
-            const uint64_t op = base_out + Tcoop + ex;
-            M.fbbase[lane] = op;
-            oo[r0 + M.fbrow[lane]] = op;
+            M.fbbase[lane] = sbase + pos + ex;
+            M.rowop[M.fbrow[lane]] = pos + ex;
         }
+        pos += tt;
     }
-    if (lane == 0 && r1 == a.n) oo[a.n] = base_out + T;
+    if (lane == 0) M.rowop[nr] = pos;
+    if (pos > scap && lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     w_sync();
+    if (lane < nr) ta.counts[r0 + lane] = M.rowop[lane + 1] - M.rowop[lane];
+    pc.mark(TP_F);
 
-    // ---------------- fallback rows: emit
-    if ((uint32_t)lane < nfb) {
+    // ---------------- fallback rows: emit into the staging slot
+    if ((uint32_t)lane < nfb && pos <= scap) {
         uint32_t st2;
         (void)fallback_row<FLAGS, true>(ta, r0 + M.fbrow[lane], fast, sfast, M.fbbase[lane], wave_gid, st2);
     }
@@ -558,20 +615,19 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         a.row_status[r0 + lane] = st3;
     }
     w_sync();
+    pc.mark(TP_FBE);
 }
 
 template <int FLAGS>
-__device__ void bpe_tiles_wave(const TileArgs &ta, const uint2 *fast, const uint16_t *sfast, TileWaveMem &M,
-                               uint32_t wave_gid) {
-    const int lane = w_lane();
-    for (;;) {
-        uint32_t t0 = 0;
-        if (lane == 0) t0 = w_atomic_add32(ta.ticket, (uint32_t)T_TPB);
-        t0 = w_shfl(t0, 0);
-        if ((uint64_t)t0 >= ta.ntiles) break;
-        const uint64_t t1 = (uint64_t)t0 + T_TPB < ta.ntiles ? (uint64_t)t0 + T_TPB : ta.ntiles;
-        for (uint64_t t = t0; t < t1; ++t) bpe_tile<FLAGS>(ta, t, fast, sfast, M, wave_gid);
+__device__ void bpe_tiles_wave(const TileArgs &ta, const uint2 *fast, const uint32_t *H, const uint16_t *sfast,
+                               TileWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
+    PassClock pc;
+    pc.init(ta.passprof != nullptr);
+    for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {  // static stride: tiles are near-equal
+        pc.mark(TP_LOOP);
+        bpe_tile<FLAGS>(ta, t, fast, H, sfast, M, wave_gid, pc);
     }
+    pc.flush(ta.passprof);
 }
 
 }  // namespace ak

@@ -43,6 +43,9 @@ inline T w_shfl(T v, int src) {
     __builtin_memcpy(&r, &y, sizeof(T));
     return r;
 }
+// value of lane src (src wave-uniform)
+template <typename T>
+inline T w_bcast(T v, int src) { return w_shfl(v, src); }
 // exclusive prefix sum over lanes; *total gets the wave sum
 inline uint32_t w_exscan(uint32_t v, uint32_t *total) {
     t_wave->slot[t_lane] = v;
@@ -67,6 +70,10 @@ inline uint32_t w_atomic_add32(uint32_t *p, uint32_t v) {
 }
 inline void w_sleep() {}
 }  // namespace ak
+inline uint64_t clock64() { return 0; }
+inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) {
+    return reinterpret_cast<std::atomic<unsigned long long> *>(p)->fetch_add(v, std::memory_order_relaxed);
+}
 
 #else
 #include <hip/hip_runtime.h>
@@ -84,16 +91,35 @@ __device__ __forceinline__ void w_sync() {
 __device__ __forceinline__ uint64_t w_ballot(bool p) { return (uint64_t)__ballot(p); }
 template <typename T>
 __device__ __forceinline__ T w_shfl(T v, int src) { return __shfl(v, src, 64); }
-__device__ __forceinline__ uint32_t w_exscan(uint32_t v, uint32_t *total) {
-    const int lane = w_lane();
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
+// value of lane src (src wave-uniform): v_readlane into an SGPR, no LDS round trip
+template <typename T>
+__device__ __forceinline__ T w_bcast(T v, int src) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "");
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+    } else {
+        const uint64_t x = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, src);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), src);
+        return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
     }
-    *total = __shfl(x, 63, 64);
-    return x - v;
+}
+// inclusive wave64 prefix sum in DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31
+// across rows); all 64 lanes must be active
+__device__ __forceinline__ uint32_t w_inscan(uint32_t v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+    return (uint32_t)x;
+}
+__device__ __forceinline__ uint32_t w_exscan(uint32_t v, uint32_t *total) {
+    const uint32_t inc = w_inscan(v);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    return inc - v;
 }
 __device__ __forceinline__ uint64_t w_atomic_load64(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -156,7 +156,7 @@ import os as _os
 
 # 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (v1); AK_BPE_PATH overrides
 BPE_PATH = int(_os.environ.get("AK_BPE_PATH", "1"))
-TILE_BYTES = 1100  # target bytes of text per wave-tile (the tile buffer holds 2048)
+TILE_BYTES = 560  # target bytes of text per wave-tile (the tile buffer holds 1024)
 
 
 def tile_rows_for(n, nbytes):
@@ -264,3 +264,15 @@ def profile_read():
         check(_lib.lib().ak_profile_read(k, ctypes.byref(ms), ctypes.byref(n)), "ak_profile_read")
         res[name] = (ms.value, n.value)
     return res
+
+
+def profile_tile_passes(dev=None):
+    """{pass name: fraction of tile-kernel wave-cycles} since the last call (profiling enabled)."""
+    ws = workspace(dev)
+    n = len(_lib.AK_TILE_PASSES)
+    buf = (ctypes.c_uint64 * n)()
+    k = _lib.lib().ak_profile_tile_passes(ws, buf, n)
+    if k < 0:
+        check(k, "ak_profile_tile_passes")
+    tot = float(sum(buf)) or 1.0
+    return {name: round(buf[i] / tot, 4) for i, name in enumerate(_lib.AK_TILE_PASSES)} if k else {}

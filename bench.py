@@ -46,6 +46,15 @@ def parse():
     return ap.parse_args()
 
 
+def log(rank, msg):
+    """progress on stderr (the JSON line is the only stdout output)"""
+    if rank == 0:
+        print("[bench %.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def cpu_baseline(args, buf, offs):
     """The oracle (plain C, one thread) on the first --cpu-rows rows of rank 0's shard."""
     from akshar_amd.models import BPEModel
@@ -79,7 +88,9 @@ def main():
 
     from akshar_amd import engine, synth
     rows = args.rows
+    log(rank, "generating %d rows" % rows)
     buf, offs = synth.generate(synth.KIND_HINGLISH, rows, seed=SEED, first=rank * rows)
+    log(rank, "generated %.1f MB" % (offs[-1] / 1e6))
     nbytes = int(offs[-1])
     pad = np.zeros(((nbytes + 15) // 16) * 16 + 16, dtype=np.uint8)
     pad[:nbytes] = buf
@@ -91,9 +102,10 @@ def main():
     def step():
         return bpe.encode_batch(gbuf, goffs, cap=cap, nbytes=nbytes)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         ids, oo = step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        log(rank, "warmup %d done" % i)
     n_ids = int(ids.numel())
 
     engine.profile_enable(True)
@@ -102,13 +114,15 @@ def main():
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         ids, oo = step()
+        log(rank, "step %d enqueued" % i)
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     prof = engine.profile_read()
+    passes = engine.profile_tile_passes(local)
     engine.profile_enable(False)
 
     gather_ms = None
@@ -150,9 +164,12 @@ def main():
                 "kernel_avg_ms": round(avg_s * 1e3, 3), "algorithmic_bytes_per_launch": int(algo),
                 "read_frac": round(read_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0,
                 "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in prof.items() if v[1]}}
+    if passes:
+        roofline["tile_pass_cycle_frac"] = passes
 
     cpu = None
     if rank == 0 and not args.no_cpu:
+        log(rank, "timed region done (%.1f ms/step); CPU baseline" % (elapsed / args.steps * 1e3))
         cpu = cpu_baseline(args, buf, offs)
 
     if rank == 0:

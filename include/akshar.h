@@ -61,6 +61,9 @@ typedef struct ak_ws ak_ws;   /* device scratch, grows on demand; one per stream
 
 const char *ak_last_error(void);
 int ak_version(void);
+/* Device self-test of the wave64 primitives the tile kernels rely on (DPP prefix scan, readlane
+ * broadcast, ballot): AK_OK, or AK_ERR_HIP with the first mismatch in ak_last_error(). */
+int ak_selftest(void);
 
 int ak_ws_create(ak_ws **out);
 void ak_ws_free(ak_ws *ws);
@@ -68,7 +71,8 @@ void ak_ws_free(ak_ws *ws);
  * tile_rows rows per wave-tile, 1..16, default 8 — pick ~1.1 KB of text per tile), 0 = one lane
  * per row (count/scan/emit). */
 int ak_ws_set_tiling(ak_ws *ws, int bpe_path, int tile_rows);
-/* Synchronous health check after a batch: AK_ERR_HIP if a device-side wait timed out. */
+/* Synchronous health check after a batch: AK_ERR_HIP if the tile path flagged an internal
+ * overflow (a row producing more ids than its bytes + 2; never observed). */
 int ak_ws_check(ak_ws *ws);
 
 /* Replaces Tokenizer.from_file(path) (tokenizer.py:96-97) for the model cli.py:276-299 trains:
@@ -122,11 +126,20 @@ int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, cons
 #define AK_PROF_SCAN 2       /* row counts -> row offsets (three small kernels) */
 #define AK_PROF_EMIT 3       /* fast emit pass */
 #define AK_PROF_EMIT_SLOW 4  /* slow-path emit pass */
-#define AK_PROF_TILES 5      /* tile-cooperative BPE kernel (single pass) */
-#define AK_PROF_NKERNELS 6
+#define AK_PROF_TILES 5      /* tile-cooperative BPE kernel (ids into per-tile staging slots) */
+#define AK_PROF_COPY 6       /* staged ids -> final positions (tile path) */
+#define AK_PROF_NKERNELS 7
 int ak_profile_enable(int on);
 int ak_profile_read(int kernel, double *total_ms, uint64_t *launches);
 void ak_profile_reset(void);
+
+/* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each
+ * pass of the tile-cooperative BPE kernel since the last call, while profiling is enabled. Slots:
+ * 0 byte staging, 1 decode+NFC+map, 2 elongation, 3 HF NFKC, 4 pre-tokenizer, 5 BPE merges,
+ * 6 fallback count, 7 id compaction + counts, 8 fallback emit, 9 loop overhead.
+ * Returns the number of slots written (0 if the tile kernel has not run), or a negative error. */
+#define AK_TILE_NPASS 10
+int ak_profile_tile_passes(ak_ws *ws, uint64_t *cycles, int n);
 
 /* Always-sufficient output capacities (elements) for n rows of total_bytes input bytes. */
 uint64_t ak_normalize_cap(uint64_t n, uint64_t total_bytes);

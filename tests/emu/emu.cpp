@@ -148,23 +148,26 @@ thread_local EmuWave *t_wave;
 extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
                                  uint32_t *out, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, int rows) {
     EmuModel *m = (EmuModel *)model;
+    if (flags != 3) return -1;
     static uint2 fast[FAST_N];
-    for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
+    static uint32_t hot_tab[FAST_N];
+    for (uint32_t i = 0; i < FAST_N; ++i) { fast[i] = prop_global(i); hot_tab[i] = hot_of(fast[i]); }
+    if (n == 0) { out_offs[0] = 0; return 0; }
+    std::vector<uint32_t> stage(offs[n] + 2 * n + 64), counts(n);
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
-    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = out; ta.ra.cap = cap; ta.ra.out_offs = out_offs;
+    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = stage.size();
     ta.ra.row_status = row_status; ta.ra.bpe = m->bdev; ta.ra.single_fast = m->bpe.fast.data();
-    std::vector<uint32_t> seg(2 * SLOW_SEG), dec(8 * SLOW_SEG), wpair(SLOW_WORD), vchar(SLOW_WORD);
-    std::vector<uint16_t> wsym(SLOW_WORD);
+    // one pool region per lane of the emulated wave (wave 0 uses regions 0..63)
+    std::vector<uint32_t> seg(64 * 2 * SLOW_SEG), dec(64 * 8 * SLOW_SEG), wpair(64 * SLOW_WORD), vchar(64 * SLOW_WORD);
+    std::vector<uint16_t> wsym(64 * SLOW_WORD);
     ta.ra.pool.seg = seg.data(); ta.ra.pool.dec = dec.data(); ta.ra.pool.wsym = wsym.data();
     ta.ra.pool.wpair = wpair.data(); ta.ra.pool.vchar = vchar.data();
     const uint64_t ntiles = (n + rows - 1) / rows;
-    std::vector<uint64_t> status(ntiles + 1, 0);
-    uint32_t ticket = 0, err = 0;
+    uint32_t err = 0;
     std::vector<uint32_t> locks(SLOW_THREADS, 0);
-    ta.status = status.data(); ta.ticket = &ticket; ta.locks = locks.data(); ta.err = &err;
+    ta.counts = counts.data(); ta.locks = locks.data(); ta.err = &err;
     ta.ntiles = ntiles; ta.rows = rows;
-    if (n == 0) { out_offs[0] = 0; return 0; }
     TileWaveMem *M = new TileWaveMem();
     EmuWave W;
     std::vector<std::thread> th;
@@ -172,10 +175,18 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
         th.emplace_back([&, lane] {
             t_lane = lane;
             t_wave = &W;
-            if (flags == 3) bpe_tiles_wave<3>(ta, fast, m->bpe.fast.data(), *M, 0);
-            else bpe_tiles_wave<2>(ta, fast, m->bpe.fast.data(), *M, 0);
+            bpe_tiles_wave<3>(ta, fast, hot_tab, m->bpe.fast.data(), *M, 0, 1);
         });
     for (auto &x : th) x.join();
     delete M;
-    return err ? -1 : (int64_t)out_offs[n];
+    if (err) return -1;
+    // scan + per-tile copy, as the launcher's scan_counts and k_tile_copy
+    out_offs[0] = 0;
+    for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
+    for (uint64_t t = 0; t < ntiles; ++t) {
+        const uint64_t r0 = t * rows, r1 = std::min<uint64_t>(r0 + rows, n);
+        const uint32_t *src = stage.data() + offs[r0] + 2 * r0;
+        for (uint64_t i = 0; i < out_offs[r1] - out_offs[r0] && out_offs[r0] + i < cap; ++i) out[out_offs[r0] + i] = src[i];
+    }
+    return (int64_t)out_offs[n];
 }
