@@ -477,7 +477,7 @@ struct SwitchSink {
 // template <s> $A </s>.
 
 struct BpeDev {
-    const uint64_t *merge_tab;  // open addressing: lo32 = left << 16 | right, hi32 = rank << 16 | new
+    const uint64_t *merge_tab;  // two-choice cuckoo: lo32 = left << 16 | right, hi32 = rank << 16 | new
     uint32_t tab_mask;
     uint32_t tab_shift;
     const uint32_t *single_sorted_cp;  // for code points >= FAST_N
@@ -486,16 +486,15 @@ struct BpeDev {
     uint32_t bos, eos;
 };
 
+// two-choice cuckoo lookup (ak_model_build.h): both candidate slots are loaded at once (L2-resident
+// table, plain loads), no probe loop -> no divergence
 __device__ __forceinline__ uint32_t merge_lookup(const BpeDev &m, uint32_t a, uint32_t b) {
     const uint32_t key = (a << 16) | b;
-    uint32_t h = (key * 0x9E3779B1u) >> m.tab_shift;
-    for (;;) {
-        const uint64_t e = m.merge_tab[h];  // L2-resident table (plain load: keep it cached)
-        const uint32_t k = (uint32_t)e;
-        if (k == key) return (uint32_t)(e >> 32);
-        if (k == 0xFFFFFFFFu) return 0xFFFFFFFFu;
-        h = (h + 1) & m.tab_mask;
-    }
+    const uint32_t h1 = (key * 0x9E3779B1u) >> m.tab_shift;
+    const uint32_t h2 = ((key ^ 0x5BD1E995u) * 0x85EBCA77u) >> m.tab_shift;
+    const uint64_t e1 = m.merge_tab[h1];
+    const uint64_t e2 = m.merge_tab[h2];
+    return (uint32_t)e1 == key ? (uint32_t)(e1 >> 32) : (uint32_t)e2 == key ? (uint32_t)(e2 >> 32) : 0xFFFFFFFFu;
 }
 
 __device__ __forceinline__ int bpe_merge_word(const BpeDev &m, uint16_t *w, uint32_t *pr, int n) {

@@ -114,6 +114,7 @@ struct ak_bpe {
     uint16_t *d_single_fast = nullptr;  // FAST_N entries
     uint32_t *d_single_cp = nullptr;
     uint16_t *d_single_id = nullptr;
+    bool tile_ok = false;  // every id < 0x7FFC: the tile kernel tags ids with bit 15 (ak_tile.h WSTART)
 };
 
 struct ak_spm {
@@ -131,6 +132,9 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
         return fail(AK_ERR_ARG, "ak_bpe_create: null argument");
     akb::BpeTables t;
     const std::string err = akb::build_bpe(n_single, single_cp, single_id, n_merges, merges, t);
+    uint32_t max_id = std::max(bos, eos);
+    for (uint32_t i = 0; i < n_single; ++i) max_id = std::max(max_id, single_id[i]);
+    for (uint64_t i = 0; i < n_merges; ++i) max_id = std::max(max_id, merges[3 * i + 2]);
     if (!err.empty()) return fail(AK_ERR_UNSUPPORTED, ("ak_bpe_create: " + err).c_str());
     ak_bpe *m = new ak_bpe();
     HIP_TRY(hipMalloc(&m->d_tab, t.tab.size() * sizeof(uint64_t)));
@@ -149,6 +153,7 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     m->dev.n_single = t.n_rest;
     m->dev.bos = bos;
     m->dev.eos = eos;
+    m->tile_ok = max_id < 0x7FFCu;
     *out = m;
     return AK_OK;
 }
@@ -455,6 +460,7 @@ extern "C" int ak_bpe_encode(const ak_bpe *m, ak_ws *w, int flags, const uint8_t
     RowArgs a = make_args(in, offs, n, ids, cap, row_status);
     a.bpe = m->dev;
     a.single_fast = m->d_single_fast;
+    if (!m->tile_ok) return launch_bpe(flags, w, a, out_offs, (hipStream_t)stream);
     return dispatch(OP_BPE, flags, w, a, out_offs, (hipStream_t)stream);
 }
 

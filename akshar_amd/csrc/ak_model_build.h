@@ -1,6 +1,6 @@
 // ak_model_build.h — host-side construction of the device model tables.
 //
-//  BPE  (HF models.BPE, tokenizer.py:96-97 / cli.py:276-299): an open-addressing hash of the
+//  BPE  (HF models.BPE, tokenizer.py:96-97 / cli.py:276-299): a two-choice cuckoo hash of the
 //       merges, 8-byte entries {left << 16 | right, rank << 16 | new_id}, load factor <= 0.5;
 //       a direct single-char id table for U+0000..U+09FF plus a sorted list for the rest.
 //  SPM  (sentencepiece unigram, tokenizer.py:88-90 / cli.py:232-248): a double-array trie over
@@ -17,6 +17,9 @@
 namespace akb {
 
 constexpr uint32_t FAST_N = 0x0A00;
+
+inline uint32_t cuckoo_h1(uint32_t key, uint32_t shift) { return (key * 0x9E3779B1u) >> shift; }
+inline uint32_t cuckoo_h2(uint32_t key, uint32_t shift) { return ((key ^ 0x5BD1E995u) * 0x85EBCA77u) >> shift; }
 
 struct BpeTables {
     std::vector<uint64_t> tab;
@@ -36,22 +39,34 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
         if (single_id[i] >= 0xFFFFu) return "vocab id >= 65535";
     for (uint64_t i = 0; i < 3ull * n_merges; ++i)
         if (merges[i] >= 0xFFFFu) return "vocab id >= 65535";
+    // two-choice cuckoo table: a key lives in slot h1(key) or h2(key), so a device lookup is two
+    // independent 8-byte loads and no probe loop (ak_dev.h merge_lookup)
     uint32_t size = 1024;
     while (size < 2u * n_merges + 16u) size <<= 1;
-    t.tab.assign(size, 0xFFFFFFFFull);
-    t.mask = size - 1;
-    t.shift = 32;
-    for (uint32_t s = size; s > 1; s >>= 1) --t.shift;
-    for (uint32_t r = 0; r < n_merges; ++r) {
-        const uint32_t key = (merges[3 * r] << 16) | merges[3 * r + 1];
-        uint32_t h = (key * 0x9E3779B1u) >> t.shift;
-        bool dup = false;
-        while ((uint32_t)t.tab[h] != 0xFFFFFFFFu) {
-            if ((uint32_t)t.tab[h] == key) { dup = true; break; }  // the lowest rank wins
-            h = (h + 1) & t.mask;
+    for (;;) {
+        t.tab.assign(size, 0xFFFFFFFFull);
+        t.mask = size - 1;
+        t.shift = 32;
+        for (uint32_t q = size; q > 1; q >>= 1) --t.shift;
+        bool ok = true;
+        for (uint32_t r = 0; r < n_merges && ok; ++r) {
+            const uint32_t key = (merges[3 * r] << 16) | merges[3 * r + 1];
+            const uint32_t a = cuckoo_h1(key, t.shift), b = cuckoo_h2(key, t.shift);
+            if ((uint32_t)t.tab[a] == key || (uint32_t)t.tab[b] == key) continue;  // the lowest rank wins
+            uint64_t e = (uint64_t)key | ((uint64_t)((r << 16) | merges[3 * r + 2]) << 32);
+            uint32_t h = a;
+            int kicks = 0;
+            for (;;) {
+                std::swap(e, t.tab[h]);
+                if ((uint32_t)e == 0xFFFFFFFFu) break;
+                const uint32_t k2 = (uint32_t)e;
+                h = cuckoo_h1(k2, t.shift) == h ? cuckoo_h2(k2, t.shift) : cuckoo_h1(k2, t.shift);
+                if (++kicks > 4096) { ok = false; break; }
+            }
         }
-        if (dup) continue;
-        t.tab[h] = (uint64_t)key | ((uint64_t)((r << 16) | merges[3 * r + 2]) << 32);
+        if (ok) break;
+        size <<= 1;  // a cycle: grow and rebuild (never needed at load <= 0.5 in practice)
+        if (size > (1u << 24)) return "cuckoo table build failed";
     }
     t.fast.assign(FAST_N, 0xFFFFu);
     std::vector<std::pair<uint32_t, uint16_t>> rest;

@@ -39,12 +39,13 @@ constexpr uint16_t V_DEAD = 0xFFFD;
 constexpr uint16_t V_B = 0xFFFE;
 constexpr uint16_t V_E = 0xFFFF;
 constexpr uint16_t V_SPECIAL = 0xFFFC;  // values >= this are sentinels / dead
-constexpr uint16_t WEND = 0x8000;       // word-end tag on a code point (all are <= U+3000)
+constexpr uint16_t WSTART = 0x8000;     // first symbol of a pre-token (ids are < 0x7FFC: checked at load)
+constexpr int WREG = 16;                // pre-tokens up to WREG-1 symbols merge in registers
 
 struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
     uint16_t v[T_E];
-    uint16_t w[T_E];
+    uint16_t w[T_E + 16];  // +16: pass B reads 16-symbol windows past a word's start
     uint64_t fbbase[T_MAXR];
     uint32_t fbcount[T_MAXR];
     uint8_t fbrow[T_MAXR];    // slot -> row index in tile
@@ -90,23 +91,89 @@ struct PassClock {  // wave-uniform; lane 0 flushes once per wave
 };
 
 // Hot per-code-point word for the cooperative passes (LDS, cp < FAST_N; built from the full
-// property record by hot_of): normalize_text map + the NFC / HF-NFC quick-check bits + HF classes.
+// property record by hot_of): normalize_text map, the NFC / HF-NFC quick-check bits, HF classes,
+// and a 6-bit order-preserving ccc code (own ccc for NFC-non-stable chars; for NFC-stable ones the
+// ccc of the last char of their canonical decomposition, 0 if none).
 constexpr uint32_t H_STABLE = 1u << 16;  // NFC-stable: ccc 0, NFC(c) == c, never a composition second
 constexpr uint32_t H_DECOMP = 1u << 17;  // has a canonical decomposition
-constexpr uint32_t H_NT = 1u << 18;      // composition second or ccc 0 (a mark that is one triggers NFC)
-constexpr uint32_t H_HFST = 1u << 19;    // HF-stable: HF ccc 0 and never a composition second
-constexpr uint32_t H_HNT = 1u << 20;     // composition second or HF ccc 0
-constexpr uint32_t H_HFSPACE = 1u << 21; // HF NFKC maps it to U+0020
-constexpr int H_CLS_SHIFT = 22;          // HF pre-tokenizer class (2 bits)
+constexpr uint32_t H_SECOND = 1u << 18;  // second char of some primary composite (or Hangul V/T)
+constexpr uint32_t H_FIRST = 1u << 19;   // first char of some primary composite (or Hangul L / LV)
+constexpr uint32_t H_HFST = 1u << 20;    // HF-stable: HF ccc 0 and not a composition second
+constexpr uint32_t H_HC0 = 1u << 21;     // HF ccc == 0
+constexpr uint32_t H_HFSPACE = 1u << 22; // HF NFKC maps it to U+0020
+constexpr int H_CLS_SHIFT = 23;          // HF pre-tokenizer class (2 bits)
+constexpr int H_CCC_SHIFT = 26;          // 6-bit ccc code
+constexpr uint32_t H_ROWSTART = 0xFFFFFFFFu;  // "previous char" at a row start / sentinel
+
+__device__ __forceinline__ uint32_t ccc_code(uint32_t c) {  // order-preserving, < 64 (Unicode 13 ccc set)
+    if (c <= 36u) return c;
+    constexpr uint8_t hi[23] = {84, 91, 103, 107, 118, 122, 129, 130, 132, 202, 214, 216,
+                                218, 220, 222, 224, 226, 228, 230, 232, 233, 234, 240};
+    uint32_t k = 37;
+    for (int i = 0; i < 23; ++i) k += c > hi[i] ? 1u : 0u;
+    return k;
+}
 
 __device__ __forceinline__ uint32_t hot_of(uint2 pr) {
+    const bool first = ((pr.x >> 23) & 1u) != 0;
+    uint32_t cc = (uint32_t)p_ccc(pr);
+    if (p_stable(pr)) {  // trailing ccc of the canonical decomposition
+        cc = 0;
+        const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
+        if (len) cc = (uint32_t)p_ccc(prop_global(AK_UT_DECOMP[idx + len - 1]));
+    }
     return p_normmap(pr) | (p_stable(pr) ? H_STABLE : 0u) | (p_decomp(pr) ? H_DECOMP : 0u) |
-           ((p_second(pr) || p_ccc(pr) == 0) ? H_NT : 0u) | ((p_ccc_hf(pr) == 0 && !p_second(pr)) ? H_HFST : 0u) |
-           ((p_second(pr) || p_ccc_hf(pr) == 0) ? H_HNT : 0u) | (p_hfspace(pr) ? H_HFSPACE : 0u) |
-           ((uint32_t)p_hfclass(pr) << H_CLS_SHIFT);
+           (p_second(pr) ? H_SECOND : 0u) | (first ? H_FIRST : 0u) |
+           ((p_ccc_hf(pr) == 0 && !p_second(pr)) ? H_HFST : 0u) | (p_ccc_hf(pr) == 0 ? H_HC0 : 0u) |
+           (p_hfspace(pr) ? H_HFSPACE : 0u) | ((uint32_t)p_hfclass(pr) << H_CLS_SHIFT) | (ccc_code(cc) << H_CCC_SHIFT);
 }
 __device__ __forceinline__ uint32_t hot(const uint32_t *H, uint32_t cp) {
     return cp < FAST_N ? H[cp] : hot_of(prop_global(cp));
+}
+
+// Exact-or-conservative test that NFC leaves the segment around mark m unchanged, given the char
+// p before it (true = "NFC might change something here": take the full path). Stable chars never
+// trigger by themselves; a non-stable char m triggers if it decomposes, if it is a starter that
+// is not a composition second, if it would be reordered before the previous mark, if it could
+// compose with the previous starter, or if it could be reordered into a decomposable previous
+// starter's trailing marks. HF: the same rule over HF's ccc (p_ccc_hf) and HF-stability.
+template <bool HF>
+__device__ __forceinline__ bool nfc_trig(uint32_t m, uint32_t p) {
+    if (p == H_ROWSTART) return true;
+    if (m & H_DECOMP) return true;
+    const uint32_t cm = HF && (m & H_HC0) ? 0u : (m >> H_CCC_SHIFT);
+    const bool pst = HF ? (p & H_HFST) != 0 : (p & H_STABLE) != 0;
+    if (!pst) {
+        const uint32_t cpv = HF && (p & H_HC0) ? 0u : (p >> H_CCC_SHIFT);
+        return cm == 0 || cm < cpv || ((m & H_SECOND) && cm > cpv);
+    }
+    return (cm == 0 && !(m & H_SECOND)) || ((m & H_SECOND) && (p & H_FIRST)) ||
+           ((p & H_DECOMP) && (p & H_STABLE) && cm < (p >> H_CCC_SHIFT));
+}
+
+// bytes p .. p+3 of an LDS byte array as one little-endian word (two aligned dword reads)
+__device__ __forceinline__ uint32_t lds_word(const uint8_t *B, int p) {
+    const uint32_t *w = (const uint32_t *)(B + (p & ~3));
+    const uint32_t lo = w[0], hi = w[1];
+    const uint32_t sh = (uint32_t)(p & 3) * 8u;
+    return sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
+}
+
+// branch-free UTF-8 decode of the char starting at p (< e) from its 4-byte window x; same
+// acceptance as lds_decode (0xFFFFFFFF = invalid)
+__device__ __forceinline__ uint32_t decode_word(uint32_t x, int p, int e) {
+    const uint32_t b0 = x & 0xFFu, b1 = (x >> 8) & 0xFFu, b2 = (x >> 16) & 0xFFu, b3 = x >> 24;
+    if (b0 < 0x80u) return b0;
+    const int l = b0 >= 0xF0u ? 4 : b0 >= 0xE0u ? 3 : b0 >= 0xC0u ? 2 : 0;
+    const bool c1 = (b1 & 0xC0u) == 0x80u, c2 = (b2 & 0xC0u) == 0x80u, c3 = (b3 & 0xC0u) == 0x80u;
+    const uint32_t cp2 = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
+    const uint32_t cp3 = ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu);
+    const uint32_t cp4 = ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
+    const uint32_t cp = l == 2 ? cp2 : l == 3 ? cp3 : cp4;
+    const bool conts = l == 2 ? c1 : l == 3 ? (c1 && c2) : (c1 && c2 && c3);
+    const uint32_t mn = l == 2 ? 0x80u : l == 3 ? 0x800u : 0x10000u;
+    const bool ok = l != 0 && b0 <= 0xF4u && p + l <= e && conts && cp >= mn && cp <= 0x10FFFFu;
+    return ok ? cp : 0xFFFFFFFFu;
 }
 
 __device__ __forceinline__ int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }
@@ -256,43 +323,31 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         if (lane == 0) M.v[vpos] = V_B;
         ++vpos;
         bool rowbad = false;
-        // Fast path: if no code point of the row trips the NFC quick check (a decomposable char, or
-        // a non-stable char that is a composition second / a starter / follows another non-stable
-        // char or the row start), NFC is the identity on the row (no NFD change, no reordering,
-        // nothing composes) and every char maps on its own: one ballot-compacted write per lane.
+        // Fast path: if no char of the row trips nfc_trig, NFC is the identity on the row and every
+        // char maps on its own: one ballot-compacted write per lane.
         bool complex = false;
         {
-            bool carry_ns = true;  // the char before the first one: the row start blocks like a mark
+            uint32_t carry_h = H_ROWSTART;  // hot word of the last char of the previous chunk
             for (int base = s; base < e; base += 64) {
                 const int p = base + lane;
                 const bool in = p < e;
-                const uint32_t byte = in ? M.bytes[p] : 0u;
-                const bool lead = in && (byte & 0xC0u) != 0x80u;
+                const uint32_t x = in ? lds_word(M.bytes, p) : 0u;
+                const bool lead = in && (x & 0xC0u) != 0x80u;
                 bool bad = in && p == s && !lead;
                 uint32_t h = 0;
                 if (lead) {
-                    int len;
-                    const uint32_t cp = lds_decode(M.bytes, p, e, len);
+                    const uint32_t cp = decode_word(x, p, e);
                     if (cp == 0xFFFFFFFFu) bad = true;
                     else h = hot(H, cp);
                 }
                 if (w_ballot(bad)) { rowbad = true; break; }
                 const uint64_t LEADS = w_ballot(lead);
-                const uint64_t NS = w_ballot(lead && !(h & H_STABLE));
                 const uint64_t pm = LEADS & lt;
-                const bool prev_ns = pm ? ((NS >> msb64(pm)) & 1ull) != 0 : carry_ns;
-                bool trig = lead && !(h & H_STABLE) && ((h & H_NT) || prev_ns || (h & H_DECOMP));
-                if (lead && (h & H_STABLE) && (h & H_DECOMP)) {
-                    // a decomposable starter (e.g. U+0929) is its own NFC image unless marks follow
-                    int len1, l2;
-                    (void)lds_decode(M.bytes, p, e, len1);
-                    if (p + len1 < e) {
-                        const uint32_t c2 = lds_decode(M.bytes, p + len1, e, l2);
-                        trig = c2 == 0xFFFFFFFFu || !(hot(H, c2) & H_STABLE);
-                    }
-                }
+                const uint32_t hprev_l = w_shfl(h, pm ? msb64(pm) : 0);
+                const uint32_t hprev = pm ? hprev_l : carry_h;
+                const bool trig = lead && !(h & H_STABLE) && nfc_trig<false>(h, hprev);
                 if (w_ballot(trig)) { complex = true; break; }
-                if (LEADS) carry_ns = ((NS >> msb64(LEADS)) & 1ull) != 0;
+                if (LEADS) carry_h = w_bcast(h, msb64(LEADS));
                 const uint32_t mv = h & 0xFFFFu;
                 const uint64_t KM = w_ballot(mv != 0u);
                 if (mv) M.v[vpos + (uint32_t)w_popc(KM & lt)] = (uint16_t)mv;
@@ -428,26 +483,19 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     // per-segment check only runs on tiles where some char trips it)
     bool hf_any = false;
     {
-        bool carry_b = true;
+        uint32_t carry_h = H_ROWSTART;
         for (uint32_t base = 0; base < wlen; base += 64) {
             const uint32_t kk = base + lane;
             const bool in = kk < wlen;
             const uint16_t x = in ? M.w[kk] : V_DEAD;
             const bool special = x >= V_SPECIAL;
-            uint32_t h = special ? 0u : hot(H, x);
-            if (in && !special && (h & H_HFSPACE)) { M.w[kk] = 0x20; h = hot(H, 0x20); }
-            const bool nst = in && !special && !(h & H_HFST);
-            const uint64_t B = w_ballot(in && (special || nst));
-            const bool prev_b = lane ? ((B >> (lane - 1)) & 1ull) != 0 : carry_b;
-            bool trig = nst && ((h & H_HNT) || prev_b || (h & H_DECOMP));
-            if (in && !special && !nst && (h & H_DECOMP) && kk + 1 < wlen) {
-                // a decomposable HF-starter is unchanged unless an HF-non-starter follows it
-                const uint16_t y = M.w[kk + 1];
-                const uint32_t hy = y < V_SPECIAL ? hot(H, y) : H_HFST;  // compat spaces become ' '
-                trig = !(hy & (H_HFST | H_HFSPACE));
-            }
+            uint32_t h = special ? H_ROWSTART : hot(H, x);
+            if (!special && (h & H_HFSPACE)) { M.w[kk] = 0x20; h = hot(H, 0x20); }
+            const uint32_t hl = w_shfl(h, lane ? lane - 1 : 0);
+            const uint32_t hprev = lane ? hl : carry_h;
+            const bool trig = in && !special && !(h & H_HFST) && nfc_trig<true>(h, hprev);
             if (w_ballot(trig)) hf_any = true;
-            carry_b = ((B >> 63) & 1ull) != 0;
+            carry_h = w_bcast(h, 63);
         }
     }
     w_sync();
@@ -498,46 +546,110 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     w_sync();
 
     pc.mark(TP_H);
-    // ---------------- pass P: Whitespace pre-tokenizer (\w+ | [^\w\s]+)
+    // ---------------- pass P: Whitespace pre-tokenizer (\w+ | [^\w\s]+) + single-char ids.
+    // In place, W becomes: row sentinels and the ids of the chars that are in the vocab (others
+    // vanish, unk_token None), each pre-token's first kept id tagged WSTART; V gets the starts.
     uint32_t nw = 0;
-    for (uint32_t base = 0; base < wlen; base += 64) {
-        const uint32_t kk = base + lane;
-        const bool in = kk < wlen;
-        auto cls = [&](uint16_t x) -> int {
-            if (x >= V_SPECIAL) return HF_S;
-            return (int)((hot(H, (uint32_t)(x & 0x7FFF)) >> H_CLS_SHIFT) & 3u);
-        };
-        const uint16_t x = in ? M.w[kk] : V_DEAD;
-        const int c0 = cls(x);
-        const int cp_ = in && kk >= 1 ? cls(M.w[kk - 1]) : HF_S;
-        const int cn = in && kk + 1 < wlen ? cls(M.w[kk + 1]) : HF_S;
-        const bool isstart = in && c0 != HF_S && c0 != cp_;
-        const bool isend = in && c0 != HF_S && c0 != cn;
-        const uint64_t sm = w_ballot(isstart);
-        w_sync();
-        if (in && x < V_SPECIAL && c0 == HF_S) M.w[kk] = V_DEAD;
-        if (isend) M.w[kk] = (uint16_t)(x | WEND);
-        if (isstart) M.v[nw + w_popc(sm & lt)] = (uint16_t)kk;
-        nw += (uint32_t)w_popc(sm);
-        w_sync();
+    {
+        uint32_t wpos = 0;
+        int carry_cls = HF_S;
+        uint32_t carry_word = 0, carry_kword = 0xFFFFFFFFu;
+        for (uint32_t base = 0; base < wlen; base += 64) {
+            const uint32_t kk = base + lane;
+            const bool in = kk < wlen;
+            const uint16_t x = in ? M.w[kk] : V_DEAD;
+            const bool special = x >= V_SPECIAL;
+            const int cls = special ? HF_S : (int)((hot(H, x) >> H_CLS_SHIFT) & 3u);
+            const int cl_l = w_shfl(cls, lane ? lane - 1 : 0);
+            const int cprev = lane ? cl_l : carry_cls;
+            const bool wordchar = !special && cls != HF_S;
+            const uint64_t SM = w_ballot(wordchar && cls != cprev);
+            const uint32_t word = carry_word + (uint32_t)w_popc(SM & (lt | (1ull << lane)));  // inclusive
+            const uint32_t id = wordchar ? single_id_of(m, sfast, x) : 0xFFFFu;
+            const bool kept = id != 0xFFFFu;
+            const uint64_t KM = w_ballot(kept);
+            const uint64_t pk = KM & lt;
+            const uint32_t kw_l = w_shfl(word, pk ? msb64(pk) : 0);
+            const uint32_t kprev = pk ? kw_l : carry_kword;
+            const bool kstart = kept && word != kprev;
+            const bool out = kept || (special && x != V_DEAD);
+            const uint64_t OM = w_ballot(out);
+            const uint64_t KS = w_ballot(kstart);
+            const uint32_t op = wpos + (uint32_t)w_popc(OM & lt);
+            w_sync();  // every lane has read its element before the in-place compaction writes
+            if (out) M.w[op] = special ? x : (uint16_t)(id | (kstart ? WSTART : 0u));
+            if (kstart) M.v[nw + (uint32_t)w_popc(KS & lt)] = (uint16_t)op;
+            wpos += (uint32_t)w_popc(OM);
+            nw += (uint32_t)w_popc(KS);
+            carry_cls = w_bcast(cls, 63);
+            carry_word = w_bcast(word, 63);
+            if (KM) carry_kword = w_bcast(word, msb64(KM));
+        }
+        wlen = wpos;
     }
+    w_sync();
 
     pc.mark(TP_P);
-    // ---------------- pass B: lane per word, merge_all in place
+    // ---------------- pass B: lane per pre-token, merge_all (lowest rank, leftmost on ties).
+    // Pre-tokens of < WREG symbols merge in registers: one min over the pair ranks per round, the
+    // merge as a static shift network, two cuckoo lookups for the new neighbours; longer ones merge
+    // in LDS (bpe_merge_lds). The loop runs while any lane still has a merge.
     for (uint32_t wb = 0; wb < nw; wb += 64) {
         const uint32_t j = wb + lane;
-        if (j < nw) {
-            const int st = M.v[j];
-            int n = 0, q = st;
-            for (;;) {
-                const uint16_t x = M.w[q];
-                const uint32_t id = single_id_of(m, sfast, (uint32_t)(x & 0x7FFF));
-                if (id != 0xFFFFu) M.w[st + n++] = (uint16_t)id;
-                ++q;
-                if (x & WEND) break;
+        const bool act = j < nw;
+        const int st = act ? (int)M.v[j] : 0;
+        uint32_t sy[WREG];
+#pragma unroll
+        for (int i = 0; i < WREG; ++i) sy[i] = (act && st + i < (int)wlen) ? M.w[st + i] : 0xFFFFu;
+        int n = WREG;
+#pragma unroll
+        for (int i = WREG - 1; i >= 1; --i) n = (sy[i] & WSTART) ? i : n;
+        const bool reg = act && n < WREG;
+#pragma unroll
+        for (int i = 0; i < WREG; ++i) sy[i] &= 0x7FFFu;
+        uint32_t rk[WREG - 1];
+#pragma unroll
+        for (int i = 0; i < WREG - 1; ++i) rk[i] = (reg && i + 1 < n) ? merge_lookup(m, sy[i], sy[i + 1]) : 0xFFFFFFFFu;
+        int nn = reg ? n : 0;
+        for (;;) {
+            uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+            for (int i = 0; i < WREG - 1; ++i) {
+                const uint32_t key = (rk[i] & 0xFFFF0000u) | (uint32_t)i;
+                best = key < best ? key : best;
             }
-            for (int z = st + n; z < q; ++z) M.w[z] = V_DEAD;
-            (void)bpe_merge_lds(m, M.w, st, n);
+            const bool mg = best < 0xFFFF0000u;
+            if (!w_ballot(mg)) break;
+            if (mg) {
+                const int bi = (int)(best & 15u);
+                uint32_t nid = 0;
+#pragma unroll
+                for (int i = 0; i < WREG - 1; ++i) nid = i == bi ? (rk[i] & 0xFFFFu) : nid;
+#pragma unroll
+                for (int i = 0; i < WREG; ++i) sy[i] = i < bi ? sy[i] : (i == bi ? nid : (i + 1 < WREG ? sy[i + 1] : 0u));
+                nn -= 1;
+                uint32_t left = 0, right = 0;
+#pragma unroll
+                for (int i = 0; i < WREG; ++i) {
+                    left = i + 1 == bi ? sy[i] : left;
+                    right = i == bi + 1 ? sy[i] : right;
+                }
+                const uint32_t L = bi > 0 ? merge_lookup(m, left, nid) : 0xFFFFFFFFu;
+                const uint32_t R = bi + 1 < nn ? merge_lookup(m, nid, right) : 0xFFFFFFFFu;
+#pragma unroll
+                for (int i = 0; i < WREG - 1; ++i)
+                    rk[i] = i + 1 < bi ? rk[i] : (i + 1 == bi ? L : (i == bi ? R : (i + 1 < WREG - 1 ? rk[i + 1] : 0xFFFFFFFFu)));
+            }
+        }
+        if (reg) {
+#pragma unroll
+            for (int i = 0; i < WREG; ++i)
+                if (i < n) M.w[st + i] = i < nn ? (uint16_t)sy[i] : V_DEAD;
+        } else if (act) {  // long pre-token
+            int len = 1;
+            while (st + len < (int)wlen && !(M.w[st + len] & WSTART)) ++len;
+            M.w[st] &= 0x7FFFu;
+            (void)bpe_merge_lds(m, M.w, st, len);
         }
     }
     w_sync();
@@ -580,7 +692,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         } else if (x == V_E) {
             if (fits) stage[op] = m.eos;
         } else if (in && x != V_DEAD) {
-            if (fits) stage[op] = x;
+            if (fits) stage[op] = x & 0x7FFFu;
         }
         pos += tot;
         rows_seen += (uint32_t)w_popc(rm);
