@@ -260,6 +260,7 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->stage);
     (void)hipFree(w->tile_misc);
     (void)hipFree(w->tile_passprof);
+    (void)hipFree(w->fb2);
     (void)hipFree(w->counts);
     (void)hipFree(w->flags);
     (void)hipFree(w->slow_list);

@@ -42,7 +42,9 @@ struct AkWs {
     // tile-cooperative BPE path
     uint32_t *stage = nullptr;      // staged ids, slot of row r at offs[r] + 2 r
     uint64_t cap_stage = 0;
-    uint32_t *tile_misc = nullptr;  // [1] slot-overflow flag, [64..64+SLOW_THREADS) pool locks
+    uint32_t *tile_misc = nullptr;  // [0] fallback-list length, [1] slot-overflow flag, [2] second list length
+    uint32_t *fb2 = nullptr;        // second fallback list (rows past the fast buffers)
+    uint64_t cap_fb2 = 0;
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 8;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (v1)

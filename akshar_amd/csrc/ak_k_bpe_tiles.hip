@@ -1,8 +1,11 @@
 // ak_k_bpe_tiles.hip — the tile-cooperative BPE encode (ak_tile.h) and its launcher:
-//   k_bpe_tiles   every wave encodes whole tiles of R rows into the tile's staging slot and writes
-//                 per-row token counts (no inter-tile communication)
-//   scan_counts   per-row counts -> u64 row offsets (out_offs)
-//   k_tile_copy   each tile's staged ids -> ids[out_offs[r0] ...] (one coalesced copy per tile)
+//   k_bpe_tiles      every wave encodes whole tiles of R rows into per-row staging slots and
+//                    writes per-row token counts; rare rows go to a fallback list
+//   k_tile_fb        fallback rows, one lane per row (ak_rows.h process_row, small private
+//                    buffers), straight into the same slots; rows that overflow those buffers go on
+//   k_tile_fb_slow   ... to the large per-thread regions of the workspace pool
+//   scan_counts      per-row counts -> u64 row offsets (out_offs)
+//   k_tile_copy      staged ids -> ids[out_offs[r] ...]
 #include <stdio.h>
 
 #include "ak_internal.h"
@@ -13,16 +16,7 @@ namespace ak {
 static_assert(T_NPASS == AK_TILE_NPASS, "pass slots: ak_tile.h vs include/akshar.h");
 
 constexpr int TILE_BLOCK = 256;  // 4 waves share the staged property tables
-
-// full property records of the first FAST_N code points in global memory (L1/L2 resident): the
-// rare paths (segments that need real NFC, fallback rows) read them; the hot passes use the
-// compact LDS words
-__device__ uint2 g_fast_props[FAST_N];
-
-__global__ void k_init_fast_props() {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < FAST_N; i += gridDim.x * blockDim.x)
-        g_fast_props[i] = prop_global(i);
-}
+constexpr int FB_BLOCK = 256;
 
 template <int FLAGS>
 __global__ __launch_bounds__(TILE_BLOCK, 4) void k_bpe_tiles(TileArgs ta) {
@@ -35,26 +29,97 @@ __global__ __launch_bounds__(TILE_BLOCK, 4) void k_bpe_tiles(TileArgs ta) {
     }
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
-    bpe_tiles_wave<FLAGS>(ta, g_fast_props, hot_tab, sfast, wm[wave], blockIdx.x * (TILE_BLOCK / 64) + wave,
+    bpe_tiles_wave<FLAGS>(ta, hot_tab, sfast, wm[wave], blockIdx.x * (TILE_BLOCK / 64) + wave,
                           gridDim.x * (TILE_BLOCK / 64));
 }
 
+// fallback rows, fast buffers (the v1 row kernel's sizes); writes ids at the row's slot
+template <int FLAGS>
+__global__ __launch_bounds__(FB_BLOCK) void k_tile_fb(TileArgs ta) {
+    __shared__ uint2 fast[FAST_N];
+    __shared__ uint16_t sfast[FAST_N];
+    __shared__ uint16_t wsym[FB_BLOCK * FAST_WORD];
+    __shared__ uint32_t wpair[FB_BLOCK * FAST_WORD];
+    const uint32_t nl = *ta.fb_count;
+    if (nl == 0) return;  // uniform: the common case
+    stage_tables(fast, sfast, ta.ra.single_fast, true);
+    uint32_t seg[FAST_SEG], seg2[FAST_SEG], dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
+    Scratch sc;
+    sc.seg = seg; sc.dec = dec; sc.seg2 = seg2; sc.dec2 = dec2; sc.seg_cap = FAST_SEG;
+    sc.wsym = wsym + threadIdx.x * FAST_WORD;
+    sc.wpair = wpair + threadIdx.x * FAST_WORD;
+    sc.word_cap = FAST_WORD;
+    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
+    sc.slow_status = ST_SLOW;
+    const RowArgs &a = ta.ra;
+    for (uint32_t i = blockIdx.x * FB_BLOCK + threadIdx.x; i < nl; i += gridDim.x * FB_BLOCK) {
+        const uint64_t r = ta.fb_list[i];
+        sc.status = 0;
+        const uint64_t cnt = process_row<OP_BPE, FLAGS, true>(a, r, fast, sfast, &sc, a.offs[r] + 2 * r);
+        if (sc.status & ST_SLOW) {
+            ta.fb2_list[atomicAdd(ta.fb2_count, 1u)] = (uint32_t)r;
+            continue;
+        }
+        ta.counts[r] = (uint32_t)cnt;
+        if (a.row_status) a.row_status[r] = (uint8_t)(sc.status & ST_BAD_UTF8);
+    }
+}
+
+// fallback rows past the fast buffers: one large pool region per thread (AK_LIMIT_* sizes)
+template <int FLAGS>
+__global__ __launch_bounds__(64) void k_tile_fb_slow(TileArgs ta) {
+    __shared__ uint2 fast[FAST_N];
+    __shared__ uint16_t sfast[FAST_N];
+    const uint32_t nl = *ta.fb2_count;
+    if (nl == 0) return;
+    stage_tables(fast, sfast, ta.ra.single_fast, true);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < SLOW_THREADS
+    const RowArgs &a = ta.ra;
+    Scratch sc;
+    sc.seg = a.pool.seg + t * 2 * SLOW_SEG;
+    sc.dec = a.pool.dec + t * 8 * SLOW_SEG;
+    sc.seg2 = sc.seg + SLOW_SEG;
+    sc.dec2 = sc.dec + 4 * SLOW_SEG;
+    sc.seg_cap = SLOW_SEG;
+    sc.wsym = a.pool.wsym + t * SLOW_WORD;
+    sc.wpair = a.pool.wpair + t * SLOW_WORD;
+    sc.word_cap = SLOW_WORD;
+    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
+    sc.slow_status = ST_LIMIT;
+    for (uint32_t i = (uint32_t)t; i < nl; i += SLOW_THREADS) {
+        const uint64_t r = ta.fb2_list[i];
+        sc.status = 0;
+        const uint64_t cnt = process_row<OP_BPE, FLAGS, true>(a, r, fast, sfast, &sc, a.offs[r] + 2 * r);
+        const bool lim = (sc.status & ST_LIMIT) != 0;
+        ta.counts[r] = lim ? 0u : (uint32_t)cnt;
+        if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0u));
+    }
+}
+
+// staged ids -> final positions; one wave per tile of R rows, lanes spread over the tile's ids
 __global__ __launch_bounds__(256) void k_tile_copy(const uint32_t *__restrict__ stage, const uint64_t *__restrict__ offs,
                                                    const uint64_t *__restrict__ out_offs, uint64_t n, uint32_t R,
                                                    uint64_t ntiles, uint32_t *__restrict__ ids, uint64_t cap,
                                                    uint64_t stage_cap) {
-    const uint32_t lane = threadIdx.x & 63;
+    const int lane = (int)(threadIdx.x & 63);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
         const uint64_t r0 = t * R;
-        const uint64_t r1 = r0 + R < n ? r0 + R : n;
-        const uint64_t s0 = offs[r0] + 2 * r0;
-        const uint32_t *src = stage + s0;
-        const uint64_t d0 = out_offs[r0];
-        const uint64_t cnt = out_offs[r1] - d0;
-        uint64_t lim = cap > d0 ? (cap - d0 < cnt ? cap - d0 : cnt) : 0;
-        if (s0 + lim > stage_cap) lim = stage_cap > s0 ? stage_cap - s0 : 0;  // never for sane counts
-        for (uint64_t i = lane; i < lim; i += 64) ids[d0 + i] = src[i];
+        const int nr = (int)((r0 + R < n ? r0 + R : n) - r0);
+        // lane j <= nr holds the tile's row j: output start and slot start
+        const uint64_t oo = lane <= nr ? out_offs[r0 + lane] : 0ull;
+        const uint64_t so = lane < nr ? offs[r0 + lane] + 2 * (r0 + lane) : 0ull;
+        const uint64_t d0 = w_bcast(oo, 0), d1 = w_bcast(oo, nr);
+        for (uint64_t o = d0 + lane; o < d1; o += 64) {
+            // last row whose output starts at or before o (<= 16 rows: a uniform readlane scan)
+            uint64_t src_row = w_bcast(so, 0), out_row = d0;
+            for (int j = 1; j < nr; ++j) {
+                const uint64_t oj = w_bcast(oo, j), sj = w_bcast(so, j);
+                if (oj <= o) { out_row = oj; src_row = sj; }
+            }
+            const uint64_t src = src_row + (o - out_row);
+            if (o < cap && src < stage_cap) ids[o] = stage[src];
+        }
     }
 }
 
@@ -98,7 +163,6 @@ int selftest_wave() {
 }
 
 static int g_tile_blocks_per_cu = 0;
-static bool g_fast_props_ready[64] = {};
 
 // flags == AK_NORM_DEFAULT only (the dispatcher sends other flags to the row kernels)
 int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t st) {
@@ -123,21 +187,13 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     }
     const int R = w->tile_rows;
     const uint64_t ntiles = (a0.n + (uint64_t)R - 1) / (uint64_t)R;
-    if (!w->tile_misc) {
-        HIP_TRY(hipMalloc(&w->tile_misc, (64 + SLOW_THREADS) * 4));
-        HIP_TRY(hipMemsetAsync(w->tile_misc, 0, (64 + SLOW_THREADS) * 4, st));
+    if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
+        HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
+        HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
     if (g_prof_on && !w->tile_passprof) {
         HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
         HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
-    }
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return set_error(AK_ERR_UNSUPPORTED, "bpe tiles: device index >= 64");
-    if (!g_fast_props_ready[dev]) {
-        k_init_fast_props<<<(FAST_N + 255) / 256, 256, 0, st>>>();
-        HIP_TRY(hipGetLastError());
-        g_fast_props_ready[dev] = true;
     }
     if (!g_tile_blocks_per_cu) {
         int b = 0;
@@ -152,17 +208,34 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     ta.ra.out_offs = nullptr;
     ta.ra.pool = w->pool;
     ta.counts = w->counts;
+    ta.fb_list = w->slow_list;              // n entries (ws_reserve)
+    ta.fb_count = w->tile_misc;
     ta.err = w->tile_misc + 1;
-    ta.locks = w->tile_misc + 64;
+    ta.fb2_count = w->tile_misc + 2;
     ta.passprof = g_prof_on ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.rows = R;
+    if (w->cap_fb2 < a0.n) {
+        (void)hipFree(w->fb2);
+        w->fb2 = nullptr;
+        HIP_TRY(hipMalloc(&w->fb2, a0.n * 4));
+        w->cap_fb2 = a0.n;
+    }
+    ta.fb2_list = w->fb2;
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
+    HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + waves_per_block - 1) / waves_per_block,
                                                        (uint64_t)num_cus() * (uint64_t)g_tile_blocks_per_cu);
     AK_PROF(AK_PROF_TILES, false, st);
     k_bpe_tiles<3><<<grid, TILE_BLOCK, 0, st>>>(ta);
     AK_PROF(AK_PROF_TILES, true, st);
+    HIP_TRY(hipGetLastError());
+    // fallback rows: the full row pipeline (exact NFC, HF-NFC, any UTF-8) into the same slots
+    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
+    k_tile_fb<3><<<(unsigned)num_cus(), FB_BLOCK, 0, st>>>(ta);
+    k_tile_fb_slow<3><<<SLOW_THREADS / 64, 64, 0, st>>>(ta);
+    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
     HIP_TRY(hipGetLastError());
     AK_PROF(AK_PROF_SCAN, false, st);
     rc = scan_counts(w, a0.n, out_offs, st);

@@ -2,23 +2,22 @@
 //
 // One wave64 owns one tile of R consecutive rows at a time. The tile's bytes are staged into LDS
 // with coalesced 16-byte loads, then the wave runs the reference pipeline as data-parallel passes
-// over LDS arrays (positions on lanes, ballot / prefix-sum compaction between passes):
-//   D  decode + NFC + normalize_text map/filter       bytes -> V (u16 code points, row sentinels)
-//      (NFC segments whose marks could change are resolved by their leader lane with nfc_full)
-//   E  remove_elongations (runs >= 3, '\n' exempt)    V -> W
-//   H  HF NFKC: compat spaces -> ' ', HF-ccc segments checked by their leader
-//   P  Whitespace pre-tokenizer: word starts -> V, word-end tags on W, spaces -> DEAD
-//   B  lane per word: cps -> ids, merge_all (lowest rank, leftmost) in place in W
-//   F  weighted compaction W -> ids (B -> <s>, E -> </s>) into the tile's staging slot, per-row
-//      token counts from the sentinels' positions
-// Tiles never wait on each other: tile t stages its ids contiguously at stage[offs[r0] + 2 r0]
-// (a row's ids never exceed its bytes + 2, so the slots cannot overlap) and writes per-row
-// counts; the launcher then scans the counts into row offsets and a copy kernel moves each
-// tile's ids to their final place (ak_k_bpe_tiles.hip). No look-back, no ticket: on MI355X every
-// inter-tile hop would be a cross-XCD L2 round trip.
-// Rows that cannot take the cooperative path (invalid UTF-8, an NFC segment over T_SEG code points,
-// a changed HF segment, or bytes beyond the tile buffer) run the sequential row pipeline
-// (ak_dev.h, process_row) in one lane of the same wave, so every row is computed exactly once.
+// over LDS arrays (positions on lanes, ballot / DPP prefix-sum compaction between passes):
+//   D  decode + normalize_text map/filter, NFC proven the identity by nfc_trig   bytes -> V
+//   E  remove_elongations (runs >= 3, '\n' exempt)                              V -> W
+//   H  HF NFKC: compat spaces -> ' ', HF-NFC proven the identity by nfc_trig<true>
+//   P  Whitespace pre-tokenizer + single-char ids, compacted in place; pre-token starts -> V
+//   B  lane per pre-token: merge_all (lowest rank, leftmost on ties), in registers up to WREG-1
+//      symbols, in LDS beyond
+//   F  ids (B -> <s>, E -> </s>) into each row's staging slot, per-row token counts
+// Only the common case runs here. A row whose NFC / HF-NFC quick check trips, with invalid UTF-8,
+// or past the tile buffer is appended to a fallback list and encoded by the row kernels of
+// ak_k_bpe_tiles.hip (ak_rows.h process_row), which write into the same per-row slot: the tile
+// kernel has no calls, no private arrays and no scratch.
+// Row r's slot is stage[offs[r] + 2 r ...] (its ids never exceed its bytes + 2), so rows and tiles
+// never wait on each other; the launcher scans the counts into row offsets and a copy kernel
+// moves the ids to their final place. No look-back, no ticket: on MI355X every inter-tile hop
+// would be a cross-XCD L2 round trip.
 // Reference semantics: normalize.py:117-148, tokenizer.py:167-193, cli.py:276-299.
 #pragma once
 #include "ak_dev.h"
@@ -27,40 +26,36 @@
 
 namespace ak {
 
-constexpr int T_BCAP = 1024;  // staged bytes per tile (rows past it fall back); sized for 4 blocks/CU
+constexpr int T_BCAP = 1024;  // staged bytes per tile (rows past it fall back)
 constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
 constexpr int T_E = T_BCAP + 2 * T_MAXR + 64;
-constexpr int T_SEG = 16;     // NFC segment length handled in the cooperative pass
-constexpr int T_FBSEG = 16;   // fallback lane buffers (private); larger rows use the locked pool
-constexpr int T_FBWORD = 64;
 
-constexpr uint16_t V_FB = 0xFFFC;    // B sentinel of a fallback row (weight = its token count)
+constexpr uint16_t V_FB = 0xFFFC;    // sentinel of a row handed to the fallback kernels (no ids here)
 constexpr uint16_t V_DEAD = 0xFFFD;
 constexpr uint16_t V_B = 0xFFFE;
 constexpr uint16_t V_E = 0xFFFF;
 constexpr uint16_t V_SPECIAL = 0xFFFC;  // values >= this are sentinels / dead
 constexpr uint16_t WSTART = 0x8000;     // first symbol of a pre-token (ids are < 0x7FFC: checked at load)
-constexpr int WREG = 16;                // pre-tokens up to WREG-1 symbols merge in registers
+constexpr int WREG = 12;                // pre-tokens up to WREG-1 symbols merge in registers
 
 struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
     uint16_t v[T_E];
-    uint16_t w[T_E + 16];  // +16: pass B reads 16-symbol windows past a word's start
-    uint64_t fbbase[T_MAXR];
-    uint32_t fbcount[T_MAXR];
-    uint8_t fbrow[T_MAXR];    // slot -> row index in tile
-    uint8_t fbslot[T_MAXR];   // coop row -> slot (0xFF none)
-    uint8_t fbstat[T_MAXR];
-    uint8_t hfbad[T_MAXR];
-    uint16_t wrow[T_MAXR + 1];  // W index of each coop row's B / FB sentinel
-    uint32_t rowop[T_MAXR + 1]; // tile-relative output position of each row's first id
+    uint16_t w[T_E + 16];        // +16: pass B reads WREG-symbol windows past a pre-token start
+    uint16_t wrow[T_MAXR + 1];   // W index of each cooperative row's sentinel
+    uint8_t fb[T_MAXR];          // row goes to the fallback kernels
+    uint32_t rowslot[T_MAXR];    // row's staging slot, relative to the tile's (S0 + 2 r0)
+    uint32_t rowop[T_MAXR + 1];  // row's first position in the tile's id stream
 };
 
 struct TileArgs {
     RowArgs ra;           // in, offs, n, row_status, bpe, single_fast; out = stage (u32), cap = its size
     uint32_t *counts;     // per-row token counts (incl. <s> </s>)
-    uint32_t *locks;      // SLOW_THREADS pool-region locks (zeroed once)
-    uint32_t *err;        // set if a tile's ids exceeded its staging slot (cannot happen: checked)
+    uint32_t *fb_list;    // rows for the fallback kernels (n entries max)
+    uint32_t *fb_count;   // its length (zeroed before the launch)
+    uint32_t *fb2_list;   // rows the fallback fast kernel could not finish (pool kernel)
+    uint32_t *fb2_count;
+    uint32_t *err;        // set if an id fell outside its row's slot (never: bytes + 2 bound)
     uint64_t *passprof;   // optional: device cycles per pass, summed over waves (T_NPASS entries)
     uint64_t ntiles;
     int rows;             // R
@@ -178,36 +173,6 @@ __device__ __forceinline__ uint32_t decode_word(uint32_t x, int p, int e) {
 
 __device__ __forceinline__ int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }
 
-__device__ __forceinline__ uint32_t lds_decode(const uint8_t *B, int p, int e, int &len) {
-    const uint32_t c = B[p];
-    if (c < 0x80u) { len = 1; return c; }
-    const int l = c >= 0xF0u ? 4 : c >= 0xE0u ? 3 : c >= 0xC0u ? 2 : 0;
-    len = 1;
-    if (l == 0 || c > 0xF4u || p + l > e) return 0xFFFFFFFFu;
-    uint32_t cp = c & (0x7Fu >> l);
-    for (int k = 1; k < l; ++k) {
-        const uint32_t b = B[p + k];
-        if ((b & 0xC0u) != 0x80u) return 0xFFFFFFFFu;
-        cp = (cp << 6) | (b & 0x3Fu);
-    }
-    const uint32_t mn = l == 2 ? 0x80u : l == 3 ? 0x800u : 0x10000u;
-    if (cp < mn || cp > 0x10FFFFu) return 0xFFFFFFFFu;
-    len = l;
-    return cp;
-}
-
-template <int FLAGS>
-__device__ __forceinline__ uint32_t map_cp(const uint2 *fast, uint32_t cp) {
-    const uint2 pr = prop(fast, cp);
-    if (FLAGS == 3) return p_normmap(pr);
-    return p_allowed(pr) ? cp : 0u;  // FLAGS == 2
-}
-
-__device__ __forceinline__ bool hf_stable(const uint2 *fast, uint32_t x) {
-    const uint2 pr = prop(fast, x);
-    return p_ccc_hf(pr) == 0 && !p_second(pr);
-}
-
 __device__ __forceinline__ uint32_t single_id_of(const BpeDev &m, const uint16_t *sfast, uint32_t cp) {
     if (cp < FAST_N) return sfast[cp];
     int lo = 0, hi = (int)m.n_single - 1;
@@ -246,50 +211,10 @@ __device__ __forceinline__ int bpe_merge_lds(const BpeDev &m, uint16_t *W, int s
     return n;
 }
 
-// sequential fallback for one row (count or emit), private buffers first, then the locked pool
-template <int FLAGS, bool EMIT>
-__device__ __noinline__ uint64_t fallback_row(const TileArgs &ta, uint64_t r, const uint2 *fast, const uint16_t *sfast,
-                                 uint64_t emit_base, uint32_t wave_gid, uint32_t &status) {
-    uint32_t seg[T_FBSEG], dec[4 * T_FBSEG], seg2[T_FBSEG], dec2[4 * T_FBSEG];
-    uint16_t wsym[T_FBWORD];
-    uint32_t wpair[T_FBWORD];
-    Scratch sc;
-    sc.seg = seg; sc.dec = dec; sc.seg2 = seg2; sc.dec2 = dec2; sc.seg_cap = T_FBSEG;
-    sc.wsym = wsym; sc.wpair = wpair; sc.word_cap = T_FBWORD;
-    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
-    sc.slow_status = ST_SLOW;
-    sc.status = 0;
-    uint64_t cnt = process_row<OP_BPE, FLAGS, EMIT>(ta.ra, r, fast, sfast, &sc, emit_base);
-    if (sc.status & ST_SLOW) {
-        // one region per (wave, lane): lanes of one wave never wait on each other (a divergent spin
-        // on a lock held by a sibling lane would never converge); SLOW_THREADS is a multiple of 64
-        static_assert(SLOW_THREADS % 64 == 0, "pool regions must tile whole waves");
-        const uint32_t region = (wave_gid * 64u + (uint32_t)w_lane()) % SLOW_THREADS;
-        while (__hip_atomic_exchange(ta.locks + region, 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != 0u)
-            w_sleep();
-        const SlowPool &P = ta.ra.pool;
-        const uint64_t t = region;
-        sc.seg = P.seg + t * 2 * SLOW_SEG;
-        sc.dec = P.dec + t * 8 * SLOW_SEG;
-        sc.seg2 = sc.seg + SLOW_SEG;
-        sc.dec2 = sc.dec + 4 * SLOW_SEG;
-        sc.seg_cap = SLOW_SEG;
-        sc.wsym = P.wsym + t * SLOW_WORD;
-        sc.wpair = P.wpair + t * SLOW_WORD;
-        sc.word_cap = SLOW_WORD;
-        sc.slow_status = ST_LIMIT;
-        sc.status = 0;
-        cnt = process_row<OP_BPE, FLAGS, EMIT>(ta.ra, r, fast, sfast, &sc, emit_base);
-        __hip_atomic_store(ta.locks + region, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        if (sc.status & ST_LIMIT) cnt = 0;
-    }
-    status = (sc.status & ST_BAD_UTF8) | (sc.status & ST_LIMIT);
-    return cnt;
-}
-
 template <int FLAGS>
-__device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, const uint32_t *H, const uint16_t *sfast,
-                         TileWaveMem &M, uint32_t wave_gid, PassClock &pc) {
+__device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, const uint16_t *sfast, TileWaveMem &M,
+                         PassClock &pc) {
+    static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const uint64_t lt = w_lanemask_lt();
     const RowArgs &a = ta.ra;
@@ -300,7 +225,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     const uint64_t myoff = lane <= nr ? a.offs[r0 + lane] : 0ull;
     const uint64_t S0 = w_bcast(myoff, 0);
     const bool fits = lane >= 1 && lane <= nr && (myoff - S0) <= (uint64_t)T_BCAP;
-    const int k = w_popc(w_ballot(fits));  // rows 0..k-1 take the cooperative path
+    const int k = w_popc(w_ballot(fits));  // rows 0..k-1 are staged; the rest fall back
     const uint64_t S1 = w_bcast(myoff, k);
     const uint64_t a0 = S0 & ~15ull;
     {
@@ -309,146 +234,55 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         uint4 *dst = (uint4 *)M.bytes;
         for (uint64_t b = (uint64_t)lane; b < nblk; b += 64) dst[b] = src[b];
     }
-    if (lane < T_MAXR) { M.fbslot[lane] = 0xFF; M.hfbad[lane] = 0; }
+    if (lane < nr) {
+        M.fb[lane] = lane >= k ? 1 : 0;
+        M.rowslot[lane] = (uint32_t)(myoff - S0) + 2u * (uint32_t)lane;
+    }
     w_sync();
 
     pc.mark(TP_STAGE);
-    // ---------------- pass D: decode + NFC + map/filter -> V
-    uint8_t *FL = (uint8_t *)M.w;  // NFC leader flags by byte position (W is free until pass E)
+    // ---------------- pass D: decode + normalize_text map/filter -> V. If no char of the row
+    // trips nfc_trig, NFC is the identity on the row and every char maps on its own: one
+    // ballot-compacted write per lane. A row that trips (or has invalid UTF-8) falls back.
     uint32_t vpos = 0;
-    uint32_t nfb = 0;
     for (int i = 0; i < k; ++i) {
         const int s = (int)(w_bcast(myoff, i) - a0), e = (int)(w_bcast(myoff, i + 1) - a0);
         const uint32_t vstart = vpos;
         if (lane == 0) M.v[vpos] = V_B;
         ++vpos;
-        bool rowbad = false;
-        // Fast path: if no char of the row trips nfc_trig, NFC is the identity on the row and every
-        // char maps on its own: one ballot-compacted write per lane.
-        bool complex = false;
-        {
-            uint32_t carry_h = H_ROWSTART;  // hot word of the last char of the previous chunk
-            for (int base = s; base < e; base += 64) {
-                const int p = base + lane;
-                const bool in = p < e;
-                const uint32_t x = in ? lds_word(M.bytes, p) : 0u;
-                const bool lead = in && (x & 0xC0u) != 0x80u;
-                bool bad = in && p == s && !lead;
-                uint32_t h = 0;
-                if (lead) {
-                    const uint32_t cp = decode_word(x, p, e);
-                    if (cp == 0xFFFFFFFFu) bad = true;
-                    else h = hot(H, cp);
-                }
-                if (w_ballot(bad)) { rowbad = true; break; }
-                const uint64_t LEADS = w_ballot(lead);
-                const uint64_t pm = LEADS & lt;
-                const uint32_t hprev_l = w_shfl(h, pm ? msb64(pm) : 0);
-                const uint32_t hprev = pm ? hprev_l : carry_h;
-                const bool trig = lead && !(h & H_STABLE) && nfc_trig<false>(h, hprev);
-                if (w_ballot(trig)) { complex = true; break; }
-                if (LEADS) carry_h = w_bcast(h, msb64(LEADS));
-                const uint32_t mv = h & 0xFFFFu;
-                const uint64_t KM = w_ballot(mv != 0u);
-                if (mv) M.v[vpos + (uint32_t)w_popc(KM & lt)] = (uint16_t)mv;
-                vpos += (uint32_t)w_popc(KM);
-            }
-        }
-        if (complex) vpos = vstart + 1;
-        for (int base = s; complex && base < e; base += 64) {
+        bool fallback = false;
+        uint32_t carry_h = H_ROWSTART;  // hot word of the last char of the previous chunk
+        for (int base = s; base < e; base += 64) {
             const int p = base + lane;
             const bool in = p < e;
-            const uint32_t byte = in ? M.bytes[p] : 0u;
-            const bool lead = in && (byte & 0xC0u) != 0x80u;
+            const uint32_t x = in ? lds_word(M.bytes, p) : 0u;
+            const bool lead = in && (x & 0xC0u) != 0x80u;
             bool bad = in && p == s && !lead;
-            uint32_t cp = 0;
-            int len = 1;
-            uint2 pr = make_uint2(0, 0);
+            uint32_t h = 0;
             if (lead) {
-                cp = lds_decode(M.bytes, p, e, len);
+                const uint32_t cp = decode_word(x, p, e);
                 if (cp == 0xFFFFFFFFu) bad = true;
-                else pr = prop(fast, cp);
+                else h = hot(H, cp);
             }
-            const bool ok = lead && !bad;
-            const bool segstart = ok && (p == s || p_stable(pr));
-            bool changed = false;
-            int nout = 0;
-            uint32_t outs[4 * T_SEG];
-            bool need = false;
-            if (segstart) {
-                need = !p_stable(pr);  // a row-initial non-stable char (e.g. U+0958) is its own segment
-                if (!need && p + len < e) {
-                    int l2;
-                    const uint32_t c2 = lds_decode(M.bytes, p + len, e, l2);
-                    need = c2 != 0xFFFFFFFFu && !p_stable(prop(fast, c2));
-                }
-            }
-            {
-                if (need) {
-                    uint32_t seg[T_SEG], dec[4 * T_SEG];
-                    int n = 0;
-                    seg[n++] = cp;
-                    int q = p + len;
-                    while (q < e) {
-                        int lq;
-                        const uint32_t c = lds_decode(M.bytes, q, e, lq);
-                        if (c == 0xFFFFFFFFu || p_stable(prop(fast, c))) break;
-                        if (n == T_SEG) { bad = true; break; }
-                        seg[n++] = c;
-                        q += lq;
-                    }
-                    if (!bad) {
-                        const int wn = nfc_full<false>(seg, dec, n, 4 * T_SEG, fast);
-                        if (wn < 0) bad = true;
-                        else {
-                            changed = wn != n;
-                            for (int j = 0; j < wn && !changed; ++j) changed = dec[j] != seg[j];
-                            if (changed)
-                                for (int j = 0; j < wn; ++j) {
-                                    const uint32_t mv = map_cp<FLAGS>(fast, dec[j]);
-                                    if (mv) outs[nout++] = mv;
-                                }
-                        }
-                    }
-                }
-            }
-            if (segstart) FL[p] = changed ? 1 : 0;
-            if (w_ballot(bad)) { rowbad = true; break; }
-            w_sync();
-            bool inchg = false;
-            if (ok && !segstart) {
-                int q = p;
-                for (;;) {
-                    --q;
-                    while (q > s && (M.bytes[q] & 0xC0u) == 0x80u) --q;
-                    int lq;
-                    const uint32_t c = lds_decode(M.bytes, q, e, lq);
-                    if (q <= s || (c != 0xFFFFFFFFu && p_stable(prop(fast, c)))) break;
-                }
-                inchg = FL[q] != 0;
-            }
-            uint32_t cnt = 0, mval = 0;
-            if (ok) {
-                if (segstart && changed) cnt = (uint32_t)nout;
-                else if (!inchg) { mval = map_cp<FLAGS>(fast, cp); cnt = mval ? 1u : 0u; }
-            }
-            uint32_t tot;
-            const uint32_t ex = w_exscan(cnt, &tot);
-            if (cnt) {
-                if (segstart && changed) for (int j = 0; j < nout; ++j) M.v[vpos + ex + j] = (uint16_t)outs[j];
-                else M.v[vpos + ex] = (uint16_t)mval;
-            }
-            vpos += tot;
+            const uint64_t LEADS = w_ballot(lead);
+            const uint64_t pm = LEADS & lt;
+            const uint32_t hprev_l = w_shfl(h, pm ? msb64(pm) : 0);
+            const uint32_t hprev = pm ? hprev_l : carry_h;
+            const bool trig = bad || (lead && !(h & H_STABLE) && nfc_trig<false>(h, hprev));
+            if (w_ballot(trig)) { fallback = true; break; }
+            if (LEADS) carry_h = w_bcast(h, msb64(LEADS));
+            const uint32_t mv = h & 0xFFFFu;
+            const uint64_t KM = w_ballot(mv != 0u);
+            if (mv) M.v[vpos + (uint32_t)w_popc(KM & lt)] = (uint16_t)mv;
+            vpos += (uint32_t)w_popc(KM);
         }
-        if (rowbad) {
+        if (fallback) {
             vpos = vstart;
-            if (lane == 0) { M.v[vpos] = V_FB; M.fbrow[nfb] = (uint8_t)i; M.fbslot[i] = (uint8_t)nfb; }
-            ++vpos;
-            ++nfb;
-        } else {
-            if (lane == 0) M.v[vpos] = V_E;
-            ++vpos;
+            if (lane == 0) { M.v[vpos] = V_FB; M.fb[i] = 1; }
+        } else if (lane == 0) {
+            M.v[vpos] = V_E;
         }
+        ++vpos;
         w_sync();
     }
     const uint32_t vlen = vpos;
@@ -479,69 +313,39 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
     w_sync();
 
     pc.mark(TP_E);
-    // ---------------- pass H: HF NFKC (compat spaces -> ' ', then the HF-NFC quick check; the full
-    // per-segment check only runs on tiles where some char trips it)
-    bool hf_any = false;
+    // ---------------- pass H: HF NFKC (compat spaces -> ' '); a row where nfc_trig<true> trips
+    // falls back
     {
         uint32_t carry_h = H_ROWSTART;
+        uint32_t rs = 0;
+        bool any = false;
         for (uint32_t base = 0; base < wlen; base += 64) {
             const uint32_t kk = base + lane;
             const bool in = kk < wlen;
             const uint16_t x = in ? M.w[kk] : V_DEAD;
             const bool special = x >= V_SPECIAL;
+            const uint64_t RM = w_ballot(in && (x == V_B || x == V_FB));
             uint32_t h = special ? H_ROWSTART : hot(H, x);
             if (!special && (h & H_HFSPACE)) { M.w[kk] = 0x20; h = hot(H, 0x20); }
             const uint32_t hl = w_shfl(h, lane ? lane - 1 : 0);
             const uint32_t hprev = lane ? hl : carry_h;
             const bool trig = in && !special && !(h & H_HFST) && nfc_trig<true>(h, hprev);
-            if (w_ballot(trig)) hf_any = true;
+            if (trig) M.fb[rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1] = 1;
+            if (w_ballot(trig)) any = true;
+            rs += (uint32_t)w_popc(RM);
             carry_h = w_bcast(h, 63);
         }
-    }
-    w_sync();
-    for (uint32_t base = 0; hf_any && base < wlen; base += 64) {
-        const uint32_t kk = base + lane;
-        bool bad = false;
-        if (kk + 1 < wlen) {
-            const uint16_t x = M.w[kk];
-            const uint16_t y = M.w[kk + 1];
-            const bool lead = x < V_SPECIAL && (hf_stable(fast, x) || kk == 0 || M.w[kk - 1] >= V_SPECIAL);
-            if (lead && y < V_SPECIAL && !hf_stable(fast, y)) {
-                uint32_t seg[T_SEG], dec[4 * T_SEG];
-                int n = 0;
-                seg[n++] = x;
-                uint32_t q = kk + 1;
-                while (q < wlen && M.w[q] < V_SPECIAL && !hf_stable(fast, M.w[q])) {
-                    if (n == T_SEG) { bad = true; break; }
-                    seg[n++] = M.w[q++];
-                }
-                if (!bad) {
-                    const int wn = nfc_full<true>(seg, dec, n, 4 * T_SEG, fast);
-                    bool changed = wn != n;
-                    for (int j = 0; j < wn && !changed; ++j) changed = dec[j] != seg[j];
-                    bad = changed || wn < 0;
-                }
-            }
-        }
-        if (bad) {
-            int ri = 0;
-            while (ri + 1 < (int)rows_seen && M.wrow[ri + 1] <= kk) ++ri;
-            M.hfbad[ri] = 1;
-        }
-    }
-    w_sync();
-    for (int ri = 0; hf_any && ri < (int)rows_seen; ++ri) {
-        if (!M.hfbad[ri]) continue;  // uniform (LDS value)
-        const uint32_t b = M.wrow[ri], e2 = M.wrow[ri + 1];
-        for (uint32_t q = b + 1 + lane; q < e2; q += 64) M.w[q] = V_DEAD;
-        if (lane == 0) { M.w[b] = V_FB; M.fbrow[nfb] = (uint8_t)ri; M.fbslot[ri] = (uint8_t)nfb; }
-        ++nfb;
         w_sync();
-    }
-    // rows past the tile buffer
-    for (int i = k; i < nr; ++i) {
-        if (lane == 0) M.fbrow[nfb] = (uint8_t)i;
-        ++nfb;
+        for (uint32_t ri = 0; any && ri < rows_seen; ++ri) {
+            const uint32_t b = M.wrow[ri], e2 = M.wrow[ri + 1];
+            const bool conv = M.fb[ri] && M.w[b] == V_B;  // same value on every lane
+            w_sync();                                      // ... read before anyone writes
+            if (conv) {
+                for (uint32_t q = b + 1 + lane; q < e2; q += 64) M.w[q] = V_DEAD;
+                if (lane == 0) M.w[b] = V_FB;
+            }
+            w_sync();
+        }
     }
     w_sync();
 
@@ -588,6 +392,21 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
         wlen = wpos;
     }
     w_sync();
+    {   // keep only pre-tokens with >= 2 symbols (a single symbol has nothing to merge): with ~4 rows
+        // per tile the rest then fits one 64-lane batch
+        uint32_t nk = 0;
+        for (uint32_t base = 0; base < nw; base += 64) {
+            const uint32_t j = base + lane;
+            const uint16_t st = j < nw ? M.v[j] : (uint16_t)0;
+            const bool multi = j < nw && st + 1u < wlen && !(M.w[st + 1] & WSTART);
+            const uint64_t MM = w_ballot(multi);
+            w_sync();
+            if (multi) M.v[nk + (uint32_t)w_popc(MM & lt)] = st;
+            nk += (uint32_t)w_popc(MM);
+        }
+        nw = nk;
+    }
+    w_sync();
 
     pc.mark(TP_P);
     // ---------------- pass B: lane per pre-token, merge_all (lowest rank, leftmost on ties).
@@ -605,6 +424,10 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
 #pragma unroll
         for (int i = WREG - 1; i >= 1; --i) n = (sy[i] & WSTART) ? i : n;
         const bool reg = act && n < WREG;
+        int len = n;  // long pre-tokens: measured before any lane writes W back
+        if (act && !reg)
+            while (st + len < (int)wlen && !(M.w[st + len] & WSTART)) ++len;
+        w_sync();
 #pragma unroll
         for (int i = 0; i < WREG; ++i) sy[i] &= 0x7FFFu;
         uint32_t rk[WREG - 1];
@@ -645,99 +468,74 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint2 *fast, cons
 #pragma unroll
             for (int i = 0; i < WREG; ++i)
                 if (i < n) M.w[st + i] = i < nn ? (uint16_t)sy[i] : V_DEAD;
-        } else if (act) {  // long pre-token
-            int len = 1;
-            while (st + len < (int)wlen && !(M.w[st + len] & WSTART)) ++len;
+        } else if (act) {  // long pre-token: merge in LDS
             M.w[st] &= 0x7FFFu;
             (void)bpe_merge_lds(m, M.w, st, len);
         }
+        w_sync();
     }
-    w_sync();
 
     pc.mark(TP_B);
-    // ---------------- fallback rows: count
-    uint32_t fbst = 0;
-    uint64_t fbcnt = 0;
-    if ((uint32_t)lane < nfb) fbcnt = fallback_row<FLAGS, false>(ta, r0 + M.fbrow[lane], fast, sfast, 0, wave_gid, fbst);
-    if ((uint32_t)lane < nfb) { M.fbcount[lane] = (uint32_t)fbcnt; M.fbstat[lane] = (uint8_t)fbst; }
-    w_sync();
+    // ---------------- fallback rows: append to the list (rare: one atomic per tile that has any)
+    {
+        const bool isfb = lane < nr && M.fb[lane];
+        const uint64_t FM = w_ballot(isfb);
+        if (FM) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(ta.fb_count, (uint32_t)w_popc(FM));
+            base = w_bcast(base, 0);
+            if (isfb) ta.fb_list[base + (uint32_t)w_popc(FM & lt)] = (uint32_t)(r0 + (uint64_t)lane);
+        }
+    }
 
     pc.mark(TP_FBC);
-    // ---------------- pass F: weighted compaction W -> staged ids, row start positions
-    auto weight = [&](uint16_t x, uint32_t ridx) -> uint32_t {
-        if (x == V_FB) return M.fbcount[M.fbslot[ridx]];
-        return x == V_DEAD ? 0u : 1u;
-    };
-    const uint64_t sbase = S0 + 2 * r0;  // this tile's staging slot
-    const uint64_t scap = (S1 - S0) + 2 * (uint64_t)k + (w_bcast(myoff, nr) - S1) + 2 * (uint64_t)(nr - k);
+    // ---------------- pass F: ids -> each row's staging slot; row start positions
+    const uint64_t sbase = S0 + 2 * r0;
     uint32_t *stage = (uint32_t *)a.out + sbase;
+    const uint64_t scap = a.cap > sbase ? a.cap - sbase : 0;
     uint32_t pos = 0;
-    rows_seen = 0;
+    uint32_t rs = 0;
+    bool over = false;
     for (uint32_t base = 0; base < wlen; base += 64) {
         const uint32_t kk = base + lane;
         const bool in = kk < wlen;
         const uint16_t x = in ? M.w[kk] : V_DEAD;
         const bool isrow = in && (x == V_B || x == V_FB);
-        const uint64_t rm = w_ballot(isrow);
-        const uint32_t ridx = rows_seen + (uint32_t)w_popc(rm & lt);
-        const uint32_t wgt = in ? weight(x, ridx) : 0u;
-        uint32_t tot;
-        const uint32_t op = pos + w_exscan(wgt, &tot);
-        const bool fits = op < scap;
-        if (isrow) M.rowop[ridx] = op;
-        if (x == V_B) {
-            if (fits) stage[op] = m.bos;
-        } else if (x == V_FB) {
-            M.fbbase[M.fbslot[ridx]] = sbase + op;
-        } else if (x == V_E) {
-            if (fits) stage[op] = m.eos;
-        } else if (in && x != V_DEAD) {
-            if (fits) stage[op] = x & 0x7FFFu;
+        const uint64_t RM = w_ballot(isrow);
+        const bool emit = in && x != V_FB && x != V_DEAD;
+        const uint64_t EM = w_ballot(emit);
+        const uint32_t op = pos + (uint32_t)w_popc(EM & lt);
+        if (isrow) M.rowop[rs + (uint32_t)w_popc(RM & lt)] = op;
+        w_sync();
+        if (emit) {
+            const uint32_t row = rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1;
+            const uint64_t d = (uint64_t)M.rowslot[row] + (op - M.rowop[row]);
+            const uint32_t val = x == V_B ? m.bos : x == V_E ? m.eos : (uint32_t)(x & 0x7FFFu);
+            if (d < scap) stage[d] = val;
+            else over = true;
         }
-        pos += tot;
-        rows_seen += (uint32_t)w_popc(rm);
+        pos += (uint32_t)w_popc(EM);
+        rs += (uint32_t)w_popc(RM);
     }
-    {   // rows past the tile buffer follow the cooperative rows
-        uint32_t tail = 0;
-        const bool istail = (uint32_t)lane < nfb && M.fbrow[lane] >= k;
-        if (istail) tail = M.fbcount[lane];
-        uint32_t tt;
-        const uint32_t ex = w_exscan(tail, &tt);
-        if (istail) {
-            M.fbbase[lane] = sbase + pos + ex;
-            M.rowop[M.fbrow[lane]] = pos + ex;
-        }
-        pos += tt;
-    }
-    if (lane == 0) M.rowop[nr] = pos;
-    if (pos > scap && lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) M.rowop[rs] = pos;
+    if (w_ballot(over) && lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     w_sync();
-    if (lane < nr) ta.counts[r0 + lane] = M.rowop[lane + 1] - M.rowop[lane];
+    if (lane < nr && !M.fb[lane]) {
+        ta.counts[r0 + lane] = M.rowop[lane + 1] - M.rowop[lane];
+        if (a.row_status) a.row_status[r0 + lane] = 0;
+    }
+    w_sync();
     pc.mark(TP_F);
-
-    // ---------------- fallback rows: emit into the staging slot
-    if ((uint32_t)lane < nfb && pos <= scap) {
-        uint32_t st2;
-        (void)fallback_row<FLAGS, true>(ta, r0 + M.fbrow[lane], fast, sfast, M.fbbase[lane], wave_gid, st2);
-    }
-    if (a.row_status && lane < nr) {
-        uint8_t st3 = 0;
-        for (uint32_t j = 0; j < nfb; ++j)
-            if (M.fbrow[j] == lane) st3 = M.fbstat[j];
-        a.row_status[r0 + lane] = st3;
-    }
-    w_sync();
-    pc.mark(TP_FBE);
 }
 
 template <int FLAGS>
-__device__ void bpe_tiles_wave(const TileArgs &ta, const uint2 *fast, const uint32_t *H, const uint16_t *sfast,
-                               TileWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
+__device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *sfast, TileWaveMem &M,
+                               uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr);
     for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {  // static stride: tiles are near-equal
         pc.mark(TP_LOOP);
-        bpe_tile<FLAGS>(ta, t, fast, H, sfast, M, wave_gid, pc);
+        bpe_tile<FLAGS>(ta, t, H, sfast, M, pc);
     }
     pc.flush(ta.passprof);
 }

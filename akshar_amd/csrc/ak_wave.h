@@ -74,6 +74,9 @@ inline uint64_t clock64() { return 0; }
 inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v) {
     return reinterpret_cast<std::atomic<unsigned long long> *>(p)->fetch_add(v, std::memory_order_relaxed);
 }
+inline uint32_t atomicAdd(uint32_t *p, uint32_t v) {
+    return reinterpret_cast<std::atomic<uint32_t> *>(p)->fetch_add(v, std::memory_order_relaxed);
+}
 
 #else
 #include <hip/hip_runtime.h>

@@ -153,20 +153,15 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     static uint32_t hot_tab[FAST_N];
     for (uint32_t i = 0; i < FAST_N; ++i) { fast[i] = prop_global(i); hot_tab[i] = hot_of(fast[i]); }
     if (n == 0) { out_offs[0] = 0; return 0; }
-    std::vector<uint32_t> stage(offs[n] + 2 * n + 64), counts(n);
+    std::vector<uint32_t> stage(offs[n] + 2 * n + 64), counts(n), fbl(n), fb2(n);
+    uint32_t fbn = 0, fb2n = 0, err = 0;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = stage.size();
     ta.ra.row_status = row_status; ta.ra.bpe = m->bdev; ta.ra.single_fast = m->bpe.fast.data();
-    // one pool region per lane of the emulated wave (wave 0 uses regions 0..63)
-    std::vector<uint32_t> seg(64 * 2 * SLOW_SEG), dec(64 * 8 * SLOW_SEG), wpair(64 * SLOW_WORD), vchar(64 * SLOW_WORD);
-    std::vector<uint16_t> wsym(64 * SLOW_WORD);
-    ta.ra.pool.seg = seg.data(); ta.ra.pool.dec = dec.data(); ta.ra.pool.wsym = wsym.data();
-    ta.ra.pool.wpair = wpair.data(); ta.ra.pool.vchar = vchar.data();
     const uint64_t ntiles = (n + rows - 1) / rows;
-    uint32_t err = 0;
-    std::vector<uint32_t> locks(SLOW_THREADS, 0);
-    ta.counts = counts.data(); ta.locks = locks.data(); ta.err = &err;
+    ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
+    ta.fb2_count = &fb2n; ta.err = &err;
     ta.ntiles = ntiles; ta.rows = rows;
     TileWaveMem *M = new TileWaveMem();
     EmuWave W;
@@ -175,18 +170,30 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
         th.emplace_back([&, lane] {
             t_lane = lane;
             t_wave = &W;
-            bpe_tiles_wave<3>(ta, fast, hot_tab, m->bpe.fast.data(), *M, 0, 1);
+            bpe_tiles_wave<3>(ta, hot_tab, m->bpe.fast.data(), *M, 0, 1);
         });
     for (auto &x : th) x.join();
     delete M;
     if (err) return -1;
-    // scan + per-tile copy, as the launcher's scan_counts and k_tile_copy
+    // fallback rows as k_tile_fb / k_tile_fb_slow: the row pipeline straight into the row's slot
+    std::vector<uint32_t> seg(2 * SLOW_SEG), dec(8 * SLOW_SEG), wpair(SLOW_WORD);
+    std::vector<uint16_t> wsym(SLOW_WORD);
+    for (uint32_t i = 0; i < fbn; ++i) {
+        const uint64_t r = fbl[i];
+        Scratch sc;
+        sc.seg = seg.data(); sc.dec = dec.data(); sc.seg2 = seg.data() + SLOW_SEG; sc.dec2 = dec.data() + 4 * SLOW_SEG;
+        sc.seg_cap = SLOW_SEG; sc.wsym = wsym.data(); sc.wpair = wpair.data(); sc.word_cap = SLOW_WORD;
+        sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
+        sc.slow_status = ST_LIMIT; sc.status = 0;
+        const uint64_t cnt = process_row<OP_BPE, 3, true>(ta.ra, r, fast, m->bpe.fast.data(), &sc, offs[r] + 2 * r);
+        const bool lim = (sc.status & ST_LIMIT) != 0;
+        counts[r] = lim ? 0 : (uint32_t)cnt;
+        if (row_status) row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0));
+    }
+    // scan + per-row copy, as the launcher's scan_counts and k_tile_copy
     out_offs[0] = 0;
     for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
-    for (uint64_t t = 0; t < ntiles; ++t) {
-        const uint64_t r0 = t * rows, r1 = std::min<uint64_t>(r0 + rows, n);
-        const uint32_t *src = stage.data() + offs[r0] + 2 * r0;
-        for (uint64_t i = 0; i < out_offs[r1] - out_offs[r0] && out_offs[r0] + i < cap; ++i) out[out_offs[r0] + i] = src[i];
-    }
+    for (uint64_t r = 0; r < n; ++r)
+        for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = stage[offs[r] + 2 * r + i];
     return (int64_t)out_offs[n];
 }

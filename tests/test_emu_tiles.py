@@ -52,3 +52,17 @@ def test_synthetic_vs_oracle(em, bpe_model, kind):
     ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+@pytest.mark.parametrize("rows", [2, 5])
+def test_mixed_pretoken_lengths(em, bpe_model, rows):
+    """Pre-tokens of 1, short (register merges), >= WREG (LDS merges) and > 64 symbols side by side
+    in one tile, so the long-word length scan runs after neighbouring words were written back."""
+    words = ["a", "hi", "namaste", "abcdefghijklmnop", "अनुच्छेदविभागीकरणसम्बन्धित", "क्षत्रिय", "?!",
+             "abcdefghijklmnopqrstuvwxyzabcdefghijklmnopqrstuvwxyzabcdefghijklmnopqrstuv", "ok", "धर्मक्षेत्रे"]
+    rng = np.random.default_rng(11)
+    texts = [" ".join(rng.choice(words, size=rng.integers(1, 12))) for _ in range(300)]
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=rows)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)
