@@ -114,7 +114,8 @@ struct ak_bpe {
     uint16_t *d_single_fast = nullptr;  // FAST_N entries
     uint32_t *d_single_cp = nullptr;
     uint16_t *d_single_id = nullptr;
-    bool tile_ok = false;  // every id < 0x7FFC: the tile kernel tags ids with bit 15 (ak_tile.h WSTART)
+    bool tile_ok = false;  // every id < 0x7FFC (the tile kernel tags ids with bit 15, ak_tile.h WSTART) and
+                           // new ids strictly increasing with rank (it compares merges by new id)
 };
 
 struct ak_spm {
@@ -134,7 +135,11 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     const std::string err = akb::build_bpe(n_single, single_cp, single_id, n_merges, merges, t);
     uint32_t max_id = std::max(bos, eos);
     for (uint32_t i = 0; i < n_single; ++i) max_id = std::max(max_id, single_id[i]);
-    for (uint64_t i = 0; i < n_merges; ++i) max_id = std::max(max_id, merges[3 * i + 2]);
+    bool monotone = true;  // the tile path picks the lowest rank as the smallest new id
+    for (uint64_t i = 0; i < n_merges; ++i) {
+        max_id = std::max(max_id, merges[3 * i + 2]);
+        if (i && merges[3 * i + 2] <= merges[3 * (i - 1) + 2]) monotone = false;
+    }
     if (!err.empty()) return fail(AK_ERR_UNSUPPORTED, ("ak_bpe_create: " + err).c_str());
     ak_bpe *m = new ak_bpe();
     HIP_TRY(hipMalloc(&m->d_tab, t.tab.size() * sizeof(uint64_t)));
@@ -153,7 +158,7 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     m->dev.n_single = t.n_rest;
     m->dev.bos = bos;
     m->dev.eos = eos;
-    m->tile_ok = max_id < 0x7FFCu;
+    m->tile_ok = max_id < 0x7FFCu && monotone;
     *out = m;
     return AK_OK;
 }

@@ -36,7 +36,7 @@ constexpr uint16_t V_B = 0xFFFE;
 constexpr uint16_t V_E = 0xFFFF;
 constexpr uint16_t V_SPECIAL = 0xFFFC;  // values >= this are sentinels / dead
 constexpr uint16_t WSTART = 0x8000;     // first symbol of a pre-token (ids are < 0x7FFC: checked at load)
-constexpr int WREG = 12;                // pre-tokens up to WREG-1 symbols merge in registers
+constexpr int WREG = 16;                // pre-tokens up to WREG-1 symbols take the rank-row merge loop
 
 struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
@@ -172,6 +172,18 @@ __device__ __forceinline__ uint32_t decode_word(uint32_t x, int p, int e) {
 }
 
 __device__ __forceinline__ int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }
+
+// per-half unsigned 16-bit min of two packed pairs (v_pk_min_u16)
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+#ifdef AK_HOST_EMU
+    const uint32_t lo = (a & 0xFFFFu) < (b & 0xFFFFu) ? (a & 0xFFFFu) : (b & 0xFFFFu);
+    const uint32_t hi = (a >> 16) < (b >> 16) ? (a >> 16) : (b >> 16);
+    return lo | (hi << 16);
+#else
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
+#endif
+}
 
 __device__ __forceinline__ uint32_t single_id_of(const BpeDev &m, const uint16_t *sfast, uint32_t cp) {
     if (cp < FAST_N) return sfast[cp];
@@ -393,7 +405,9 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, cons
     }
     w_sync();
     {   // keep only pre-tokens with >= 2 symbols (a single symbol has nothing to merge): with ~4 rows
-        // per tile the rest then fits one 64-lane batch
+        // per tile the rest then fits one 64-lane batch. The kept starts go to the TOP of V
+        // (V[T_E-1-k]) so pass B can use bytes + the bottom of V for its rank rows; the read and
+        // write ranges never meet (singles + 2 * multis <= chars < T_E).
         uint32_t nk = 0;
         for (uint32_t base = 0; base < nw; base += 64) {
             const uint32_t j = base + lane;
@@ -401,7 +415,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, cons
             const bool multi = j < nw && st + 1u < wlen && !(M.w[st + 1] & WSTART);
             const uint64_t MM = w_ballot(multi);
             w_sync();
-            if (multi) M.v[nk + (uint32_t)w_popc(MM & lt)] = st;
+            if (multi) M.v[T_E - 1 - (nk + (uint32_t)w_popc(MM & lt))] = st;
             nk += (uint32_t)w_popc(MM);
         }
         nw = nk;
@@ -410,69 +424,89 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, cons
 
     pc.mark(TP_P);
     // ---------------- pass B: lane per pre-token, merge_all (lowest rank, leftmost on ties).
-    // Pre-tokens of < WREG symbols merge in registers: one min over the pair ranks per round, the
-    // merge as a static shift network, two cuckoo lookups for the new neighbours; longer ones merge
-    // in LDS (bpe_merge_lds). The loop runs while any lane still has a merge.
-    for (uint32_t wb = 0; wb < nw; wb += 64) {
-        const uint32_t j = wb + lane;
-        const bool act = j < nw;
-        const int st = act ? (int)M.v[j] : 0;
-        uint32_t sy[WREG];
+    // Pre-tokens of < WREG symbols: the symbols stay in place in W (merged-away slots become
+    // V_DEAD, an alive-slot bitmask finds neighbours), the pair values live in a per-lane 32-byte
+    // LDS row of u16 new ids (bytes + bottom of V; new ids increase with rank: checked at load, so
+    // the smallest id is the lowest rank). One round = 2 ds_read_b128 + a packed-u16 min + two
+    // cuckoo lookups for the new neighbours + 3 u16 writes. Longer pre-tokens merge in LDS.
+    {
+        // 64 rank rows fit bytes + the part of V below the kept starts (at most T_BCAP / 2 of them)
+        static_assert(64 * 2 * WREG <= (T_BCAP + 32) + 2 * (T_E - T_BCAP / 2), "rank rows overlap the starts");
+        uint16_t *rk16 = (uint16_t *)(M.bytes + lane * (2 * WREG));
+        for (uint32_t wb = 0; wb < nw; wb += 64) {
+            const uint32_t j = wb + lane;
+            const bool act = j < nw;
+            const int st = act ? (int)M.v[T_E - 1 - j] : 0;
+            uint32_t sy[WREG];
 #pragma unroll
-        for (int i = 0; i < WREG; ++i) sy[i] = (act && st + i < (int)wlen) ? M.w[st + i] : 0xFFFFu;
-        int n = WREG;
+            for (int i = 0; i < WREG; ++i) sy[i] = (act && st + i < (int)wlen) ? M.w[st + i] : 0xFFFFu;
+            int n = WREG;
 #pragma unroll
-        for (int i = WREG - 1; i >= 1; --i) n = (sy[i] & WSTART) ? i : n;
-        const bool reg = act && n < WREG;
-        int len = n;  // long pre-tokens: measured before any lane writes W back
-        if (act && !reg)
-            while (st + len < (int)wlen && !(M.w[st + len] & WSTART)) ++len;
-        w_sync();
+            for (int i = WREG - 1; i >= 1; --i) n = (sy[i] & WSTART) ? i : n;
+            const bool reg = act && n < WREG;
+            int len = n;  // long pre-tokens: measured before any lane writes W back
+            if (act && !reg)
+                while (st + len < (int)wlen && !(M.w[st + len] & WSTART)) ++len;
+            uint32_t d[WREG / 2];
 #pragma unroll
-        for (int i = 0; i < WREG; ++i) sy[i] &= 0x7FFFu;
-        uint32_t rk[WREG - 1];
-#pragma unroll
-        for (int i = 0; i < WREG - 1; ++i) rk[i] = (reg && i + 1 < n) ? merge_lookup(m, sy[i], sy[i + 1]) : 0xFFFFFFFFu;
-        int nn = reg ? n : 0;
-        for (;;) {
-            uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-            for (int i = 0; i < WREG - 1; ++i) {
-                const uint32_t key = (rk[i] & 0xFFFF0000u) | (uint32_t)i;
-                best = key < best ? key : best;
+            for (int k = 0; k < WREG / 2; ++k) {
+                const int i = 2 * k;
+                const uint32_t lo = (reg && i + 1 < n) ? merge_lookup(m, sy[i] & 0x7FFFu, sy[i + 1]) & 0xFFFFu : 0xFFFFu;
+                const uint32_t hi = (i + 2 < WREG && reg && i + 2 < n) ? merge_lookup(m, sy[i + 1], sy[(i + 2) % WREG]) & 0xFFFFu : 0xFFFFu;
+                d[k] = lo | (hi << 16);
             }
-            const bool mg = best < 0xFFFF0000u;
-            if (!w_ballot(mg)) break;
-            if (mg) {
-                const int bi = (int)(best & 15u);
-                uint32_t nid = 0;
+            w_sync();  // every lane has read V and its window before rank rows overwrite bytes / V
+            if (reg) {
+                uint4 *r4 = (uint4 *)rk16;
+                r4[0] = make_uint4(d[0], d[1], d[2], d[3]);
+                r4[1] = make_uint4(d[4], d[5], d[6], d[7]);
+                M.w[st] = (uint16_t)(sy[0] & 0x7FFFu);
+            }
+            uint32_t alive = reg ? (1u << n) - 1u : 0u;
+            for (;;) {
+                uint32_t e[WREG / 2];
+                if (reg) {
+                    const uint4 *r4 = (const uint4 *)rk16;
+                    const uint4 x0 = r4[0], x1 = r4[1];
+                    e[0] = x0.x; e[1] = x0.y; e[2] = x0.z; e[3] = x0.w; e[4] = x1.x; e[5] = x1.y; e[6] = x1.z; e[7] = x1.w;
+                } else {
 #pragma unroll
-                for (int i = 0; i < WREG - 1; ++i) nid = i == bi ? (rk[i] & 0xFFFFu) : nid;
-#pragma unroll
-                for (int i = 0; i < WREG; ++i) sy[i] = i < bi ? sy[i] : (i == bi ? nid : (i + 1 < WREG ? sy[i + 1] : 0u));
-                nn -= 1;
-                uint32_t left = 0, right = 0;
-#pragma unroll
-                for (int i = 0; i < WREG; ++i) {
-                    left = i + 1 == bi ? sy[i] : left;
-                    right = i == bi + 1 ? sy[i] : right;
+                    for (int k = 0; k < WREG / 2; ++k) e[k] = 0xFFFFFFFFu;
                 }
-                const uint32_t L = bi > 0 ? merge_lookup(m, left, nid) : 0xFFFFFFFFu;
-                const uint32_t R = bi + 1 < nn ? merge_lookup(m, nid, right) : 0xFFFFFFFFu;
+                uint32_t mv = e[0];
 #pragma unroll
-                for (int i = 0; i < WREG - 1; ++i)
-                    rk[i] = i + 1 < bi ? rk[i] : (i + 1 == bi ? L : (i == bi ? R : (i + 1 < WREG - 1 ? rk[i + 1] : 0xFFFFFFFFu)));
+                for (int k = 1; k < WREG / 2; ++k) mv = pk_min_u16(mv, e[k]);
+                const uint32_t minv = (mv & 0xFFFFu) < (mv >> 16) ? (mv & 0xFFFFu) : (mv >> 16);
+                const bool mg = minv != 0xFFFFu;
+                if (!w_ballot(mg)) break;
+                if (mg) {
+                    int bi = 0;
+#pragma unroll
+                    for (int i = WREG - 2; i >= 0; --i) bi = ((e[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu) == minv ? i : bi;
+                    const uint32_t after = alive >> (bi + 1);
+                    const int jn = bi + 1 + __builtin_ctz(after);  // the right symbol of the pair
+                    const uint32_t below = alive & ((1u << bi) - 1u);
+                    const int pl = below ? 31 - __builtin_clz(below) : -1;
+                    const uint32_t aj = jn + 1 < 32 ? alive >> (jn + 1) : 0u;
+                    const int q = aj ? jn + 1 + __builtin_ctz(aj) : -1;
+                    const uint32_t left = pl >= 0 ? M.w[st + pl] : 0u;
+                    const uint32_t right = q >= 0 ? M.w[st + q] : 0u;
+                    M.w[st + bi] = (uint16_t)minv;
+                    M.w[st + jn] = V_DEAD;
+                    alive &= ~(1u << jn);
+                    const uint32_t L = pl >= 0 ? merge_lookup(m, left, minv) & 0xFFFFu : 0xFFFFu;
+                    const uint32_t R = q >= 0 ? merge_lookup(m, minv, right) & 0xFFFFu : 0xFFFFu;
+                    if (pl >= 0) rk16[pl] = (uint16_t)L;
+                    rk16[bi] = (uint16_t)R;
+                    rk16[jn] = 0xFFFFu;
+                }
             }
+            if (act && !reg) {  // long pre-token: merge in LDS
+                M.w[st] &= 0x7FFFu;
+                (void)bpe_merge_lds(m, M.w, st, len);
+            }
+            w_sync();
         }
-        if (reg) {
-#pragma unroll
-            for (int i = 0; i < WREG; ++i)
-                if (i < n) M.w[st + i] = i < nn ? (uint16_t)sy[i] : V_DEAD;
-        } else if (act) {  // long pre-token: merge in LDS
-            M.w[st] &= 0x7FFFu;
-            (void)bpe_merge_lds(m, M.w, st, len);
-        }
-        w_sync();
     }
 
     pc.mark(TP_B);
