@@ -21,12 +21,11 @@ constexpr int FB_BLOCK = 256;
 template <int FLAGS>
 __global__ __launch_bounds__(TILE_BLOCK, 4) void k_bpe_tiles(TileArgs ta) {
     __shared__ uint32_t hot_tab[FAST_N];
-    __shared__ uint16_t sfast[FAST_N];
+    __shared__ uint16_t sfast[SFAST_N];
     __shared__ TileWaveMem wm[TILE_BLOCK / 64];
-    for (uint32_t i = threadIdx.x; i < FAST_N; i += TILE_BLOCK) {
-        hot_tab[i] = hot_of(prop_global(i));
-        sfast[i] = ta.ra.single_fast[i];
-    }
+    for (uint32_t i = threadIdx.x; i < FAST_N; i += TILE_BLOCK) hot_tab[i] = hot_of(prop_global(i));
+    for (uint32_t i = threadIdx.x; i < SFAST_N; i += TILE_BLOCK)
+        sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
     bpe_tiles_wave<FLAGS>(ta, hot_tab, sfast, wm[wave], blockIdx.x * (TILE_BLOCK / 64) + wave,

@@ -185,14 +185,23 @@ __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
 #endif
 }
 
-__device__ __forceinline__ uint32_t single_id_of(const BpeDev &m, const uint16_t *sfast, uint32_t cp) {
-    if (cp < FAST_N) return sfast[cp];
+// single-char vocab ids in LDS for the chars normalize_text can produce as word chars: ASCII and
+// U+0900..U+09FF (SFAST_N entries); anything else reads the model's global tables
+constexpr uint32_t SFAST_N = 0x80 + 0x100;
+__device__ __forceinline__ uint32_t sfast_index(uint32_t cp) {
+    return cp < 0x80u ? cp : (cp - 0x900u < 0x100u ? cp - 0x900u + 0x80u : 0xFFFFFFFFu);
+}
+__device__ __forceinline__ uint32_t single_id_of(const BpeDev &m, const uint16_t *sfast, const uint16_t *gfast,
+                                                 uint32_t cp) {
+    const uint32_t k = sfast_index(cp);
+    if (k != 0xFFFFFFFFu) return sfast[k];
+    if (cp < FAST_N) return gfast[cp];
     int lo = 0, hi = (int)m.n_single - 1;
     while (lo <= hi) {
         const int mid = (lo + hi) >> 1;
-        const uint32_t k = m.single_sorted_cp[mid];
-        if (k == cp) return m.single_sorted_id[mid];
-        if (k < cp) lo = mid + 1; else hi = mid - 1;
+        const uint32_t key = m.single_sorted_cp[mid];
+        if (key == cp) return m.single_sorted_id[mid];
+        if (key < cp) lo = mid + 1; else hi = mid - 1;
     }
     return 0xFFFFu;
 }
@@ -381,7 +390,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, cons
             const bool wordchar = !special && cls != HF_S;
             const uint64_t SM = w_ballot(wordchar && cls != cprev);
             const uint32_t word = carry_word + (uint32_t)w_popc(SM & (lt | (1ull << lane)));  // inclusive
-            const uint32_t id = wordchar ? single_id_of(m, sfast, x) : 0xFFFFu;
+            const uint32_t id = wordchar ? single_id_of(m, sfast, a.single_fast, x) : 0xFFFFu;
             const bool kept = id != 0xFFFFu;
             const uint64_t KM = w_ballot(kept);
             const uint64_t pk = KM & lt;

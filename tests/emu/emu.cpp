@@ -163,6 +163,8 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
     ta.fb2_count = &fb2n; ta.err = &err;
     ta.ntiles = ntiles; ta.rows = rows;
+    std::vector<uint16_t> sfast(SFAST_N);
+    for (uint32_t i = 0; i < SFAST_N; ++i) sfast[i] = m->bpe.fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     TileWaveMem *M = new TileWaveMem();
     EmuWave W;
     std::vector<std::thread> th;
@@ -170,7 +172,7 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
         th.emplace_back([&, lane] {
             t_lane = lane;
             t_wave = &W;
-            bpe_tiles_wave<3>(ta, hot_tab, m->bpe.fast.data(), *M, 0, 1);
+            bpe_tiles_wave<3>(ta, hot_tab, sfast.data(), *M, 0, 1);
         });
     for (auto &x : th) x.join();
     delete M;
