@@ -42,7 +42,6 @@ struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
     uint16_t v[T_E];
     uint16_t w[T_E + 16];        // +16: pass B reads WREG-symbol windows past a pre-token start
-    uint16_t wrow[T_MAXR + 1];   // W index of each cooperative row's sentinel
     uint8_t fb[T_MAXR];          // row goes to the fallback kernels
     uint32_t rowslot[T_MAXR];    // row's staging slot, relative to the tile's (S0 + 2 r0)
     uint32_t rowop[T_MAXR + 1];  // row's first position in the tile's id stream
@@ -310,124 +309,80 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, cons
     w_sync();
 
     pc.mark(TP_D);
-    // ---------------- pass E: remove_elongations V -> W (+ row sentinel positions)
-    uint32_t wlen = 0, rows_seen = 0;
-    for (uint32_t base = 0; base < vlen; base += 64) {
-        const uint32_t kk = base + lane;
-        const bool in = kk < vlen;
-        const uint16_t x = in ? M.v[kk] : V_DEAD;
-        const uint16_t pa = in && kk >= 1 ? M.v[kk - 1] : V_DEAD;
-        const uint16_t pb = in && kk >= 2 ? M.v[kk - 2] : V_DEAD;
-        const uint16_t nx = in && kk + 1 < vlen ? M.v[kk + 1] : V_DEAD;
-        const bool drop = in && x < V_SPECIAL && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
-        const bool keep = in && !drop;
-        const uint64_t km = w_ballot(keep);
-        const uint32_t pos = wlen + (uint32_t)w_popc(km & lt);
-        const bool isrow = in && (x == V_B || x == V_FB);
-        const uint64_t rm = w_ballot(isrow);
-        if (keep) M.w[pos] = x;
-        if (isrow) M.wrow[rows_seen + w_popc(rm & lt)] = (uint16_t)pos;
-        wlen += (uint32_t)w_popc(km);
-        rows_seen += (uint32_t)w_popc(rm);
-    }
-    if (lane == 0) M.wrow[rows_seen] = (uint16_t)wlen;
-    w_sync();
-
-    pc.mark(TP_E);
-    // ---------------- pass H: HF NFKC (compat spaces -> ' '); a row where nfc_trig<true> trips
-    // falls back
+    // ---------------- pass N (fused): remove_elongations, HF NFKC, Whitespace pre-tokenizer and
+    // single-char ids in one sweep over V, writing the compacted id stream to W:
+    //   elongation  drop x when x == prev and (prev == prev2 or next == x)  (runs >= 3, not '\n')
+    //   HF NFKC     compat spaces -> ' '; a row where nfc_trig<true> trips is marked for fallback
+    //               (pass F skips its ids, the fallback kernels encode it)
+    //   pre-tokens  \w+ | [^\w\s]+ over the kept chars; chars outside the vocab vanish
+    //               (unk_token None); the first kept id of each pre-token carries WSTART
+    // "previous" always means the previous KEPT element (shuffled from its lane or carried over).
+    uint32_t wlen = 0;
     {
-        uint32_t carry_h = H_ROWSTART;
-        uint32_t rs = 0;
-        bool any = false;
-        for (uint32_t base = 0; base < wlen; base += 64) {
-            const uint32_t kk = base + lane;
-            const bool in = kk < wlen;
-            const uint16_t x = in ? M.w[kk] : V_DEAD;
-            const bool special = x >= V_SPECIAL;
-            const uint64_t RM = w_ballot(in && (x == V_B || x == V_FB));
-            uint32_t h = special ? H_ROWSTART : hot(H, x);
-            if (!special && (h & H_HFSPACE)) { M.w[kk] = 0x20; h = hot(H, 0x20); }
-            const uint32_t hl = w_shfl(h, lane ? lane - 1 : 0);
-            const uint32_t hprev = lane ? hl : carry_h;
-            const bool trig = in && !special && !(h & H_HFST) && nfc_trig<true>(h, hprev);
-            if (trig) M.fb[rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1] = 1;
-            if (w_ballot(trig)) any = true;
-            rs += (uint32_t)w_popc(RM);
-            carry_h = w_bcast(h, 63);
-        }
-        w_sync();
-        for (uint32_t ri = 0; any && ri < rows_seen; ++ri) {
-            const uint32_t b = M.wrow[ri], e2 = M.wrow[ri + 1];
-            const bool conv = M.fb[ri] && M.w[b] == V_B;  // same value on every lane
-            w_sync();                                      // ... read before anyone writes
-            if (conv) {
-                for (uint32_t q = b + 1 + lane; q < e2; q += 64) M.w[q] = V_DEAD;
-                if (lane == 0) M.w[b] = V_FB;
-            }
-            w_sync();
-        }
-    }
-    w_sync();
-
-    pc.mark(TP_H);
-    // ---------------- pass P: Whitespace pre-tokenizer (\w+ | [^\w\s]+) + single-char ids.
-    // In place, W becomes: row sentinels and the ids of the chars that are in the vocab (others
-    // vanish, unk_token None), each pre-token's first kept id tagged WSTART; V gets the starts.
-    uint32_t nw = 0;
-    {
-        uint32_t wpos = 0;
+        uint32_t carry_h = H_ROWSTART, carry_word = 0, carry_kword = 0xFFFFFFFFu, rs = 0;
         int carry_cls = HF_S;
-        uint32_t carry_word = 0, carry_kword = 0xFFFFFFFFu;
-        for (uint32_t base = 0; base < wlen; base += 64) {
+        for (uint32_t base = 0; base < vlen; base += 64) {
             const uint32_t kk = base + lane;
-            const bool in = kk < wlen;
-            const uint16_t x = in ? M.w[kk] : V_DEAD;
+            const bool in = kk < vlen;
+            uint16_t x = in ? M.v[kk] : V_DEAD;
+            const uint16_t pa = in && kk >= 1 ? M.v[kk - 1] : V_DEAD;
+            const uint16_t pb = in && kk >= 2 ? M.v[kk - 2] : V_DEAD;
+            const uint16_t nx = in && kk + 1 < vlen ? M.v[kk + 1] : V_DEAD;
             const bool special = x >= V_SPECIAL;
-            const int cls = special ? HF_S : (int)((hot(H, x) >> H_CLS_SHIFT) & 3u);
-            const int cl_l = w_shfl(cls, lane ? lane - 1 : 0);
-            const int cprev = lane ? cl_l : carry_cls;
-            const bool wordchar = !special && cls != HF_S;
+            const bool drop = in && !special && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
+            const bool keep = in && !drop;
+            uint32_t h = special ? H_ROWSTART : hot(H, x);
+            if (!special && (h & H_HFSPACE)) { x = 0x20; h = hot(H, 0x20); }
+            const int cls = special ? HF_S : (int)((h >> H_CLS_SHIFT) & 3u);
+            const uint64_t KM = w_ballot(keep);
+            const uint64_t pk = KM & lt;
+            const int src = pk ? msb64(pk) : 0;
+            const uint32_t h_l = w_shfl(h, src);
+            const int cls_l = w_shfl(cls, src);
+            const uint32_t hprev = pk ? h_l : carry_h;
+            const int cprev = pk ? cls_l : carry_cls;
+            // HF-NFC quick check -> row fallback
+            const uint64_t RM = w_ballot(keep && (x == V_B || x == V_FB));
+            const bool trig = keep && !special && !(h & H_HFST) && nfc_trig<true>(h, hprev);
+            if (trig) M.fb[rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1] = 1;
+            // pre-tokenizer + ids
+            const bool wordchar = keep && !special && cls != HF_S;
             const uint64_t SM = w_ballot(wordchar && cls != cprev);
             const uint32_t word = carry_word + (uint32_t)w_popc(SM & (lt | (1ull << lane)));  // inclusive
             const uint32_t id = wordchar ? single_id_of(m, sfast, a.single_fast, x) : 0xFFFFu;
             const bool kept = id != 0xFFFFu;
-            const uint64_t KM = w_ballot(kept);
-            const uint64_t pk = KM & lt;
-            const uint32_t kw_l = w_shfl(word, pk ? msb64(pk) : 0);
-            const uint32_t kprev = pk ? kw_l : carry_kword;
+            const uint64_t K2 = w_ballot(kept);
+            const uint64_t pk2 = K2 & lt;
+            const uint32_t kw_l = w_shfl(word, pk2 ? msb64(pk2) : 0);
+            const uint32_t kprev = pk2 ? kw_l : carry_kword;
             const bool kstart = kept && word != kprev;
-            const bool out = kept || (special && x != V_DEAD);
+            const bool out = kept || (keep && special);
             const uint64_t OM = w_ballot(out);
-            const uint64_t KS = w_ballot(kstart);
-            const uint32_t op = wpos + (uint32_t)w_popc(OM & lt);
-            w_sync();  // every lane has read its element before the in-place compaction writes
-            if (out) M.w[op] = special ? x : (uint16_t)(id | (kstart ? WSTART : 0u));
-            if (kstart) M.v[nw + (uint32_t)w_popc(KS & lt)] = (uint16_t)op;
-            wpos += (uint32_t)w_popc(OM);
-            nw += (uint32_t)w_popc(KS);
-            carry_cls = w_bcast(cls, 63);
+            if (out) M.w[wlen + (uint32_t)w_popc(OM & lt)] = special ? x : (uint16_t)(id | (kstart ? WSTART : 0u));
+            wlen += (uint32_t)w_popc(OM);
+            rs += (uint32_t)w_popc(RM);
+            if (KM) {
+                const int lk = msb64(KM);
+                carry_h = w_bcast(h, lk);
+                carry_cls = w_bcast(cls, lk);
+            }
             carry_word = w_bcast(word, 63);
-            if (KM) carry_kword = w_bcast(word, msb64(KM));
+            if (K2) carry_kword = w_bcast(word, msb64(K2));
         }
-        wlen = wpos;
     }
     w_sync();
-    {   // keep only pre-tokens with >= 2 symbols (a single symbol has nothing to merge): with ~4 rows
-        // per tile the rest then fits one 64-lane batch. The kept starts go to the TOP of V
-        // (V[T_E-1-k]) so pass B can use bytes + the bottom of V for its rank rows; the read and
-        // write ranges never meet (singles + 2 * multis <= chars < T_E).
-        uint32_t nk = 0;
-        for (uint32_t base = 0; base < nw; base += 64) {
-            const uint32_t j = base + lane;
-            const uint16_t st = j < nw ? M.v[j] : (uint16_t)0;
-            const bool multi = j < nw && st + 1u < wlen && !(M.w[st + 1] & WSTART);
-            const uint64_t MM = w_ballot(multi);
-            w_sync();
-            if (multi) M.v[T_E - 1 - (nk + (uint32_t)w_popc(MM & lt))] = st;
-            nk += (uint32_t)w_popc(MM);
-        }
-        nw = nk;
+
+    pc.mark(TP_E);
+    // ---------------- pass S: starts of the pre-tokens with >= 2 symbols (a single symbol has
+    // nothing to merge), to the TOP of V (V[T_E-1-k]) so pass B can use bytes + the bottom of V
+    // for its rank rows (at most T_BCAP / 2 such pre-tokens).
+    uint32_t nw = 0;
+    for (uint32_t base = 0; base < wlen; base += 64) {
+        const uint32_t kk = base + lane;
+        const bool multi = kk + 1 < wlen && (M.w[kk] & 0x8000u) && M.w[kk] < V_SPECIAL && !(M.w[kk + 1] & 0x8000u);
+        const uint64_t MM = w_ballot(multi);
+        if (multi) M.v[T_E - 1 - (nw + (uint32_t)w_popc(MM & lt))] = (uint16_t)kk;
+        nw += (uint32_t)w_popc(MM);
     }
     w_sync();
 
@@ -545,13 +500,13 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, cons
         const uint16_t x = in ? M.w[kk] : V_DEAD;
         const bool isrow = in && (x == V_B || x == V_FB);
         const uint64_t RM = w_ballot(isrow);
-        const bool emit = in && x != V_FB && x != V_DEAD;
+        const uint32_t row = rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1;
+        const bool emit = in && x != V_FB && x != V_DEAD && !M.fb[row];
         const uint64_t EM = w_ballot(emit);
         const uint32_t op = pos + (uint32_t)w_popc(EM & lt);
         if (isrow) M.rowop[rs + (uint32_t)w_popc(RM & lt)] = op;
         w_sync();
         if (emit) {
-            const uint32_t row = rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1;
             const uint64_t d = (uint64_t)M.rowslot[row] + (op - M.rowop[row]);
             const uint32_t val = x == V_B ? m.bos : x == V_E ? m.eos : (uint32_t)(x & 0x7FFFu);
             if (d < scap) stage[d] = val;

@@ -135,8 +135,9 @@ void ak_profile_reset(void);
 
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each
  * pass of the tile-cooperative BPE kernel since the last call, while profiling is enabled. Slots:
- * 0 byte staging, 1 decode+NFC+map, 2 elongation, 3 HF NFKC, 4 pre-tokenizer, 5 BPE merges,
- * 6 fallback count, 7 id compaction + counts, 8 fallback emit, 9 loop overhead.
+ * 0 byte staging, 1 decode + NFC check + map/filter, 2 fused elongation + HF NFKC + pre-tokenizer,
+ * 3 (unused), 4 pre-token start list, 5 BPE merges, 6 fallback-list append, 7 ids into row slots +
+ * counts, 8 (unused), 9 loop overhead.
  * Returns the number of slots written (0 if the tile kernel has not run), or a negative error. */
 #define AK_TILE_NPASS 10
 int ak_profile_tile_passes(ak_ws *ws, uint64_t *cycles, int n);
