@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 METRIC = "MB of raw UTF-8 tokenized/sec @1 GPU (+ tokens/s); bit-exact vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SEED = 1234
+TRAFFIC_FILE = "r01_v3_tiles_pmc.json"  # PMC HBM bytes of the tile kernel at the default config
 
 
 def parse():
@@ -148,22 +149,36 @@ def main():
     value = job_bytes * args.steps / elapsed / 1e6
     toks = job_ids * args.steps / elapsed
 
-    # dominant kernel: per-launch algorithmic bytes / its average launch duration
+    # dominant kernel: per-launch algorithmic bytes / its average launch duration (HIP events the
+    # library records around its own launches on the encode stream)
     kern = max(("count", "emit", "tiles"), key=lambda k: prof[k][0])
     k_ms, k_n = prof[kern]
     avg_s = k_ms / max(k_n, 1) / 1e3
-    read_bytes = nbytes + 8 * (rows + 1)
-    # count pass writes a u32 per row; emit / single-pass tiles write ids + row offsets
-    write_bytes = 4 * rows if kern == "count" else 4 * n_ids + 8 * (rows + 1)
+    read_bytes = nbytes + 8 * (rows + 1)  # raw UTF-8 rows + u64 row offsets
+    if kern == "count":
+        write_bytes = 4 * rows  # u32 count per row
+    elif kern == "emit":
+        write_bytes = 4 * n_ids + 8 * (rows + 1)  # u32 ids + u64 row offsets
+    else:
+        write_bytes = 4 * n_ids + 4 * rows  # u32 ids into the row slots + u32 count per row
     algo = read_bytes + write_bytes
     achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
     kname = {"count": "k_rows_fast<OP_BPE,3,false> (count pass)", "emit": "k_rows_fast<OP_BPE,3,true> (emit pass)",
-             "tiles": "k_bpe_tiles<3> (tile-cooperative single pass)"}[kern]
+             "tiles": "k_bpe_tiles<3> (tile-cooperative encode)"}[kern]
+    traffic, traffic_src = None, None
+    tfile = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
+    if kern == "tiles" and os.path.exists(tfile):
+        t = json.load(open(tfile))
+        if t.get("rows") == rows and t.get("bytes") == nbytes:  # the same launch shape, measured by PMC
+            traffic = int(t["hbm_bytes_per_launch"])
+            traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same 10 M-row launch)" % TRAFFIC_FILE
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": kname,
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
                 "kernel_avg_ms": round(avg_s * 1e3, 3), "algorithmic_bytes_per_launch": int(algo),
                 "read_frac": round(read_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0,
                 "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in prof.items() if v[1]}}
+    if traffic_src:
+        roofline["traffic_source"] = traffic_src
     if passes:
         roofline["tile_pass_cycle_frac"] = passes
 
