@@ -47,6 +47,7 @@ SIGNATURES = {
     "ak_profile_read": (I32, [I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
     "ak_profile_reset": (None, []),
     "ak_profile_tile_passes": (I32, [P, ctypes.POINTER(U64), I32]),
+    "ak_ws_fallback_rows": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
     "ak_normalize_cap": (U64, [U64, U64]),
     "ak_segment_cap": (U64, [U64, U64]),
     "ak_bpe_encode_cap": (U64, [U64, U64]),

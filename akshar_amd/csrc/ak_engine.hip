@@ -249,6 +249,19 @@ extern "C" int ak_ws_check(ak_ws *w) {
 namespace ak { int selftest_wave(); }
 extern "C" int ak_selftest(void) { return ak::selftest_wave(); }
 
+extern "C" int ak_ws_fallback_rows(ak_ws *w, uint64_t *rows, uint64_t *pool_rows) {
+    if (!w || !rows || !pool_rows) return fail(AK_ERR_ARG, "ak_ws_fallback_rows: null argument");
+    *rows = 0;
+    *pool_rows = 0;
+    if (!w->tile_misc) return AK_OK;
+    uint32_t h[3] = {0, 0, 0};
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(h, w->tile_misc, sizeof(h), hipMemcpyDeviceToHost));
+    *rows = h[0];
+    *pool_rows = h[2];
+    return AK_OK;
+}
+
 extern "C" int ak_profile_tile_passes(ak_ws *w, uint64_t *cycles, int n) {
     if (!w || !cycles || n < 0) return fail(AK_ERR_ARG, "ak_profile_tile_passes: bad argument");
     memset(cycles, 0, sizeof(uint64_t) * (size_t)n);

@@ -10,8 +10,9 @@
 //   B  lane per pre-token: merge_all (lowest rank, leftmost on ties), in registers up to WREG-1
 //      symbols, in LDS beyond
 //   F  ids (B -> <s>, E -> </s>) into each row's staging slot, per-row token counts
-// Only the common case runs here. A row whose NFC / HF-NFC quick check trips, with invalid UTF-8,
-// or past the tile buffer is appended to a fallback list and encoded by the row kernels of
+// Only the common case runs here (rows past the 1 KB tile buffer start the next sub-tile). A row
+// whose NFC / HF-NFC quick check trips, with invalid UTF-8, or alone over the tile buffer is
+// appended to a fallback list and encoded by the row kernels of
 // ak_k_bpe_tiles.hip (ak_rows.h process_row), which write into the same per-row slot: the tile
 // kernel has no calls, no private arrays and no scratch.
 // Row r's slot is stage[offs[r] + 2 r ...] (its ids never exceed its bytes + 2), so rows and tiles
@@ -232,20 +233,20 @@ __device__ __forceinline__ int bpe_merge_lds(const BpeDev &m, uint16_t *W, int s
 }
 
 template <int FLAGS>
-__device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, const uint16_t *sfast, TileWaveMem &M,
-                         PassClock &pc) {
+__device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *sfast,
+                        TileWaveMem &M, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const uint64_t lt = w_lanemask_lt();
     const RowArgs &a = ta.ra;
     const BpeDev &m = a.bpe;
-    const uint64_t r0 = t * (uint64_t)ta.rows;
-    const uint64_t r1 = r0 + (uint64_t)ta.rows < a.n ? r0 + (uint64_t)ta.rows : a.n;
-    const int nr = (int)(r1 - r0);
-    const uint64_t myoff = lane <= nr ? a.offs[r0 + lane] : 0ull;
+    const int nr0 = (int)(rend - r0);
+    const uint64_t myoff = lane <= nr0 ? a.offs[r0 + lane] : 0ull;
     const uint64_t S0 = w_bcast(myoff, 0);
-    const bool fits = lane >= 1 && lane <= nr && (myoff - S0) <= (uint64_t)T_BCAP;
-    const int k = w_popc(w_ballot(fits));  // rows 0..k-1 are staged; the rest fall back
+    const bool fits = lane >= 1 && lane <= nr0 && (myoff - S0) <= (uint64_t)T_BCAP;
+    const int k = w_popc(w_ballot(fits));  // rows 0..k-1 fit the tile buffer
+    // rows past the buffer are the caller's next sub-tile; a single row over T_BCAP bytes falls back
+    const int nr = k ? k : 1;
     const uint64_t S1 = w_bcast(myoff, k);
     const uint64_t a0 = S0 & ~15ull;
     {
@@ -524,6 +525,7 @@ __device__ void bpe_tile(const TileArgs &ta, uint64_t t, const uint32_t *H, cons
     }
     w_sync();
     pc.mark(TP_F);
+    return nr;
 }
 
 template <int FLAGS>
@@ -533,7 +535,9 @@ __device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
     pc.init(ta.passprof != nullptr);
     for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {  // static stride: tiles are near-equal
         pc.mark(TP_LOOP);
-        bpe_tile<FLAGS>(ta, t, H, sfast, M, pc);
+        const uint64_t r0 = t * (uint64_t)ta.rows;
+        const uint64_t r1 = r0 + (uint64_t)ta.rows < ta.ra.n ? r0 + (uint64_t)ta.rows : ta.ra.n;
+        for (uint64_t r = r0; r < r1;) r += (uint64_t)bpe_tile<FLAGS>(ta, r, r1, H, sfast, M, pc);
     }
     pc.flush(ta.passprof);
 }

@@ -276,3 +276,11 @@ def profile_tile_passes(dev=None):
         check(k, "ak_profile_tile_passes")
     tot = float(sum(buf)) or 1.0
     return {name: round(buf[i] / tot, 4) for i, name in enumerate(_lib.AK_TILE_PASSES)} if k else {}
+
+
+def fallback_rows(dev=None):
+    """(rows, pool rows) of the last tile-path BPE encode that took the sequential fallback kernels."""
+    ws = workspace(dev)
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    check(_lib.lib().ak_ws_fallback_rows(ws, ctypes.byref(a), ctypes.byref(b)), "ak_ws_fallback_rows")
+    return a.value, b.value

@@ -124,6 +124,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = engine.profile_read()
     passes = engine.profile_tile_passes(local)
+    fb_rows = engine.fallback_rows(local)
     engine.profile_enable(False)
 
     gather_ms = None
@@ -181,6 +182,7 @@ def main():
         roofline["traffic_source"] = traffic_src
     if passes:
         roofline["tile_pass_cycle_frac"] = passes
+        roofline["fallback_rows_per_step"] = fb_rows[0]
 
     cpu = None
     if rank == 0 and not args.no_cpu:

@@ -133,6 +133,11 @@ int ak_profile_enable(int on);
 int ak_profile_read(int kernel, double *total_ms, uint64_t *launches);
 void ak_profile_reset(void);
 
+/* Rows of the last tile-path ak_bpe_encode on this workspace that took the sequential fallback
+ * kernels (NFC / HF-NFC quick check tripped, invalid UTF-8, or past the 1 KB tile buffer), and how
+ * many of those needed the large pool buffers. Synchronizes the device. */
+int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
+
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each
  * pass of the tile-cooperative BPE kernel since the last call, while profiling is enabled. Slots:
  * 0 byte staging, 1 decode + NFC check + map/filter, 2 fused elongation + HF NFKC + pre-tokenizer,
