@@ -44,6 +44,7 @@ struct TileWaveMem {
     uint16_t v[T_E];
     uint16_t w[T_E + 16];        // +16: pass B reads WREG-symbol windows past a pre-token start
     uint8_t fb[T_MAXR];          // row goes to the fallback kernels
+    uint16_t rowend[T_MAXR];     // row's end in the staged bytes
     uint32_t rowslot[T_MAXR];    // row's staging slot, relative to the tile's (S0 + 2 r0)
     uint32_t rowop[T_MAXR + 1];  // row's first position in the tile's id stream
 };
@@ -255,56 +256,90 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         uint4 *dst = (uint4 *)M.bytes;
         for (uint64_t b = (uint64_t)lane; b < nblk; b += 64) dst[b] = src[b];
     }
+    const uint64_t nextoff = w_shfl(myoff, lane + 1);
     if (lane < nr) {
         M.fb[lane] = lane >= k ? 1 : 0;
+        M.rowend[lane] = (uint16_t)(nextoff - a0);
         M.rowslot[lane] = (uint32_t)(myoff - S0) + 2u * (uint32_t)lane;
     }
     w_sync();
 
     pc.mark(TP_STAGE);
-    // ---------------- pass D: decode + normalize_text map/filter -> V. If no char of the row
-    // trips nfc_trig, NFC is the identity on the row and every char maps on its own: one
-    // ballot-compacted write per lane. A row that trips (or has invalid UTF-8) falls back.
-    uint32_t vpos = 0;
+    // ---------------- pass D1: per row, 64 bytes per step: the positions of the UTF-8 lead bytes ->
+    // P (in W, free until pass N), each row opened by a mark entry. A row that starts with a
+    // continuation byte is invalid UTF-8: fallback (stray continuation bytes inside a row are caught
+    // in D2: the chars' lengths must tile the row).
+    uint16_t *P = M.w;
+    uint32_t np = 0;
     for (int i = 0; i < k; ++i) {
         const int s = (int)(w_bcast(myoff, i) - a0), e = (int)(w_bcast(myoff, i + 1) - a0);
-        const uint32_t vstart = vpos;
-        if (lane == 0) M.v[vpos] = V_B;
-        ++vpos;
-        bool fallback = false;
-        uint32_t carry_h = H_ROWSTART;  // hot word of the last char of the previous chunk
+        if (lane == 0) P[np] = 0x8000u;
+        ++np;
+        bool bad_row = false;
         for (int base = s; base < e; base += 64) {
             const int p = base + lane;
             const bool in = p < e;
-            const uint32_t x = in ? lds_word(M.bytes, p) : 0u;
-            const bool lead = in && (x & 0xC0u) != 0x80u;
-            bool bad = in && p == s && !lead;
-            uint32_t h = 0;
-            if (lead) {
-                const uint32_t cp = decode_word(x, p, e);
-                if (cp == 0xFFFFFFFFu) bad = true;
+            const uint32_t b = in ? M.bytes[p] : 0u;
+            const bool lead = in && (b & 0xC0u) != 0x80u;
+            if (w_ballot(in && !lead && p == s)) { bad_row = true; break; }
+            const uint64_t LM = w_ballot(lead);
+            if (lead) P[np + (uint32_t)w_popc(LM & lt)] = (uint16_t)p;
+            np += (uint32_t)w_popc(LM);
+        }
+        if (bad_row && lane == 0) M.fb[i] = 1;
+    }
+    w_sync();
+
+    // ---------------- pass D2: the whole tile's chars, 64 per step: decode (branch-free, dword
+    // window), hot word, nfc_trig against the previous char (a mark = row start), then the
+    // normalize_text map (lower / allowlist) -> V with <s>/</s> sentinels around each row. If no
+    // char of a row trips nfc_trig, NFC is the identity on it; a row that trips is marked for the
+    // fallback kernels (pass F skips it).
+    uint32_t vpos = 0;
+    {
+        uint32_t carry_h = H_ROWSTART, rows = 0;
+        for (uint32_t c0 = 0; c0 < np; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            const bool in = c < np;
+            const uint32_t ent = in ? P[c] : 0x8000u;
+            const bool mark = in && (ent & 0x8000u);
+            const uint64_t RMK = w_ballot(mark);
+            const int row = (int)(rows + (uint32_t)w_popc(RMK & (lt | (1ull << lane)))) - 1;
+            const bool chr = in && !mark;
+            uint32_t h = H_ROWSTART;
+            bool bad = false;
+            if (chr) {
+                const int pos = (int)(ent & 0x7FFFu);
+                const int rend = (int)M.rowend[row];
+                const uint32_t cp = decode_word(lds_word(M.bytes, pos), pos, rend);
+                // the next lead (or the row end) must sit right after this char: else stray bytes
+                const uint32_t nent = c + 1 < np ? P[c + 1] : 0x8000u;
+                const int nxt = (nent & 0x8000u) ? rend : (int)nent;
+                if (cp == 0xFFFFFFFFu || pos + utf8_len(cp) != nxt) { bad = true; h = 0; }
                 else h = hot(H, cp);
             }
-            const uint64_t LEADS = w_ballot(lead);
-            const uint64_t pm = LEADS & lt;
-            const uint32_t hprev_l = w_shfl(h, pm ? msb64(pm) : 0);
-            const uint32_t hprev = pm ? hprev_l : carry_h;
-            const bool trig = bad || (lead && !(h & H_STABLE) && nfc_trig<false>(h, hprev));
-            if (w_ballot(trig)) { fallback = true; break; }
-            if (LEADS) carry_h = w_bcast(h, msb64(LEADS));
-            const uint32_t mv = h & 0xFFFFu;
-            const uint64_t KM = w_ballot(mv != 0u);
-            if (mv) M.v[vpos + (uint32_t)w_popc(KM & lt)] = (uint16_t)mv;
-            vpos += (uint32_t)w_popc(KM);
+            const uint32_t hl = w_shfl(h, lane ? lane - 1 : 0);
+            const uint32_t hprev = lane ? hl : carry_h;
+            const bool trig = chr && (bad || (!(h & H_STABLE) && nfc_trig<false>(h, hprev)));
+            if (trig) M.fb[row] = 1;
+            const uint32_t mv = chr ? (h & 0xFFFFu) : 0u;
+            const uint32_t cnt = mark ? (row > 0 ? 2u : 1u) : (mv ? 1u : 0u);
+            uint32_t tot;
+            const uint32_t ex = w_exscan(cnt, &tot);
+            if (mark) {
+                if (row > 0) { M.v[vpos + ex] = V_E; M.v[vpos + ex + 1] = V_B; }
+                else M.v[vpos + ex] = V_B;
+            } else if (mv) {
+                M.v[vpos + ex] = (uint16_t)mv;
+            }
+            vpos += tot;
+            rows += (uint32_t)w_popc(RMK);
+            carry_h = w_bcast(h, 63);
         }
-        if (fallback) {
-            vpos = vstart;
-            if (lane == 0) { M.v[vpos] = V_FB; M.fb[i] = 1; }
-        } else if (lane == 0) {
-            M.v[vpos] = V_E;
+        if (k > 0) {
+            if (lane == 0) M.v[vpos] = V_E;
+            ++vpos;
         }
-        ++vpos;
-        w_sync();
     }
     const uint32_t vlen = vpos;
     w_sync();

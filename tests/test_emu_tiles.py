@@ -36,13 +36,14 @@ def test_fallback_rows_match_oracle(em, bpe_model, rows):
              "ज्ञ" * 100 + " " + "hello " * 100, "ऩ" + "़" * 40 + "्" * 40, "Ḱ" + "̣" * 20, "", "ok",
              "न€़ ে€া", "क" + "॑" * 20 + "़", "ড়" * 3, "aaj मौसम", "x" * 2047, "y" * 2048, "z" * 2049]
     raw = [t.encode("utf-8") for t in texts]
-    raw += [b"\xff\xfeabc", b"ok \xe0\xa4", b"\xc3(", b"\xed\xa0\x80 x", b"\x80lead", b"mid\xf4\x90\x80\x80end"]
+    raw += [b"\xff\xfeabc", b"ok \xe0\xa4", b"\xc3(", b"\xed\xa0\x80 x", b"\x80lead", b"mid\xf4\x90\x80\x80end",
+            b"a\x80b", b"\xc3\xa9\xa9 ok", b"\xe0\xa4\x95\x80\xe0\xa4\x96", "न".encode() + b"\x80" + "़".encode()]
     buf, offs = _raw_rows(raw)
     ids, oo, st = emu.bpe_tiles(em, buf, offs, rows=rows)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
     assert rows_ints(ids, oo) == rows_ints(ref, ro)
     # invalid UTF-8 flagged; the surrogate form ED A0 80 decodes (as the oracle, cf. surrogatepass)
-    assert st[len(texts):].tolist() == [1, 1, 1, 0, 1, 1]
+    assert st[len(texts):].tolist() == [1, 1, 1, 0, 1, 1, 1, 1, 1, 1]
 
 
 @pytest.mark.parametrize("kind", [0, 1, 2])
