@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--gather", action="store_true", help="also all-gather the id streams (RCCL)")
     ap.add_argument("--cpu-rows", type=int, default=400_000, help="CPU baseline sample (rows)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-others", action="store_true", help="skip the config 2/3/5 side measurements")
     return ap.parse_args()
 
 
@@ -71,6 +72,44 @@ def cpu_baseline(args, buf, offs):
             "tokens_per_s": round(len(ids) / dt, 1),
             "sample": "first %d rows (%.1f MB) of the same synthetic Hinglish batch, oracle/akshar_oracle.c "
                       "or_bpe_encode single-threaded, %.1f s" % (n, len(sub) / 1e6, dt)}
+
+
+def other_configs(dev, rows=1_000_000):
+    """SURVEY.md §8 configs 2, 3 and 5 on this GPU (1 M synthetic rows each, inputs in HBM): the
+    single-GPU rates of the other rows of the scope table, reported beside the headline line."""
+    from akshar_amd import engine, synth
+
+    def timed(fn, reps=3):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / reps
+
+    out = {}
+    spm = engine.SPM(os.path.join(ROOT, "models", "akshar.model"), dev=dev)
+    for kind, name in ((synth.KIND_DEVANAGARI, "devanagari"), (synth.KIND_HINGLISH, "hinglish")):
+        buf, offs = synth.generate(kind, rows, seed=SEED + 7)
+        pad = np.zeros(((len(buf) + 15) // 16) * 16 + 16, dtype=np.uint8)
+        pad[:len(buf)] = buf
+        gb, go = engine.to_device(pad, offs.astype(np.int64), dev=dev)
+        mb = len(buf) / 1e6
+        ops = {"segment": lambda: engine.segment_batch(gb, go, flags=3),
+               "segment_raw": lambda: engine.segment_batch(gb, go, flags=engine.AK_RAW),
+               "normalize": lambda: engine.normalize_batch(gb, go),
+               "switches": lambda: engine.switches_batch(gb, go),
+               "spm_encode": lambda: spm.encode_batch(gb, go)}
+        res = {k: round(mb / timed(f), 1) for k, f in ops.items()}
+        res["rows"], res["mb"] = rows, round(mb, 1)
+        out[name] = res
+    d, h = out["devanagari"], out["hinglish"]
+    t3 = sum(1.0 / h[k] for k in ("normalize", "switches", "segment"))
+    return {"unit": "MB/s of raw UTF-8 (1 M synthetic rows, inputs in HBM, v1 row kernels)",
+            "cfg2_segment_devanagari": d["segment"], "cfg2_segment_devanagari_raw": d["segment_raw"],
+            "cfg3_normalize_switches_segment_hinglish": round(1.0 / t3, 1),
+            "cfg5_spm_encode_hinglish_per_gpu": h["spm_encode"], "detail": out}
 
 
 def main():
@@ -184,6 +223,11 @@ def main():
         roofline["tile_pass_cycle_frac"] = passes
         roofline["fallback_rows_per_step"] = fb_rows[0]
 
+    others = None
+    if rank == 0 and not args.no_others:
+        log(rank, "other configs")
+        others = other_configs(local)
+
     cpu = None
     if rank == 0 and not args.no_cpu:
         log(rank, "timed region done (%.1f ms/step); CPU baseline" % (elapsed / args.steps * 1e3))
@@ -201,6 +245,8 @@ def main():
                        "parallelism": "dp%d (row shards, no data-path collective)" % world},
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if others:
+            line["other_configs"] = others
         if gather_ms is not None:
             line["gather_ms"] = round(gather_ms, 3)
         print(json.dumps(line), flush=True)

@@ -3,6 +3,7 @@
 // A debugging and CPU-test aid for the device pipeline code; never loaded by the product.
 #define AK_HOST_EMU 1
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -145,6 +146,9 @@ thread_local int t_lane;
 thread_local EmuWave *t_wave;
 }  // namespace ak
 
+static uint32_t g_last_fb = 0;
+extern "C" uint32_t emu_last_fallback_rows() { return g_last_fb; }
+
 extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
                                  uint32_t *out, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, int rows) {
     EmuModel *m = (EmuModel *)model;
@@ -177,6 +181,8 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     for (auto &x : th) x.join();
     delete M;
     if (err) return -1;
+    g_last_fb = fbn;
+    if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
     // fallback rows as k_tile_fb / k_tile_fb_slow: the row pipeline straight into the row's slot
     std::vector<uint32_t> seg(2 * SLOW_SEG), dec(8 * SLOW_SEG), wpair(SLOW_WORD);
     std::vector<uint16_t> wsym(SLOW_WORD);

@@ -28,6 +28,7 @@ def lib():
         L.emu_free.argtypes = [P]
         L.emu_bpe_tiles.restype = ctypes.c_int64
         L.emu_bpe_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
+        L.emu_last_fallback_rows.restype = ctypes.c_uint32
         L.emu_run.restype = ctypes.c_int64
         L.emu_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_uint64, P, P,
                               ctypes.c_uint64, P]
@@ -90,3 +91,7 @@ def bpe_tiles(model, buf, offs, flags=3, rows=8):
                               oo.ctypes.data, st.ctypes.data, rows)
     assert 0 <= tot <= cap, tot
     return out[:tot], oo, st[:n]
+
+
+def last_fallback_rows():
+    return int(lib().emu_last_fallback_rows())

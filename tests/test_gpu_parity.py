@@ -144,3 +144,34 @@ def test_large_batch_property(eng, bpe_model):
     assert oo[-1] == len(ref) == ids.numel()
     assert np.array_equal(oo, ro)
     assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
+
+
+def test_wave_primitives_selftest(eng):
+    """DPP prefix scan, readlane broadcast and ballot behave as the tile kernels assume."""
+    from akshar_amd import _lib
+    assert _lib.lib().ak_selftest() == 0, _lib.lib().ak_last_error().decode()
+
+
+def test_tile_path_fallback_accounting(eng, bpe_model):
+    """Hinglish rows take the cooperative path (no fallback); rows that need real NFC, carry invalid
+    UTF-8 or exceed the tile buffer are counted as fallback rows and still match the oracle."""
+    buf, offs = _synth(1, 50000, 77)
+    gb, go = _to_dev(eng, buf, offs)
+    bpe = eng.BPE(bpe_model)
+    bpe.encode_batch(gb, go)
+    assert eng.fallback_rows()[0] == 0
+    texts = ["\u0928\u0939\u0940\u0902", "\u0928\u093c\u093e", "caf\u00e9", "x" * 1500, "aaj", "\u0929\u094d"]
+    raw = [t.encode() for t in texts] + [b"a\x80b"]
+    offs2 = np.zeros(len(raw) + 1, dtype=np.int64)
+    np.cumsum([len(r) for r in raw], out=offs2[1:])
+    b2 = np.frombuffer(b"".join(raw), dtype=np.uint8).copy()
+    gb2, go2 = _to_dev(eng, b2, offs2)
+    st = torch.zeros(len(raw), dtype=torch.uint8, device=gb2.device)
+    ids, oo = bpe.encode_batch(gb2, go2, row_status=st)
+    fb, _ = eng.fallback_rows()
+    # न + nukta composes under NFC; 1,500 B exceed the tile buffer; a stray continuation byte. café
+    # (precomposed, nothing follows) and precomposed ऩ + virama (canonical already) stay cooperative.
+    assert fb == 3
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(b2, offs2.astype(np.uint64))
+    assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
+    assert _cpu(st).tolist()[-1] == 1
