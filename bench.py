@@ -121,8 +121,13 @@ def main():
         rank = int(os.environ["RANK"])
         world = int(os.environ["WORLD_SIZE"])
         local = int(os.environ.get("LOCAL_RANK", rank))
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("AK_BENCH_BACKEND", "nccl")  # gloo: rehearse N ranks on one GPU
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(torch.cuda.device_count(), 1)
+            tdist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -176,10 +181,11 @@ def main():
         gather_ms = (time.perf_counter() - tg) * 1e3
 
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if tdist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([nbytes, n_ids], dtype=torch.float64, device=dev)
+        tot = torch.tensor([nbytes, n_ids], dtype=torch.float64, device=rdev)
         tdist.all_reduce(tot)
         job_bytes, job_ids = float(tot[0]), float(tot[1])
     else:
