@@ -1,0 +1,58 @@
+"""Summarise a tools/profile_round.sh output directory into profiles/<tag>_*.
+
+  python tools/pmc_summary.py gpurun_out/v4/prof r01_v4
+
+writes profiles/<tag>_bench_kernel_stats.csv (the rocprofv3 --stats summary of the bench run),
+profiles/<tag>_bench.json (the bench line of that run) and profiles/<tag>_tiles_pmc.json (the PMC
+passes over one cfg4-size tile-kernel launch, HBM bytes corrected as MI355X_MICROARCH.md says:
+FETCH_SIZE is in KiB and counts half of the 16-B/lane streaming reads on gfx950 -> x1024 x2,
+WRITE_SIZE in KiB -> x1024).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counters(path, match="bpe_tiles"):
+    agg, meta = collections.defaultdict(float), {}
+    for r in csv.DictReader(open(path)):
+        if match in r["Kernel_Name"]:
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            meta = {"vgpr": int(r.get("Arch_VGPR_Count") or r.get("VGPR_Count") or 0),
+                    "lds_block": int(r.get("LDS_Block_Size") or r.get("Lds_Size") or 0),
+                    "scratch": int(r.get("Scratch_Size") or 0)}
+    return dict(agg), meta
+
+
+def main(src, tag):
+    out = os.path.join(ROOT, "profiles")
+    shutil.copy(os.path.join(src, "bench", "bench_kernel_stats.csv"), os.path.join(out, tag + "_bench_kernel_stats.csv"))
+    line = [ln for ln in open(os.path.join(src, "bench_stdout.log")) if ln.startswith("{")][-1]
+    open(os.path.join(out, tag + "_bench.json"), "w").write(line)
+    allc, meta = {}, {}
+    for name in ("fetch", "write", "sq1", "sq2"):
+        p = os.path.join(src, name, name + "_counter_collection.csv")
+        if os.path.exists(p):
+            c, m = counters(p)
+            allc.update(c)
+            meta = meta or m
+    rd = allc["FETCH_SIZE"] * 1024 * 2
+    wr = allc["WRITE_SIZE"] * 1024
+    rec = {"kernel": "k_bpe_tiles<3>",
+           "command": "rocprofv3 --pmc <counters> -- python3 tools/prof_op.py bpe 10000000 1 1 (one cfg4-size launch, "
+                      "10 M synthetic Hinglish rows); separate passes per counter group (tools/profile_round.sh)",
+           "rows": 10000000, "counters": allc, **meta,
+           "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+           "note": "read = FETCH_SIZE x 1024 x 2 (gfx950 half-count correction for 16-B/lane streaming reads), "
+                   "write = WRITE_SIZE x 1024"}
+    json.dump(rec, open(os.path.join(out, tag + "_tiles_pmc.json"), "w"), indent=1)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
