@@ -478,6 +478,7 @@ struct SwitchSink {
 
 struct BpeDev {
     const uint64_t *merge_tab;  // two-choice cuckoo: lo32 = left << 16 | right, hi32 = rank << 16 | new
+    const uint32_t *merge_ctab; // the same slots, 4-byte entries (ak_model_build.h build_bpe; tile path)
     uint32_t tab_mask;
     uint32_t tab_shift;
     const uint32_t *single_sorted_cp;  // for code points >= FAST_N
@@ -495,6 +496,21 @@ __device__ __forceinline__ uint32_t merge_lookup(const BpeDev &m, uint32_t a, ui
     const uint64_t e1 = m.merge_tab[h1];
     const uint64_t e2 = m.merge_tab[h2];
     return (uint32_t)e1 == key ? (uint32_t)(e1 >> 32) : (uint32_t)e2 == key ? (uint32_t)(e2 >> 32) : 0xFFFFFFFFu;
+}
+
+// the same lookup on the compact table: the new id (= rank order for tile_ok models), 0xFFFF if none.
+// One 4-byte load per candidate slot: half the registers in flight and half the L2 footprint.
+__device__ __forceinline__ uint32_t merge_lookup_c(const BpeDev &m, uint32_t a, uint32_t b) {
+    const uint32_t key = (a << 16) | b;
+    const uint32_t p1 = key * 0x9E3779B1u, p2 = (key ^ 0x5BD1E995u) * 0x85EBCA77u;
+    const uint32_t lowmask = (1u << m.tab_shift) - 1u;
+    // 32-bit byte offsets (the table is < 4 GB): saddr + voffset loads, one VGPR per address
+    const char *base = (const char *)m.merge_ctab;
+    const uint32_t e1 = *(const uint32_t *)(base + ((p1 >> m.tab_shift) << 2));
+    const uint32_t e2 = *(const uint32_t *)(base + ((p2 >> m.tab_shift) << 2));
+    const uint32_t t1 = (p1 & lowmask) << 16, t2 = ((p2 & lowmask) << 16) | 0x8000u;
+    const uint32_t v = (e1 ^ t1) < 0x8000u ? (e1 & 0x7FFFu) : (e2 ^ t2) < 0x8000u ? (e2 & 0x7FFFu) : 0x7FFFu;
+    return v == 0x7FFFu ? 0xFFFFu : v;
 }
 
 __device__ __forceinline__ int bpe_merge_word(const BpeDev &m, uint16_t *w, uint32_t *pr, int n) {

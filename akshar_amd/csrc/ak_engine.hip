@@ -111,6 +111,7 @@ extern "C" int ak_version(void) { return 1; }
 struct ak_bpe {
     BpeDev dev;
     uint64_t *d_tab = nullptr;
+    uint32_t *d_ctab = nullptr;
     uint16_t *d_single_fast = nullptr;  // FAST_N entries
     uint32_t *d_single_cp = nullptr;
     uint16_t *d_single_id = nullptr;
@@ -144,6 +145,8 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     ak_bpe *m = new ak_bpe();
     HIP_TRY(hipMalloc(&m->d_tab, t.tab.size() * sizeof(uint64_t)));
     HIP_TRY(hipMemcpy(m->d_tab, t.tab.data(), t.tab.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_ctab, t.ctab.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(m->d_ctab, t.ctab.data(), t.ctab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&m->d_single_fast, FAST_N * sizeof(uint16_t)));
     HIP_TRY(hipMemcpy(m->d_single_fast, t.fast.data(), FAST_N * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&m->d_single_cp, t.rest_cp.size() * sizeof(uint32_t)));
@@ -151,6 +154,7 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     HIP_TRY(hipMalloc(&m->d_single_id, t.rest_id.size() * sizeof(uint16_t)));
     HIP_TRY(hipMemcpy(m->d_single_id, t.rest_id.data(), t.rest_id.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     m->dev.merge_tab = m->d_tab;
+    m->dev.merge_ctab = m->d_ctab;
     m->dev.tab_mask = t.mask;
     m->dev.tab_shift = t.shift;
     m->dev.single_sorted_cp = m->d_single_cp;
@@ -166,6 +170,7 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
 extern "C" void ak_bpe_free(ak_bpe *m) {
     if (!m) return;
     (void)hipFree(m->d_tab);
+    (void)hipFree(m->d_ctab);
     (void)hipFree(m->d_single_fast);
     (void)hipFree(m->d_single_cp);
     (void)hipFree(m->d_single_id);

@@ -7,6 +7,7 @@
 //   scan_counts      per-row counts -> u64 row offsets (out_offs)
 //   k_tile_copy      staged ids -> ids[out_offs[r] ...]
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "ak_internal.h"
 #include "ak_tile.h"
@@ -15,15 +16,15 @@ namespace ak {
 
 static_assert(T_NPASS == AK_TILE_NPASS, "pass slots: ak_tile.h vs include/akshar.h");
 
-constexpr int TILE_BLOCK = 256;  // 4 waves share the staged property tables
+constexpr int TILE_BLOCK = 512;  // 8 waves share the staged property tables; 4 blocks (8 waves/SIMD) per CU
 constexpr int FB_BLOCK = 256;
 
 template <int FLAGS>
-__global__ __launch_bounds__(TILE_BLOCK, 4) void k_bpe_tiles(TileArgs ta) {
-    __shared__ uint32_t hot_tab[FAST_N];
+__global__ __launch_bounds__(TILE_BLOCK, 8) void k_bpe_tiles(TileArgs ta) {
+    __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t sfast[SFAST_N];
     __shared__ TileWaveMem wm[TILE_BLOCK / 64];
-    for (uint32_t i = threadIdx.x; i < FAST_N; i += TILE_BLOCK) hot_tab[i] = hot_of(prop_global(i));
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += TILE_BLOCK) hot_tab[i] = hot_of(prop_global(hot_cp(i)));
     for (uint32_t i = threadIdx.x; i < SFAST_N; i += TILE_BLOCK)
         sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     __syncthreads();
@@ -224,8 +225,11 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
     HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
+    // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit
+    int bpc = g_tile_blocks_per_cu;
+    if (const char *e = getenv("AK_TILE_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + waves_per_block - 1) / waves_per_block,
-                                                       (uint64_t)num_cus() * (uint64_t)g_tile_blocks_per_cu);
+                                                       (uint64_t)num_cus() * (uint64_t)bpc);
     AK_PROF(AK_PROF_TILES, false, st);
     k_bpe_tiles<3><<<grid, TILE_BLOCK, 0, st>>>(ta);
     AK_PROF(AK_PROF_TILES, true, st);

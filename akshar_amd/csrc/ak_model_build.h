@@ -23,6 +23,7 @@ inline uint32_t cuckoo_h2(uint32_t key, uint32_t shift) { return ((key ^ 0x5BD1E
 
 struct BpeTables {
     std::vector<uint64_t> tab;
+    std::vector<uint32_t> ctab;  // the same slots, 4-byte entries (tile path; see build_compact)
     uint32_t mask = 0;
     uint32_t shift = 0;  // slot = (key * 0x9E3779B1) >> shift: the product's HIGH bits
     std::vector<uint16_t> fast;     // FAST_N entries, 0xFFFF = not in vocab
@@ -41,7 +42,7 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
         if (merges[i] >= 0xFFFFu) return "vocab id >= 65535";
     // two-choice cuckoo table: a key lives in slot h1(key) or h2(key), so a device lookup is two
     // independent 8-byte loads and no probe loop (ak_dev.h merge_lookup)
-    uint32_t size = 1024;
+    uint32_t size = 1u << 16;  // >= 2^16 slots: the compact entries keep 32 - 16 product bits
     while (size < 2u * n_merges + 16u) size <<= 1;
     for (;;) {
         t.tab.assign(size, 0xFFFFFFFFull);
@@ -67,6 +68,21 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
         if (ok) break;
         size <<= 1;  // a cycle: grow and rebuild (never needed at load <= 0.5 in practice)
         if (size > (1u << 24)) return "cuckoo table build failed";
+    }
+    // compact entries for the tile path: slot = product >> shift, so (slot, product's low `shift`
+    // bits, which hash) identifies the key exactly (both products are bijections of the key):
+    // entry = low bits << 16 | which << 15 | new id (< 0x7FFC); 0x00007FFF = empty (reads as "no
+    // merge" whatever it matches). The tile path compares new ids as ranks (monotone, checked at load).
+    t.ctab.assign(size, 0x00007FFFu);
+    for (uint32_t h = 0; h < size; ++h) {
+        const uint32_t key = (uint32_t)t.tab[h];
+        if (key == 0xFFFFFFFFu) continue;
+        const uint32_t nw = (uint32_t)(t.tab[h] >> 32) & 0xFFFFu;
+        if (nw >= 0x7FFFu) continue;  // such a model is not tile_ok: the entry is never read
+        const bool first = cuckoo_h1(key, t.shift) == h;
+        const uint32_t prod = first ? key * 0x9E3779B1u : (key ^ 0x5BD1E995u) * 0x85EBCA77u;
+        const uint32_t low = prod & ((1u << t.shift) - 1u);
+        t.ctab[h] = (low << 16) | (first ? 0u : 0x8000u) | nw;
     }
     t.fast.assign(FAST_N, 0xFFFFu);
     std::vector<std::pair<uint32_t, uint16_t>> rest;

@@ -27,7 +27,7 @@
 
 namespace ak {
 
-constexpr int T_BCAP = 1024;  // staged bytes per tile (rows past it fall back)
+constexpr int T_BCAP = 768;   // staged bytes per tile (rows past it start the next sub-tile)
 constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
 constexpr int T_E = T_BCAP + 2 * T_MAXR + 64;
 
@@ -38,6 +38,10 @@ constexpr uint16_t V_E = 0xFFFF;
 constexpr uint16_t V_SPECIAL = 0xFFFC;  // values >= this are sentinels / dead
 constexpr uint16_t WSTART = 0x8000;     // first symbol of a pre-token (ids are < 0x7FFC: checked at load)
 constexpr int WREG = 16;                // pre-tokens up to WREG-1 symbols take the rank-row merge loop
+// pre-tokens of >= 2 symbols one tile may hold for pass B (their starts share V with the rank rows);
+// a tile with more (never in text: 240 two-symbol pre-tokens in 768 bytes) sends its rows to the
+// fallback kernels
+constexpr int T_SCAP = 240;
 
 struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
@@ -47,6 +51,7 @@ struct TileWaveMem {
     uint16_t rowend[T_MAXR];     // row's end in the staged bytes
     uint32_t rowslot[T_MAXR];    // row's staging slot, relative to the tile's (S0 + 2 r0)
     uint32_t rowop[T_MAXR + 1];  // row's first position in the tile's id stream
+    uint64_t passacc[10];        // PassClock accumulators (ak_profile_tile_passes)
 };
 
 struct TileArgs {
@@ -64,20 +69,23 @@ struct TileArgs {
 
 // pass profile slots (ak_profile_tile_passes)
 enum { TP_STAGE, TP_D, TP_E, TP_H, TP_P, TP_B, TP_FBC, TP_F, TP_FBE, TP_LOOP, T_NPASS };
+static_assert(T_NPASS == sizeof(TileWaveMem::passacc) / 8, "TileWaveMem::passacc");
 
-struct PassClock {  // wave-uniform; lane 0 flushes once per wave
-    uint64_t acc[T_NPASS];
+struct PassClock {  // wave-uniform; the accumulators live in the wave's LDS (no registers held)
+    uint64_t *acc;     // T_NPASS entries (TileWaveMem::passacc)
     uint64_t last;
     bool on;
-    __device__ __forceinline__ void init(bool enabled) {
+    __device__ __forceinline__ void init(bool enabled, uint64_t *lds_acc) {
         on = enabled;
-        for (int i = 0; i < T_NPASS; ++i) acc[i] = 0;
+        acc = lds_acc;
+        if (on && w_lane() == 0)
+            for (int i = 0; i < T_NPASS; ++i) acc[i] = 0;
         last = on ? clock64() : 0;
     }
     __device__ __forceinline__ void mark(int k) {
         if (!on) return;
         const uint64_t now = clock64();
-        acc[k] += now - last;
+        if (w_lane() == 0) acc[k] += now - last;
         last = now;
     }
     __device__ __forceinline__ void flush(uint64_t *dst) {
@@ -123,8 +131,15 @@ __device__ __forceinline__ uint32_t hot_of(uint2 pr) {
            ((p_ccc_hf(pr) == 0 && !p_second(pr)) ? H_HFST : 0u) | (p_ccc_hf(pr) == 0 ? H_HC0 : 0u) |
            (p_hfspace(pr) ? H_HFSPACE : 0u) | ((uint32_t)p_hfclass(pr) << H_CLS_SHIFT) | (ccc_code(cc) << H_CCC_SHIFT);
 }
+// LDS holds the hot words of U+0000..U+017F and U+0900..U+09FF (HOT_N entries, 2.5 KB, so that 8
+// waves per SIMD fit); any other code point builds its word from the global property trie
+constexpr uint32_t HOT_LO = 0x180;
+constexpr uint32_t HOT_N = HOT_LO + 0x100;
+__device__ __forceinline__ uint32_t hot_cp(uint32_t i) { return i < HOT_LO ? i : i - HOT_LO + 0x900u; }
 __device__ __forceinline__ uint32_t hot(const uint32_t *H, uint32_t cp) {
-    return cp < FAST_N ? H[cp] : hot_of(prop_global(cp));
+    if (cp < HOT_LO) return H[cp];
+    if (cp - 0x900u < 0x100u) return H[cp - 0x900u + HOT_LO];
+    return hot_of(prop_global(cp));
 }
 
 // Exact-or-conservative test that NFC leaves the segment around mark m unchanged, given the char
@@ -211,14 +226,14 @@ __device__ __forceinline__ uint32_t single_id_of(const BpeDev &m, const uint16_t
 // up in batches of 8 independent loads so one L2 round trip serves up to 8 pairs.
 __device__ __forceinline__ int bpe_merge_lds(const BpeDev &m, uint16_t *W, int st, int n) {
     while (n > 1) {
-        uint32_t best = 0xFFFFFFFFu;
+        uint32_t best = 0xFFFFu;  // merge_lookup_c: new id (rank order), 0xFFFF = no merge
         int bi = -1;
         for (int i0 = 0; i0 + 1 < n; i0 += 8) {
             uint32_t v[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int i = i0 + q;
-                v[q] = i + 1 < n ? merge_lookup(m, W[st + i], W[st + i + 1]) : 0xFFFFFFFFu;
+                v[q] = i + 1 < n ? merge_lookup_c(m, W[st + i], W[st + i + 1]) : 0xFFFFu;
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q)
@@ -411,14 +426,19 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     pc.mark(TP_E);
     // ---------------- pass S: starts of the pre-tokens with >= 2 symbols (a single symbol has
     // nothing to merge), to the TOP of V (V[T_E-1-k]) so pass B can use bytes + the bottom of V
-    // for its rank rows (at most T_BCAP / 2 such pre-tokens).
+    // for its rank rows (at most T_SCAP such pre-tokens; more: the tile's rows fall back).
     uint32_t nw = 0;
     for (uint32_t base = 0; base < wlen; base += 64) {
         const uint32_t kk = base + lane;
         const bool multi = kk + 1 < wlen && (M.w[kk] & 0x8000u) && M.w[kk] < V_SPECIAL && !(M.w[kk + 1] & 0x8000u);
         const uint64_t MM = w_ballot(multi);
-        if (multi) M.v[T_E - 1 - (nw + (uint32_t)w_popc(MM & lt))] = (uint16_t)kk;
+        const uint32_t j = nw + (uint32_t)w_popc(MM & lt);
+        if (multi && j < (uint32_t)T_SCAP) M.v[T_E - 1 - j] = (uint16_t)kk;
         nw += (uint32_t)w_popc(MM);
+    }
+    if (nw > (uint32_t)T_SCAP) {
+        if (lane < nr) M.fb[lane] = 1;
+        nw = 0;
     }
     w_sync();
 
@@ -430,8 +450,8 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     // the smallest id is the lowest rank). One round = 2 ds_read_b128 + a packed-u16 min + two
     // cuckoo lookups for the new neighbours + 3 u16 writes. Longer pre-tokens merge in LDS.
     {
-        // 64 rank rows fit bytes + the part of V below the kept starts (at most T_BCAP / 2 of them)
-        static_assert(64 * 2 * WREG <= (T_BCAP + 32) + 2 * (T_E - T_BCAP / 2), "rank rows overlap the starts");
+        // 64 rank rows fit bytes + the part of V below the kept starts (at most T_SCAP of them)
+        static_assert(64 * 2 * WREG <= (T_BCAP + 32) + 2 * (T_E - T_SCAP), "rank rows overlap the starts");
         uint16_t *rk16 = (uint16_t *)(M.bytes + lane * (2 * WREG));
         for (uint32_t wb = 0; wb < nw; wb += 64) {
             const uint32_t j = wb + lane;
@@ -451,8 +471,8 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
 #pragma unroll
             for (int k = 0; k < WREG / 2; ++k) {
                 const int i = 2 * k;
-                const uint32_t lo = (reg && i + 1 < n) ? merge_lookup(m, sy[i] & 0x7FFFu, sy[i + 1]) & 0xFFFFu : 0xFFFFu;
-                const uint32_t hi = (i + 2 < WREG && reg && i + 2 < n) ? merge_lookup(m, sy[i + 1], sy[(i + 2) % WREG]) & 0xFFFFu : 0xFFFFu;
+                const uint32_t lo = (reg && i + 1 < n) ? merge_lookup_c(m, sy[i] & 0x7FFFu, sy[i + 1]) & 0xFFFFu : 0xFFFFu;
+                const uint32_t hi = (i + 2 < WREG && reg && i + 2 < n) ? merge_lookup_c(m, sy[i + 1], sy[(i + 2) % WREG]) & 0xFFFFu : 0xFFFFu;
                 d[k] = lo | (hi << 16);
             }
             w_sync();  // every lane has read V and its window before rank rows overwrite bytes / V
@@ -494,8 +514,8 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     M.w[st + bi] = (uint16_t)minv;
                     M.w[st + jn] = V_DEAD;
                     alive &= ~(1u << jn);
-                    const uint32_t L = pl >= 0 ? merge_lookup(m, left, minv) & 0xFFFFu : 0xFFFFu;
-                    const uint32_t R = q >= 0 ? merge_lookup(m, minv, right) & 0xFFFFu : 0xFFFFu;
+                    const uint32_t L = pl >= 0 ? merge_lookup_c(m, left, minv) & 0xFFFFu : 0xFFFFu;
+                    const uint32_t R = q >= 0 ? merge_lookup_c(m, minv, right) & 0xFFFFu : 0xFFFFu;
                     if (pl >= 0) rk16[pl] = (uint16_t)L;
                     rk16[bi] = (uint16_t)R;
                     rk16[jn] = 0xFFFFu;
@@ -567,7 +587,7 @@ template <int FLAGS>
 __device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *sfast, TileWaveMem &M,
                                uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
-    pc.init(ta.passprof != nullptr);
+    pc.init(ta.passprof != nullptr, M.passacc);
     for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {  // static stride: tiles are near-equal
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * (uint64_t)ta.rows;

@@ -32,6 +32,7 @@ extern "C" void *emu_bpe_create(uint32_t n_single, const uint32_t *cp, const uin
     EmuModel *m = new EmuModel();
     if (!akb::build_bpe(n_single, cp, id, n_merges, merges, m->bpe).empty()) { delete m; return nullptr; }
     m->bdev.merge_tab = m->bpe.tab.data();
+    m->bdev.merge_ctab = m->bpe.ctab.data();
     m->bdev.tab_mask = m->bpe.mask;
     m->bdev.tab_shift = m->bpe.shift;
     m->bdev.single_sorted_cp = m->bpe.rest_cp.data();
@@ -154,8 +155,9 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     EmuModel *m = (EmuModel *)model;
     if (flags != 3) return -1;
     static uint2 fast[FAST_N];
-    static uint32_t hot_tab[FAST_N];
-    for (uint32_t i = 0; i < FAST_N; ++i) { fast[i] = prop_global(i); hot_tab[i] = hot_of(fast[i]); }
+    static uint32_t hot_tab[HOT_N];
+    for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
+    for (uint32_t i = 0; i < HOT_N; ++i) hot_tab[i] = hot_of(prop_global(hot_cp(i)));
     if (n == 0) { out_offs[0] = 0; return 0; }
     std::vector<uint32_t> stage(offs[n] + 2 * n + 64), counts(n), fbl(n), fb2(n);
     uint32_t fbn = 0, fb2n = 0, err = 0;
