@@ -60,6 +60,12 @@ def _deps(src, seen=None):
     return seen
 
 
+# per-TU code-generation flags. ak_k_bpe_tiles.hip: without machine LICM the tile kernel keeps its
+# per-lane constants and addresses in-loop (rematerialised) and fits the 64 VGPRs of 8 waves/SIMD
+# with no scratch spills (with it: 20 VGPRs spilled to scratch in every tile's prologue).
+TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"]}
+
+
 def build_hip(force=False, jobs=None):
     """Compile each stale .hip TU (own source or any header it reaches changed) to an object in
     parallel, then link the shared library."""
@@ -81,7 +87,7 @@ def build_hip(force=False, jobs=None):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _stale(obj, sorted(_deps(src))):
-            cmds.append(common + ["-c", "-o", obj, src])
+            cmds.append(common + TU_FLAGS.get(os.path.basename(src), []) + ["-c", "-o", obj, src])
     jobs = jobs or min(max(len(cmds), 1), max(1, (os.cpu_count() or 4)), 16)
     with ThreadPoolExecutor(jobs) as ex:
         for f in [ex.submit(_run, c) for c in cmds]:

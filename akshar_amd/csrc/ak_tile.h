@@ -253,7 +253,6 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                         TileWaveMem &M, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
-    const uint64_t lt = w_lanemask_lt();
     const RowArgs &a = ta.ra;
     const BpeDev &m = a.bpe;
     const int nr0 = (int)(rend - r0);
@@ -298,7 +297,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             const bool lead = in && (b & 0xC0u) != 0x80u;
             if (w_ballot(in && !lead && p == s)) { bad_row = true; break; }
             const uint64_t LM = w_ballot(lead);
-            if (lead) P[np + (uint32_t)w_popc(LM & lt)] = (uint16_t)p;
+            if (lead) P[np + w_rank(LM)] = (uint16_t)p;
             np += (uint32_t)w_popc(LM);
         }
         if (bad_row && lane == 0) M.fb[i] = 1;
@@ -319,7 +318,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             const uint32_t ent = in ? P[c] : 0x8000u;
             const bool mark = in && (ent & 0x8000u);
             const uint64_t RMK = w_ballot(mark);
-            const int row = (int)(rows + (uint32_t)w_popc(RMK & (lt | (1ull << lane)))) - 1;
+            const int row = (int)(rows + w_rank_incl(RMK)) - 1;
             const bool chr = in && !mark;
             uint32_t h = H_ROWSTART;
             bool bad = false;
@@ -386,6 +385,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             if (!special && (h & H_HFSPACE)) { x = 0x20; h = hot(H, 0x20); }
             const int cls = special ? HF_S : (int)((h >> H_CLS_SHIFT) & 3u);
             const uint64_t KM = w_ballot(keep);
+            const uint64_t lt = w_lanemask_lt();  // N only: the nearest kept lane below
             const uint64_t pk = KM & lt;
             const int src = pk ? msb64(pk) : 0;
             const uint32_t h_l = w_shfl(h, src);
@@ -395,11 +395,11 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             // HF-NFC quick check -> row fallback
             const uint64_t RM = w_ballot(keep && (x == V_B || x == V_FB));
             const bool trig = keep && !special && !(h & H_HFST) && nfc_trig<true>(h, hprev);
-            if (trig) M.fb[rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1] = 1;
+            if (trig) M.fb[rs + w_rank_incl(RM) - 1] = 1;
             // pre-tokenizer + ids
             const bool wordchar = keep && !special && cls != HF_S;
             const uint64_t SM = w_ballot(wordchar && cls != cprev);
-            const uint32_t word = carry_word + (uint32_t)w_popc(SM & (lt | (1ull << lane)));  // inclusive
+            const uint32_t word = carry_word + w_rank_incl(SM);  // inclusive
             const uint32_t id = wordchar ? single_id_of(m, sfast, a.single_fast, x) : 0xFFFFu;
             const bool kept = id != 0xFFFFu;
             const uint64_t K2 = w_ballot(kept);
@@ -409,7 +409,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             const bool kstart = kept && word != kprev;
             const bool out = kept || (keep && special);
             const uint64_t OM = w_ballot(out);
-            if (out) M.w[wlen + (uint32_t)w_popc(OM & lt)] = special ? x : (uint16_t)(id | (kstart ? WSTART : 0u));
+            if (out) M.w[wlen + w_rank(OM)] = special ? x : (uint16_t)(id | (kstart ? WSTART : 0u));
             wlen += (uint32_t)w_popc(OM);
             rs += (uint32_t)w_popc(RM);
             if (KM) {
@@ -432,7 +432,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const uint32_t kk = base + lane;
         const bool multi = kk + 1 < wlen && (M.w[kk] & 0x8000u) && M.w[kk] < V_SPECIAL && !(M.w[kk + 1] & 0x8000u);
         const uint64_t MM = w_ballot(multi);
-        const uint32_t j = nw + (uint32_t)w_popc(MM & lt);
+        const uint32_t j = nw + w_rank(MM);
         if (multi && j < (uint32_t)T_SCAP) M.v[T_E - 1 - j] = (uint16_t)kk;
         nw += (uint32_t)w_popc(MM);
     }
@@ -538,7 +538,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(ta.fb_count, (uint32_t)w_popc(FM));
             base = w_bcast(base, 0);
-            if (isfb) ta.fb_list[base + (uint32_t)w_popc(FM & lt)] = (uint32_t)(r0 + (uint64_t)lane);
+            if (isfb) ta.fb_list[base + w_rank(FM)] = (uint32_t)(r0 + (uint64_t)lane);
         }
     }
 
@@ -556,11 +556,11 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const uint16_t x = in ? M.w[kk] : V_DEAD;
         const bool isrow = in && (x == V_B || x == V_FB);
         const uint64_t RM = w_ballot(isrow);
-        const uint32_t row = rs + (uint32_t)w_popc(RM & (lt | (1ull << lane))) - 1;
+        const uint32_t row = rs + w_rank_incl(RM) - 1;
         const bool emit = in && x != V_FB && x != V_DEAD && !M.fb[row];
         const uint64_t EM = w_ballot(emit);
-        const uint32_t op = pos + (uint32_t)w_popc(EM & lt);
-        if (isrow) M.rowop[rs + (uint32_t)w_popc(RM & lt)] = op;
+        const uint32_t op = pos + w_rank(EM);
+        if (isrow) M.rowop[rs + w_rank(RM)] = op;
         w_sync();
         if (emit) {
             const uint64_t d = (uint64_t)M.rowslot[row] + (op - M.rowop[row]);

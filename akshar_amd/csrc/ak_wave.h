@@ -143,6 +143,16 @@ __device__ __forceinline__ uint64_t w_lanemask_lt() {
     return l == 0 ? 0ull : (~0ull >> (64 - l));
 }
 __device__ __forceinline__ int w_popc(uint64_t m) { return __builtin_popcountll(m); }
+// set bits of the wave-uniform mask m below this lane: v_mbcnt_lo/hi, no per-lane mask register
+__device__ __forceinline__ uint32_t w_rank(uint64_t m) {
+#ifdef AK_HOST_EMU
+    return (uint32_t)w_popc(m & w_lanemask_lt());
+#else
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+#endif
+}
+// ... at or below this lane (the shift and the low bit are scalar work on the uniform mask)
+__device__ __forceinline__ uint32_t w_rank_incl(uint64_t m) { return w_rank(m >> 1) + (uint32_t)(m & 1ull); }
 // wave-wide 64-bit sum (butterfly), every lane gets the total
 __device__ __forceinline__ uint64_t w_sum64(uint64_t x) {
     const int l = w_lane();
