@@ -96,29 +96,41 @@ __global__ __launch_bounds__(64) void k_tile_fb_slow(TileArgs ta) {
     }
 }
 
-// staged ids -> final positions; one wave per tile of R rows, lanes spread over the tile's ids
+// staged ids -> final positions. One wave per group of 32 rows: lanes 0..32 hold the group's output
+// offsets, lanes 0..31 its slot starts; rows go COPY_B at a time, one masked load per row (a row has
+// < 64 ids: 64 lanes cover it; longer rows finish in a loop), all COPY_B loads in flight before
+// the stores, so a group costs 4 L2/HBM round trips instead of one per row (16: slower).
+constexpr int COPY_G = 32;
+constexpr int COPY_B = 8;   // rows whose loads are in flight together
 __global__ __launch_bounds__(256) void k_tile_copy(const uint32_t *__restrict__ stage, const uint64_t *__restrict__ offs,
-                                                   const uint64_t *__restrict__ out_offs, uint64_t n, uint32_t R,
-                                                   uint64_t ntiles, uint32_t *__restrict__ ids, uint64_t cap,
-                                                   uint64_t stage_cap) {
+                                                   const uint64_t *__restrict__ out_offs, uint64_t n,
+                                                   uint32_t *__restrict__ ids, uint64_t cap, uint64_t stage_cap) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t t = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < ntiles; t += nwaves) {
-        const uint64_t r0 = t * R;
-        const int nr = (int)((r0 + R < n ? r0 + R : n) - r0);
-        // lane j <= nr holds the tile's row j: output start and slot start
+    const uint64_t ngroups = (n + COPY_G - 1) / COPY_G;
+    for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < ngroups; g += nwaves) {
+        const uint64_t r0 = g * COPY_G;
+        const int nr = (int)(r0 + COPY_G < n ? COPY_G : n - r0);
         const uint64_t oo = lane <= nr ? out_offs[r0 + lane] : 0ull;
-        const uint64_t so = lane < nr ? offs[r0 + lane] + 2 * (r0 + lane) : 0ull;
-        const uint64_t d0 = w_bcast(oo, 0), d1 = w_bcast(oo, nr);
-        for (uint64_t o = d0 + lane; o < d1; o += 64) {
-            // last row whose output starts at or before o (<= 16 rows: a uniform readlane scan)
-            uint64_t src_row = w_bcast(so, 0), out_row = d0;
-            for (int j = 1; j < nr; ++j) {
-                const uint64_t oj = w_bcast(oo, j), sj = w_bcast(so, j);
-                if (oj <= o) { out_row = oj; src_row = sj; }
+        const uint64_t so = lane < nr ? offs[r0 + lane] + 2 * (r0 + (uint64_t)lane) : 0ull;
+        for (int j0 = 0; j0 < nr; j0 += COPY_B) {
+            uint32_t v[COPY_B];
+#pragma unroll
+            for (int q = 0; q < COPY_B; ++q) {
+                const int j = j0 + q < nr ? j0 + q : nr - 1;
+                const uint64_t d0 = w_bcast(oo, j), d1 = w_bcast(oo, j + 1), s0 = w_bcast(so, j);
+                const uint64_t src = s0 + (uint64_t)lane;
+                v[q] = (j0 + q < nr && (uint64_t)lane < d1 - d0 && src < stage_cap) ? stage[src] : 0u;
             }
-            const uint64_t src = src_row + (o - out_row);
-            if (o < cap && src < stage_cap) ids[o] = stage[src];
+#pragma unroll
+            for (int q = 0; q < COPY_B; ++q) {
+                const int j = j0 + q < nr ? j0 + q : nr - 1;
+                const uint64_t d0 = w_bcast(oo, j), d1 = w_bcast(oo, j + 1), s0 = w_bcast(so, j);
+                const uint64_t dst = d0 + (uint64_t)lane;
+                if (j0 + q < nr && (uint64_t)lane < d1 - d0 && dst < cap) ids[dst] = v[q];
+                for (uint64_t o = 64 + (uint64_t)lane; j0 + q < nr && o < d1 - d0; o += 64)  // rows of >= 64 ids
+                    if (d0 + o < cap && s0 + o < stage_cap) ids[d0 + o] = stage[s0 + o];
+            }
         }
     }
 }
@@ -244,10 +256,10 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     rc = scan_counts(w, a0.n, out_offs, st);
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
-    const unsigned cgrid = (unsigned)std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)num_cus() * 8);
+    const uint64_t ngroups = (a0.n + COPY_G - 1) / COPY_G;
+    const unsigned cgrid = (unsigned)std::min<uint64_t>((ngroups + 3) / 4, (uint64_t)num_cus() * 8);
     AK_PROF(AK_PROF_COPY, false, st);
-    k_tile_copy<<<cgrid, 256, 0, st>>>(w->stage, a0.offs, out_offs, a0.n, (uint32_t)R, ntiles, (uint32_t *)a0.out,
-                                       a0.cap, w->cap_stage);
+    k_tile_copy<<<cgrid, 256, 0, st>>>(w->stage, a0.offs, out_offs, a0.n, (uint32_t *)a0.out, a0.cap, w->cap_stage);
     AK_PROF(AK_PROF_COPY, true, st);
     HIP_TRY(hipGetLastError());
     return AK_OK;
