@@ -596,26 +596,33 @@ struct BpeSink {  // normalized stream -> HF NFKC -> BpeWordSink
 
 // ------------------------------------------------------------------------------------------
 // SentencePiece unigram (0.2.2 EncodeOptimized) with the identity normalizer and byte fallback.
+// (The trie is walked per code point; sentencepiece walks UTF-8 bytes, but a piece match always
+// ends on a char boundary, so the set of (start, piece) lattice nodes is the same.)
 // Every U+2581 is a forced lattice boundary when no piece holds it past its first char
 // (checked at model load), so the Viterbi runs one "▁word" at a time with the running best
 // score carried across words — the same float/double arithmetic as the whole-row lattice.
 
 struct SpmDev {
-    const int4 *trie;      // double array: {check, base, value, 0}; value = id | kind << 24
-    const float *scores;
+    const int4 *trie;      // code-point double array: {check, base, value, aux}; value = id | kind << 24,
+                           // aux = score bits (normal) or UTF-8 byte length (user defined)
+    const uint16_t *cmap_page;  // cp >> 7 -> page (0: no piece holds a char of it)
+    const uint16_t *cmap;       // page * 128 + (cp & 127) -> code 1..K, 0 = in no piece
+    const uint32_t *code_cp;    // code -> cp
     const int32_t *byte_ids;
+    int32_t root_base;
     int32_t unk_id;
     float unk_score;       // min_score - 10
     float max_score;
 };
 
-__device__ __forceinline__ int trie_step(const SpmDev &m, int node, uint32_t byte, int &value) {
-    const int4 r = m.trie[node];
-    const int t = r.y + (int)byte + 1;
-    const int4 e = m.trie[t];
-    if (e.x != node) return -1;
-    value = e.z;
-    return t;
+// word chars are stored as 0x80000000 | code for chars some piece holds, the plain code point
+// otherwise (the walk stops there; such a char can only become an unk node)
+constexpr uint32_t SPM_CODED = 0x80000000u;
+
+__device__ __forceinline__ uint32_t spm_code(const SpmDev &m, uint32_t cp) {
+    const uint32_t pg = m.cmap_page[cp >> 7];
+    const uint32_t c = m.cmap[pg * 128u + (cp & 127u)];
+    return c ? (SPM_CODED | c) : cp;
 }
 
 struct SpmSink {
@@ -628,51 +635,56 @@ struct SpmSink {
     __device__ __forceinline__ void init(const SpmDev *md, Scratch *s) {
         m = md; sc = s; started = false; pending_space = false; wl = 0; base = 0.0f;
     }
+    __device__ __forceinline__ void put_bytes(uint32_t cp) {
+        const int cl = utf8_len(cp);
+        if (cl == 1) c.put((uint32_t)m->byte_ids[cp]);
+        else if (cl == 2) { c.put((uint32_t)m->byte_ids[0xC0u | (cp >> 6)]); c.put((uint32_t)m->byte_ids[0x80u | (cp & 63u)]); }
+        else if (cl == 3) {
+            c.put((uint32_t)m->byte_ids[0xE0u | (cp >> 12)]); c.put((uint32_t)m->byte_ids[0x80u | ((cp >> 6) & 63u)]);
+            c.put((uint32_t)m->byte_ids[0x80u | (cp & 63u)]);
+        } else {
+            c.put((uint32_t)m->byte_ids[0xF0u | (cp >> 18)]); c.put((uint32_t)m->byte_ids[0x80u | ((cp >> 12) & 63u)]);
+            c.put((uint32_t)m->byte_ids[0x80u | ((cp >> 6) & 63u)]); c.put((uint32_t)m->byte_ids[0x80u | (cp & 63u)]);
+        }
+    }
     __device__ __forceinline__ void solve() {
         const int L = wl;
         float *best = sc->vbest;
         int32_t *start = sc->vstart;
         int32_t *pid = sc->vid;
+        const uint32_t *vc = sc->vchar;
         best[0] = base;
         for (int i = 1; i <= L; ++i) { start[i] = -1; best[i] = 0.0f; pid[i] = -1; }
         for (int s = 0; s < L; ++s) {
             const float till = best[s];
             bool has_single = false;
-            int node = 0;
-            int length = 0;
-            const int mblen = utf8_len(sc->vchar[s]);
-            for (int k = s; k < L && node >= 0; ++k) {
-                const uint32_t cp = sc->vchar[k];
-                const int cl = utf8_len(cp);
-                int value = -1;
-                if (cl == 1) node = trie_step(*m, node, cp, value);
-                else {
-                    uint32_t bytes[4];
-                    if (cl == 2) { bytes[0] = 0xC0u | (cp >> 6); bytes[1] = 0x80u | (cp & 63u); }
-                    else if (cl == 3) { bytes[0] = 0xE0u | (cp >> 12); bytes[1] = 0x80u | ((cp >> 6) & 63u); bytes[2] = 0x80u | (cp & 63u); }
-                    else { bytes[0] = 0xF0u | (cp >> 18); bytes[1] = 0x80u | ((cp >> 12) & 63u); bytes[2] = 0x80u | ((cp >> 6) & 63u); bytes[3] = 0x80u | (cp & 63u); }
-                    for (int q = 0; q < cl && node >= 0; ++q) node = trie_step(*m, node, bytes[q], value);
-                }
-                if (node < 0) break;
-                length += cl;
+            int node = 0, nb = m->root_base;
+            for (int k = s; k < L; ++k) {
+                const uint32_t v = vc[k];
+                if (!(v & SPM_CODED)) break;
+                const int t = nb + (int)(v & ~SPM_CODED);
+                const int4 e = m->trie[t];
+                if (e.x != node) break;
+                node = t;
+                nb = e.y;
+                const int value = e.z;
                 if (value < 0) continue;
                 const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
-                const int id = value & 0xFFFFFF;
                 if (kind == 2) continue;
-                const double score = kind == 1 ? (double)((float)length * m->max_score) - 0.1 : (double)m->scores[id];
+                const int id = value & 0xFFFFFF;
+                const double score = kind == 1 ? (double)((float)e.w * m->max_score) - 0.1 : (double)__int_as_float(e.w);
                 const double cand = score + (double)till;
-                const int e = k + 1;
-                if (start[e] == -1 || cand > (double)best[e]) { best[e] = (float)cand; start[e] = s; pid[e] = id; }
-                if (!has_single && length == mblen) has_single = true;
+                const int ee = k + 1;
+                if (start[ee] == -1 || cand > (double)best[ee]) { best[ee] = (float)cand; start[ee] = s; pid[ee] = id; }
+                if (k == s) has_single = true;  // sentencepiece: a piece of length == the first char's length
             }
             if (!has_single) {
-                const int e = s + 1;
+                const int ee = s + 1;
                 const float cand = m->unk_score + till;
-                if (start[e] == -1 || cand > best[e]) { best[e] = cand; start[e] = s; pid[e] = m->unk_id; }
+                if (start[ee] == -1 || cand > best[ee]) { best[ee] = cand; start[ee] = s; pid[ee] = m->unk_id; }
             }
         }
-        // backtrack: mark the path by chaining start[] into a forward list in vstart
-        // (reuse best[] as a scratch "next" array: nxt[s] = e for each node s->e on the path)
+        // backtrack: chain start[] into a forward list (best[] reused as "next": nxt[s] = e)
         int e = L;
         int32_t *nxt = (int32_t *)best;
         const float keep = best[L];
@@ -680,18 +692,9 @@ struct SpmSink {
         for (int s = 0; s < L;) {
             const int t = nxt[s];
             const int id = pid[t];
-            if (id == m->unk_id) {
-                const uint32_t cp = sc->vchar[s];  // an unk node is exactly one char
-                const int cl = utf8_len(cp);
-                if (cl == 1) c.put((uint32_t)m->byte_ids[cp]);
-                else if (cl == 2) { c.put((uint32_t)m->byte_ids[0xC0u | (cp >> 6)]); c.put((uint32_t)m->byte_ids[0x80u | (cp & 63u)]); }
-                else if (cl == 3) {
-                    c.put((uint32_t)m->byte_ids[0xE0u | (cp >> 12)]); c.put((uint32_t)m->byte_ids[0x80u | ((cp >> 6) & 63u)]);
-                    c.put((uint32_t)m->byte_ids[0x80u | (cp & 63u)]);
-                } else {
-                    c.put((uint32_t)m->byte_ids[0xF0u | (cp >> 18)]); c.put((uint32_t)m->byte_ids[0x80u | ((cp >> 12) & 63u)]);
-                    c.put((uint32_t)m->byte_ids[0x80u | ((cp >> 6) & 63u)]); c.put((uint32_t)m->byte_ids[0x80u | (cp & 63u)]);
-                }
+            if (id == m->unk_id) {  // an unk node is exactly one char: byte fallback
+                const uint32_t v = vc[s];
+                put_bytes((v & SPM_CODED) ? m->code_cp[v & ~SPM_CODED] : v);
             } else {
                 c.put((uint32_t)id);
             }
@@ -703,7 +706,7 @@ struct SpmSink {
     __device__ __forceinline__ void put_char(uint32_t cp) {
         if (cp == 0x2581u && wl > 0) solve();
         if (wl >= sc->vcap) { sc->status |= sc->slow_status; return; }
-        sc->vchar[wl++] = cp;
+        sc->vchar[wl++] = spm_code(*m, cp);
     }
     __device__ __forceinline__ void push(uint32_t cp) {
         if (cp == 0x20u) { if (started) pending_space = true; return; }

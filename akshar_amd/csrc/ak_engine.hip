@@ -122,7 +122,9 @@ struct ak_bpe {
 struct ak_spm {
     SpmDev dev;
     int4 *d_trie = nullptr;
-    float *d_scores = nullptr;
+    uint16_t *d_cmap_page = nullptr;
+    uint16_t *d_cmap = nullptr;
+    uint32_t *d_code_cp = nullptr;
     int32_t *d_byte_ids = nullptr;
     uint32_t n_nodes = 0;
 };
@@ -188,12 +190,19 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->n_nodes = t.n_nodes;
     HIP_TRY(hipMalloc(&m->d_trie, t.n_nodes * sizeof(int4)));
     HIP_TRY(hipMemcpy(m->d_trie, t.trie.data(), t.n_nodes * sizeof(int4), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&m->d_scores, std::max<uint32_t>(n, 1) * sizeof(float)));
-    HIP_TRY(hipMemcpy(m->d_scores, scores, n * sizeof(float), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_cmap_page, t.cmap_page.size() * sizeof(uint16_t)));
+    HIP_TRY(hipMemcpy(m->d_cmap_page, t.cmap_page.data(), t.cmap_page.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_cmap, t.cmap.size() * sizeof(uint16_t)));
+    HIP_TRY(hipMemcpy(m->d_cmap, t.cmap.data(), t.cmap.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&m->d_code_cp, t.code_cp.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(m->d_code_cp, t.code_cp.data(), t.code_cp.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&m->d_byte_ids, 256 * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(m->d_byte_ids, byte_ids, 256 * sizeof(int32_t), hipMemcpyHostToDevice));
     m->dev.trie = m->d_trie;
-    m->dev.scores = m->d_scores;
+    m->dev.cmap_page = m->d_cmap_page;
+    m->dev.cmap = m->d_cmap;
+    m->dev.code_cp = m->d_code_cp;
+    m->dev.root_base = t.root_base;
     m->dev.byte_ids = m->d_byte_ids;
     m->dev.unk_id = unk_id;
     m->dev.unk_score = t.min_score - 10.0f;
@@ -205,7 +214,9 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
 extern "C" void ak_spm_free(ak_spm *m) {
     if (!m) return;
     (void)hipFree(m->d_trie);
-    (void)hipFree(m->d_scores);
+    (void)hipFree(m->d_cmap_page);
+    (void)hipFree(m->d_cmap);
+    (void)hipFree(m->d_code_cp);
     (void)hipFree(m->d_byte_ids);
     delete m;
 }

@@ -2,6 +2,7 @@
 // on the CPU (debugging aid; never part of the product library).
 #pragma once
 #include <stdint.h>
+#include <string.h>
 #define __device__
 #define __host__
 #define __forceinline__ inline
@@ -12,6 +13,7 @@ struct alignas(16) uint4 { uint32_t x, y, z, w; };
 static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }
 static inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
 static inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
+static inline float __int_as_float(int v) { float f; memcpy(&f, &v, 4); return f; }
 #define __HIP_MEMORY_SCOPE_AGENT 0
 template <class T>
 static inline T __hip_atomic_exchange(T *p, T v, int, int) { return __atomic_exchange_n(p, v, __ATOMIC_SEQ_CST); }

@@ -57,6 +57,9 @@ void prof_mark(int kernel, bool end, hipStream_t st);
     do { if (ak::g_prof_on) ak::prof_mark((k), (end), (st)); } while (0)
 
 int ws_reserve(AkWs *w, uint64_t n);
+int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st);
+int launch_stage_copy(AkWs *w, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, uint32_t *ids, uint64_t cap,
+                      uint32_t mul, uint32_t add, hipStream_t st);
 int scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st);
 int num_cus();
 
@@ -184,6 +187,118 @@ inline int launch_rows(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_t st) {
     AK_PROF(AK_PROF_EMIT_SLOW, true, st);
     HIP_TRY(hipGetLastError());
     return AK_OK;
+}
+
+
+// ---- single-pass staged rows (SPM): the row pipeline runs ONCE, straight into a per-row staging
+// slot of the workspace (row r owns [mul*offs[r] + add*r, mul*offs[r+1] + add*(r+1)): mul / add
+// bound the op's output per raw byte / per row), then counts -> offsets and one coalesced copy.
+// Halves the work of count -> scan -> emit for ops whose per-row cost is the pipeline itself.
+template <int OP, int FLAGS>
+__global__ __launch_bounds__(ROW_BLOCK) void k_rows_stage(RowArgs a, uint32_t mul, uint32_t add) {
+    __shared__ uint2 fast[FAST_N];
+    __shared__ uint16_t sfast[1];
+    stage_tables(fast, sfast, nullptr, false);
+    uint32_t seg[FAST_SEG], seg2[FAST_SEG];
+    uint32_t dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
+    uint32_t vchar[OP == OP_SPM ? FAST_VCAP : 1];
+    float vbest[OP == OP_SPM ? FAST_VCAP + 1 : 1];
+    int32_t vstart[OP == OP_SPM ? FAST_VCAP + 1 : 1];
+    int32_t vid[OP == OP_SPM ? FAST_VCAP + 1 : 1];
+    Scratch sc;
+    sc.seg = seg; sc.dec = dec; sc.seg2 = seg2; sc.dec2 = dec2; sc.seg_cap = FAST_SEG;
+    sc.wsym = nullptr; sc.wpair = nullptr; sc.word_cap = 0;
+    sc.vchar = vchar; sc.vbest = vbest; sc.vstart = vstart; sc.vid = vid; sc.vcap = FAST_VCAP;
+    sc.slow_status = ST_SLOW;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
+        sc.status = 0;
+        const uint64_t b = a.offs[r], e = a.offs[r + 1];
+        const uint64_t s0 = mul * b + add * r, s1 = mul * e + add * (r + 1);
+        const uint64_t cnt = process_row<OP, FLAGS, true>(a, r, fast, sfast, &sc, s0, s1);
+        if (sc.status & ST_SLOW) {
+            a.slow_list[atomicAdd(a.slow_count, 1u)] = (uint32_t)r;
+            continue;
+        }
+        const bool over = cnt > s1 - s0;  // cannot happen (mul / add are worst-case bounds): reported, not hidden
+        a.counts[r] = over ? 0u : (uint32_t)cnt;
+        if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (over ? ST_LIMIT : 0u));
+    }
+}
+
+template <int OP, int FLAGS>
+__global__ __launch_bounds__(64) void k_rows_stage_slow(RowArgs a, uint32_t mul, uint32_t add) {
+    __shared__ uint2 fast[FAST_N];
+    __shared__ uint16_t sfast[1];
+    const uint32_t ns = *a.slow_count;
+    if (ns == 0) return;  // uniform: the common case
+    stage_tables(fast, sfast, nullptr, false);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < SLOW_THREADS
+    Scratch sc;
+    sc.seg = a.pool.seg + t * 2 * SLOW_SEG;
+    sc.dec = a.pool.dec + t * 8 * SLOW_SEG;
+    sc.seg2 = sc.seg + SLOW_SEG;
+    sc.dec2 = sc.dec + 4 * SLOW_SEG;
+    sc.seg_cap = SLOW_SEG;
+    sc.wsym = a.pool.wsym + t * SLOW_WORD;
+    sc.wpair = a.pool.wpair + t * SLOW_WORD;
+    sc.word_cap = SLOW_WORD;
+    sc.vchar = a.pool.vchar + t * SLOW_WORD;
+    sc.vbest = a.pool.vbest + t * (SLOW_WORD + 1);
+    sc.vstart = a.pool.vstart + t * (SLOW_WORD + 1);
+    sc.vid = a.pool.vid + t * (SLOW_WORD + 1);
+    sc.vcap = SLOW_WORD;
+    sc.slow_status = ST_LIMIT;
+    for (uint32_t i = (uint32_t)t; i < ns; i += SLOW_THREADS) {
+        const uint64_t r = a.slow_list[i];
+        sc.status = 0;
+        const uint64_t b = a.offs[r], e = a.offs[r + 1];
+        const uint64_t s0 = mul * b + add * r, s1 = mul * e + add * (r + 1);
+        const uint64_t cnt = process_row<OP, FLAGS, true>(a, r, fast, sfast, &sc, s0, s1);
+        const bool lim = (sc.status & ST_LIMIT) != 0 || cnt > s1 - s0;
+        a.counts[r] = lim ? 0u : (uint32_t)cnt;
+        if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0u));
+    }
+}
+
+template <int OP, int FLAGS>
+inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_t st, uint32_t mul, uint32_t add) {
+    if (a.n == 0) {
+        HIP_TRY(hipMemsetAsync(out_offs, 0, 8, st));
+        return AK_OK;
+    }
+    int rc = ws_reserve(w, a.n);
+    if (rc) return rc;
+    uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging area
+    HIP_TRY(hipMemcpyAsync(&nbytes, a.offs + a.n, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    rc = ws_stage_reserve(w, (uint64_t)mul * nbytes + (uint64_t)add * a.n + 64, st);
+    if (rc) return rc;
+    uint32_t *ids = (uint32_t *)a.out;
+    const uint64_t cap = a.cap;
+    a.out = w->stage;
+    a.cap = w->cap_stage;
+    a.counts = w->counts;
+    a.flags = w->flags;
+    a.slow_list = w->slow_list;
+    a.slow_count = w->slow_count;
+    a.pool = w->pool;
+    a.out_offs = nullptr;
+    const uint64_t want = (a.n + ROW_BLOCK - 1) / ROW_BLOCK;
+    const unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)num_cus() * 8);
+    HIP_TRY(hipMemsetAsync(w->slow_count, 0, 4, st));
+    AK_PROF(AK_PROF_EMIT, false, st);
+    k_rows_stage<OP, FLAGS><<<grid, ROW_BLOCK, 0, st>>>(a, mul, add);
+    AK_PROF(AK_PROF_EMIT, true, st);
+    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
+    k_rows_stage_slow<OP, FLAGS><<<SLOW_THREADS / 64, 64, 0, st>>>(a, mul, add);
+    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
+    HIP_TRY(hipGetLastError());
+    AK_PROF(AK_PROF_SCAN, false, st);
+    rc = scan_counts(w, a.n, out_offs, st);
+    if (rc) return rc;
+    AK_PROF(AK_PROF_SCAN, true, st);
+    return launch_stage_copy(w, a.offs, out_offs, a.n, ids, cap, mul, add, st);
 }
 
 

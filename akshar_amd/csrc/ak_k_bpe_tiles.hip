@@ -102,9 +102,11 @@ __global__ __launch_bounds__(64) void k_tile_fb_slow(TileArgs ta) {
 // the stores, so a group costs 4 L2/HBM round trips instead of one per row (16: slower).
 constexpr int COPY_G = 32;
 constexpr int COPY_B = 8;   // rows whose loads are in flight together
+// The slot of row r starts at mul * offs[r] + add * r (tile BPE: 1, 2; staged SPM: 3, 4).
 __global__ __launch_bounds__(256) void k_tile_copy(const uint32_t *__restrict__ stage, const uint64_t *__restrict__ offs,
                                                    const uint64_t *__restrict__ out_offs, uint64_t n,
-                                                   uint32_t *__restrict__ ids, uint64_t cap, uint64_t stage_cap) {
+                                                   uint32_t *__restrict__ ids, uint64_t cap, uint64_t stage_cap,
+                                                   uint32_t mul, uint32_t add) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t ngroups = (n + COPY_G - 1) / COPY_G;
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(256) void k_tile_copy(const uint32_t *__restrict__ 
         const uint64_t r0 = g * COPY_G;
         const int nr = (int)(r0 + COPY_G < n ? COPY_G : n - r0);
         const uint64_t oo = lane <= nr ? out_offs[r0 + lane] : 0ull;
-        const uint64_t so = lane < nr ? offs[r0 + lane] + 2 * (r0 + (uint64_t)lane) : 0ull;
+        const uint64_t so = lane < nr ? (uint64_t)mul * offs[r0 + lane] + (uint64_t)add * (r0 + (uint64_t)lane) : 0ull;
         for (int j0 = 0; j0 < nr; j0 += COPY_B) {
             uint32_t v[COPY_B];
 #pragma unroll
@@ -189,14 +191,8 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     uint64_t nbytes = 0;
     HIP_TRY(hipMemcpyAsync(&nbytes, a0.offs + a0.n, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    const uint64_t need = nbytes + 2 * a0.n + 64;
-    if (need > w->cap_stage) {
-        (void)hipFree(w->stage);
-        w->stage = nullptr;
-        const uint64_t c = std::max<uint64_t>(need, w->cap_stage + w->cap_stage / 2);
-        HIP_TRY(hipMalloc(&w->stage, c * 4));
-        w->cap_stage = c;
-    }
+    rc = ws_stage_reserve(w, nbytes + 2 * a0.n + 64, st);
+    if (rc) return rc;
     const int R = w->tile_rows;
     const uint64_t ntiles = (a0.n + (uint64_t)R - 1) / (uint64_t)R;
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
@@ -256,10 +252,27 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     rc = scan_counts(w, a0.n, out_offs, st);
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
-    const uint64_t ngroups = (a0.n + COPY_G - 1) / COPY_G;
+    return launch_stage_copy(w, a0.offs, out_offs, a0.n, (uint32_t *)a0.out, a0.cap, 1, 2, st);
+}
+
+int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st) {
+    if (need <= w->cap_stage) return AK_OK;
+    HIP_TRY(hipStreamSynchronize(st));  // the old buffer may still be read by queued work
+    const uint64_t c = std::max<uint64_t>(need, w->cap_stage + w->cap_stage / 2);
+    (void)hipFree(w->stage);
+    w->stage = nullptr;
+    w->cap_stage = 0;
+    HIP_TRY(hipMalloc(&w->stage, c * 4));
+    w->cap_stage = c;
+    return AK_OK;
+}
+
+int launch_stage_copy(AkWs *w, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, uint32_t *ids, uint64_t cap,
+                      uint32_t mul, uint32_t add, hipStream_t st) {
+    const uint64_t ngroups = (n + COPY_G - 1) / COPY_G;
     const unsigned cgrid = (unsigned)std::min<uint64_t>((ngroups + 3) / 4, (uint64_t)num_cus() * 8);
     AK_PROF(AK_PROF_COPY, false, st);
-    k_tile_copy<<<cgrid, 256, 0, st>>>(w->stage, a0.offs, out_offs, a0.n, (uint32_t *)a0.out, a0.cap, w->cap_stage);
+    k_tile_copy<<<cgrid, 256, 0, st>>>(w->stage, offs, out_offs, n, ids, cap, w->cap_stage, mul, add);
     AK_PROF(AK_PROF_COPY, true, st);
     HIP_TRY(hipGetLastError());
     return AK_OK;

@@ -4,10 +4,12 @@
 //       merges, 8-byte entries {left << 16 | right, rank << 16 | new_id}, load factor <= 0.5;
 //       a direct single-char id table for U+0000..U+09FF plus a sorted list for the rest.
 //  SPM  (sentencepiece unigram, tokenizer.py:88-90 / cli.py:232-248): a double-array trie over
-//       the UTF-8 bytes of every NORMAL / USER_DEFINED / UNUSED piece, 16-byte nodes
-//       {check, base, value, 0} so one load serves one byte step.
+//       the code points of every NORMAL / USER_DEFINED / UNUSED piece (dense codes via a paged
+//       code-point map), 16-byte nodes {check, base, value, score} so one load serves one
+//       code point of the walk.
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 #include <string>
@@ -99,19 +101,49 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
 }
 
 struct SpmTables {
-    std::vector<int> trie;  // 4 ints per node: check, base, value, 0
+    std::vector<int> trie;          // 4 ints per node: check, base, value, aux
     uint32_t n_nodes = 0;
+    int root_base = 0;
+    std::vector<uint16_t> cmap_page;  // SPM_CMAP_PAGES entries: page of cp >> 7 (0 = no piece char)
+    std::vector<uint16_t> cmap;       // pages of 128 codes; page 0 all zero
+    std::vector<uint32_t> code_cp;    // code -> code point (code 0 unused)
     float min_score = 0, max_score = 0;
 };
 
-// Double-array trie: node 0 is the root; the child of node s on byte b is t = base[s] + b + 1
-// with check[t] == s; value[t] = piece id | kind << 24 (kind 0 normal, 1 user, 2 unused) or -1.
+constexpr uint32_t SPM_CMAP_PAGES = 0x110000u >> 7;
+
+inline int utf8_decode_piece(const std::string &s, std::vector<uint32_t> &cps) {
+    cps.clear();
+    for (size_t i = 0; i < s.size();) {
+        const unsigned char c = (unsigned char)s[i];
+        int len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+        if (!len || i + len > s.size()) return -1;
+        uint32_t cp = len == 1 ? c : len == 2 ? (c & 31u) : len == 3 ? (c & 15u) : (c & 7u);
+        for (int k = 1; k < len; ++k) {
+            const unsigned char d = (unsigned char)s[i + k];
+            if ((d >> 6) != 2) return -1;
+            cp = (cp << 6) | (d & 63u);
+        }
+        cps.push_back(cp);
+        i += len;
+    }
+    return 0;
+}
+
+// Double-array trie over CODE POINTS of every NORMAL / USER_DEFINED / UNUSED piece: the code
+// points that occur in some piece get dense codes 1..K (cmap), node 0 is the root, the child of
+// node s on code c is t = base[s] + c with check[t] == s. value[t] = piece id | kind << 24 (kind 0
+// normal, 1 user defined, 2 unused) or -1; aux[t] = the piece's score bits (normal) or its UTF-8
+// byte length (user defined, scored by length). One 16-byte load per code point of the walk
+// (the byte-level trie needed two loads per UTF-8 byte plus the score load).
 inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
                              const uint8_t *types, SpmTables &out) {
     if (n >= (1u << 24)) return "too many pieces";
     float min_score = 3.4e38f, max_score = -3.4e38f;
-    struct P { std::string s; int val; };
+    struct P { std::vector<uint32_t> cps; int val; int aux; };
     std::vector<P> ps;
+    std::vector<uint32_t> alpha;
+    std::vector<uint32_t> cps;
     for (uint32_t i = 0; i < n; ++i) {
         const int ty = types[i];
         if (ty == 1) { min_score = std::min(min_score, scores[i]); max_score = std::max(max_score, scores[i]); }
@@ -121,15 +153,37 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
         std::string s((const char *)piece_bytes + a, (size_t)(b - a));
         // a piece holding U+2581 past its first char would break the per-word lattice split
         if (s.find("\xe2\x96\x81", 1) != std::string::npos) return "piece with an inner U+2581";
+        if (utf8_decode_piece(s, cps)) return "piece with invalid UTF-8";
         const int kind = ty == 1 ? 0 : ty == 4 ? 1 : 2;
-        ps.push_back({s, (int)i | (kind << 24)});
+        int aux = 0;
+        if (kind == 0) memcpy(&aux, &scores[i], 4);
+        else if (kind == 1) aux = (int)s.size();
+        ps.push_back({cps, (int)i | (kind << 24), aux});
+        alpha.insert(alpha.end(), cps.begin(), cps.end());
     }
-    std::sort(ps.begin(), ps.end(), [](const P &x, const P &y) { return x.s < y.s; });
-    struct N { std::vector<std::pair<int, int>> kids; int val = -1; };
+    std::sort(alpha.begin(), alpha.end());
+    alpha.erase(std::unique(alpha.begin(), alpha.end()), alpha.end());
+    if (alpha.size() >= 0x7FFFu) return "too many distinct piece characters";
+    const int K = (int)alpha.size();
+    out.code_cp.assign(K + 1, 0);
+    out.cmap_page.assign(SPM_CMAP_PAGES, 0);
+    out.cmap.assign(128, 0);
+    for (int c = 1; c <= K; ++c) {
+        const uint32_t cp = alpha[c - 1];
+        out.code_cp[c] = cp;
+        if (cp >= 0x110000u) return "piece character out of range";
+        uint16_t &pg = out.cmap_page[cp >> 7];
+        if (!pg) { pg = (uint16_t)(out.cmap.size() / 128); out.cmap.resize(out.cmap.size() + 128, 0); }
+        out.cmap[(size_t)pg * 128 + (cp & 127u)] = (uint16_t)c;
+    }
+    auto code_of = [&](uint32_t cp) { return (int)(std::lower_bound(alpha.begin(), alpha.end(), cp) - alpha.begin()) + 1; };
+    std::sort(ps.begin(), ps.end(), [](const P &x, const P &y) { return x.cps < y.cps; });
+    struct N { std::vector<std::pair<int, int>> kids; int val = -1; int aux = 0; };
     std::vector<N> nodes(1);
     for (const P &p : ps) {
         int cur = 0;
-        for (unsigned char ch : p.s) {
+        for (uint32_t cp : p.cps) {
+            const int ch = code_of(cp);
             int nxt = -1;
             for (auto &kd : nodes[cur].kids)
                 if (kd.first == ch) { nxt = kd.second; break; }
@@ -140,9 +194,9 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
             }
             cur = nxt;
         }
-        if (nodes[cur].val < 0) nodes[cur].val = p.val;
+        if (nodes[cur].val < 0) { nodes[cur].val = p.val; nodes[cur].aux = p.aux; }
     }
-    std::vector<int> check, base, value;
+    std::vector<int> check, base, value, aux;
     std::vector<char> used_base;
     auto grow = [&](size_t want) {
         if (check.size() < want) {
@@ -150,6 +204,7 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
             check.resize(m, -2);
             base.resize(m, 0);
             value.resize(m, -1);
+            aux.resize(m, 0);
             used_base.resize(m, 0);
         }
     };
@@ -165,21 +220,22 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
         auto &kids = nodes[u].kids;
         if (kids.empty()) continue;
         std::sort(kids.begin(), kids.end());
-        int b = std::max(0, next_free - kids[0].first - 1);
+        int b = std::max(1, next_free - kids[0].first);
         for (;; ++b) {
-            grow((size_t)b + 258);
+            grow((size_t)b + K + 2);
             if (used_base[b]) continue;
             bool ok = true;
             for (auto &kd : kids)
-                if (check[b + kd.first + 1] != -2) { ok = false; break; }
+                if (check[b + kd.first] != -2) { ok = false; break; }
             if (ok) break;
         }
         used_base[b] = 1;
         base[s] = b;
         for (auto &kd : kids) {
-            const int t = b + kd.first + 1;
+            const int t = b + kd.first;
             check[t] = s;
             value[t] = nodes[kd.second].val;
+            aux[t] = nodes[kd.second].aux;
             slot[kd.second] = t;
             queue.push_back(kd.second);
         }
@@ -187,15 +243,17 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
     }
     size_t nn = check.size();
     while (nn > 1 && check[nn - 1] == -2) --nn;
-    nn += 258;  // every base + byte + 1 probe stays in range
+    nn += (size_t)K + 2;  // every base + code probe stays in range (leaf bases are 0)
     grow(nn);
     out.trie.assign(4 * nn, 0);
     for (size_t i = 0; i < nn; ++i) {
         out.trie[4 * i] = check[i];
         out.trie[4 * i + 1] = base[i];
         out.trie[4 * i + 2] = value[i];
+        out.trie[4 * i + 3] = aux[i];
     }
     out.n_nodes = (uint32_t)nn;
+    out.root_base = base[0];
     out.min_score = min_score;
     out.max_score = max_score;
     return "";

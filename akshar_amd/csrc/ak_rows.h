@@ -85,37 +85,38 @@ __device__ __forceinline__ void run_input(Sink &sink, const uint2 *fast, Scratch
 // Process row r; returns the output count. EMIT writes at out_offs[r].
 template <int OP, int FLAGS, bool EMIT>
 __device__ __forceinline__ uint64_t process_row(const RowArgs &a, uint64_t r, const uint2 *fast, const uint16_t *sfast,
-                                               Scratch *sc, uint64_t emit_base) {
+                                               Scratch *sc, uint64_t emit_base, uint64_t emit_cap = ~0ull) {
     const uint64_t b = a.offs[r], e = a.offs[r + 1];
     Reader rd;
     rd.init(a.in);
     const uint64_t base = EMIT ? emit_base : 0;
+    const uint64_t cap = a.cap < emit_cap ? a.cap : emit_cap;
     if constexpr (OP == OP_NORMALIZE) {
         Utf8Sink s;
-        s.c = Cursor<uint8_t>{(uint8_t *)a.out, base, a.cap, EMIT};
+        s.c = Cursor<uint8_t>{(uint8_t *)a.out, base, cap, EMIT};
         run_input<FLAGS>(s, fast, sc, rd, b, e);
         return s.c.pos - base;
     } else if constexpr (OP == OP_SEGMENT) {
         SegSink s;
-        s.c = Cursor<uint32_t>{(uint32_t *)a.out, base, a.cap, EMIT};
+        s.c = Cursor<uint32_t>{(uint32_t *)a.out, base, cap, EMIT};
         s.init(fast, a.matras != 0);
         run_input<FLAGS>(s, fast, sc, rd, b, e);
         return s.c.pos - base;
     } else if constexpr (OP == OP_SWITCHES) {
         SwitchSink s;
-        s.c = Cursor<uint32_t>{(uint32_t *)a.out, base, a.cap, EMIT};
+        s.c = Cursor<uint32_t>{(uint32_t *)a.out, base, cap, EMIT};
         s.labels = a.labels;
         s.init(fast);
         run_input<FLAGS>(s, fast, sc, rd, b, e);
         return s.c.pos - base;
     } else if constexpr (OP == OP_BPE) {
         BpeSink s;
-        s.init(&a.bpe, fast, sfast, sc, Cursor<uint32_t>{(uint32_t *)a.out, base, a.cap, EMIT});
+        s.init(&a.bpe, fast, sfast, sc, Cursor<uint32_t>{(uint32_t *)a.out, base, cap, EMIT});
         run_input<FLAGS>(s, fast, sc, rd, b, e);
         return s.words.c.pos - base;
     } else {
         SpmSink s;
-        s.c = Cursor<uint32_t>{(uint32_t *)a.out, base, a.cap, EMIT};
+        s.c = Cursor<uint32_t>{(uint32_t *)a.out, base, cap, EMIT};
         s.init(&a.spm, sc);
         run_input<FLAGS>(s, fast, sc, rd, b, e);
         return s.c.pos - base;

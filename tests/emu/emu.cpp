@@ -50,7 +50,10 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->scores.assign(scores, scores + n);
     m->byte_ids.assign(byte_ids, byte_ids + 256);
     m->sdev.trie = (const int4 *)m->spm.trie.data();
-    m->sdev.scores = m->scores.data();
+    m->sdev.cmap_page = m->spm.cmap_page.data();
+    m->sdev.cmap = m->spm.cmap.data();
+    m->sdev.code_cp = m->spm.code_cp.data();
+    m->sdev.root_base = m->spm.root_base;
     m->sdev.byte_ids = m->byte_ids.data();
     m->sdev.unk_id = unk_id;
     m->sdev.unk_score = m->spm.min_score - 10.0f;
