@@ -42,6 +42,8 @@ struct AkWs {
     // tile-cooperative BPE path
     uint32_t *stage = nullptr;      // staged ids, slot of row r at offs[r] + 2 r
     uint64_t cap_stage = 0;
+    uint8_t *stage8 = nullptr;      // staged run labels (switches), same slots as stage
+    uint64_t cap_stage8 = 0;
     uint32_t *tile_misc = nullptr;  // [0] fallback-list length, [1] slot-overflow flag, [2] second list length
     uint32_t *fb2 = nullptr;        // second fallback list (rows past the fast buffers)
     uint64_t cap_fb2 = 0;
@@ -58,8 +60,9 @@ void prof_mark(int kernel, bool end, hipStream_t st);
 
 int ws_reserve(AkWs *w, uint64_t n);
 int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st);
+int ws_stage8_reserve(AkWs *w, uint64_t need, hipStream_t st);
 int launch_stage_copy(AkWs *w, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, uint32_t *ids, uint64_t cap,
-                      uint32_t mul, uint32_t add, hipStream_t st);
+                      uint32_t mul, uint32_t add, hipStream_t st, uint8_t *labels = nullptr);
 int scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st);
 int num_cus();
 
@@ -190,7 +193,7 @@ inline int launch_rows(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_t st) {
 }
 
 
-// ---- single-pass staged rows (SPM): the row pipeline runs ONCE, straight into a per-row staging
+// ---- single-pass staged rows (SPM, segment, switches): the row pipeline runs ONCE, straight into a per-row staging
 // slot of the workspace (row r owns [mul*offs[r] + add*r, mul*offs[r+1] + add*(r+1)): mul / add
 // bound the op's output per raw byte / per row), then counts -> offsets and one coalesced copy.
 // Halves the work of count -> scan -> emit for ops whose per-row cost is the pipeline itself.
@@ -272,8 +275,15 @@ inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_
     uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging area
     HIP_TRY(hipMemcpyAsync(&nbytes, a.offs + a.n, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    rc = ws_stage_reserve(w, (uint64_t)mul * nbytes + (uint64_t)add * a.n + 64, st);
+    const uint64_t need = (uint64_t)mul * nbytes + (uint64_t)add * a.n + 64;
+    rc = ws_stage_reserve(w, need, st);
     if (rc) return rc;
+    uint8_t *labels = a.labels;
+    if (labels) {
+        rc = ws_stage8_reserve(w, need, st);
+        if (rc) return rc;
+        a.labels = w->stage8;
+    }
     uint32_t *ids = (uint32_t *)a.out;
     const uint64_t cap = a.cap;
     a.out = w->stage;
@@ -298,7 +308,7 @@ inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_
     rc = scan_counts(w, a.n, out_offs, st);
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
-    return launch_stage_copy(w, a.offs, out_offs, a.n, ids, cap, mul, add, st);
+    return launch_stage_copy(w, a.offs, out_offs, a.n, ids, cap, mul, add, st, labels);
 }
 
 

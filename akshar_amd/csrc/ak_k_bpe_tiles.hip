@@ -103,9 +103,10 @@ __global__ __launch_bounds__(64) void k_tile_fb_slow(TileArgs ta) {
 constexpr int COPY_G = 32;
 constexpr int COPY_B = 8;   // rows whose loads are in flight together
 // The slot of row r starts at mul * offs[r] + add * r (tile BPE: 1, 2; staged SPM: 3, 4).
-__global__ __launch_bounds__(256) void k_tile_copy(const uint32_t *__restrict__ stage, const uint64_t *__restrict__ offs,
+template <class T>
+__global__ __launch_bounds__(256) void k_tile_copy(const T *__restrict__ stage, const uint64_t *__restrict__ offs,
                                                    const uint64_t *__restrict__ out_offs, uint64_t n,
-                                                   uint32_t *__restrict__ ids, uint64_t cap, uint64_t stage_cap,
+                                                   T *__restrict__ ids, uint64_t cap, uint64_t stage_cap,
                                                    uint32_t mul, uint32_t add) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -116,13 +117,13 @@ __global__ __launch_bounds__(256) void k_tile_copy(const uint32_t *__restrict__ 
         const uint64_t oo = lane <= nr ? out_offs[r0 + lane] : 0ull;
         const uint64_t so = lane < nr ? (uint64_t)mul * offs[r0 + lane] + (uint64_t)add * (r0 + (uint64_t)lane) : 0ull;
         for (int j0 = 0; j0 < nr; j0 += COPY_B) {
-            uint32_t v[COPY_B];
+            T v[COPY_B];
 #pragma unroll
             for (int q = 0; q < COPY_B; ++q) {
                 const int j = j0 + q < nr ? j0 + q : nr - 1;
                 const uint64_t d0 = w_bcast(oo, j), d1 = w_bcast(oo, j + 1), s0 = w_bcast(so, j);
                 const uint64_t src = s0 + (uint64_t)lane;
-                v[q] = (j0 + q < nr && (uint64_t)lane < d1 - d0 && src < stage_cap) ? stage[src] : 0u;
+                v[q] = (j0 + q < nr && (uint64_t)lane < d1 - d0 && src < stage_cap) ? stage[src] : (T)0;
             }
 #pragma unroll
             for (int q = 0; q < COPY_B; ++q) {
@@ -267,12 +268,25 @@ int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st) {
     return AK_OK;
 }
 
+int ws_stage8_reserve(AkWs *w, uint64_t need, hipStream_t st) {
+    if (need <= w->cap_stage8) return AK_OK;
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t c = std::max<uint64_t>(need, w->cap_stage8 + w->cap_stage8 / 2);
+    (void)hipFree(w->stage8);
+    w->stage8 = nullptr;
+    w->cap_stage8 = 0;
+    HIP_TRY(hipMalloc(&w->stage8, c));
+    w->cap_stage8 = c;
+    return AK_OK;
+}
+
 int launch_stage_copy(AkWs *w, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, uint32_t *ids, uint64_t cap,
-                      uint32_t mul, uint32_t add, hipStream_t st) {
+                      uint32_t mul, uint32_t add, hipStream_t st, uint8_t *labels) {
     const uint64_t ngroups = (n + COPY_G - 1) / COPY_G;
     const unsigned cgrid = (unsigned)std::min<uint64_t>((ngroups + 3) / 4, (uint64_t)num_cus() * 8);
     AK_PROF(AK_PROF_COPY, false, st);
-    k_tile_copy<<<cgrid, 256, 0, st>>>(w->stage, offs, out_offs, n, ids, cap, w->cap_stage, mul, add);
+    k_tile_copy<uint32_t><<<cgrid, 256, 0, st>>>(w->stage, offs, out_offs, n, ids, cap, w->cap_stage, mul, add);
+    if (labels) k_tile_copy<uint8_t><<<cgrid, 256, 0, st>>>(w->stage8, offs, out_offs, n, labels, cap, w->cap_stage8, mul, add);
     AK_PROF(AK_PROF_COPY, true, st);
     HIP_TRY(hipGetLastError());
     return AK_OK;
