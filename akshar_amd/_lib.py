@@ -41,6 +41,7 @@ SIGNATURES = {
     "ak_normalize": (I32, [P, I32, P, P, U64, P, U64, P, P, P]),
     "ak_segment": (I32, [P, I32, I32, P, P, U64, P, U64, P, P, P]),
     "ak_switches": (I32, [P, I32, P, P, U64, P, P, U64, P, P, P]),
+    "ak_analyze": (I32, [P, I32, I32, P, P, U64, P, U64, P, P, U64, P, P, P, U64, P, P, P]),
     "ak_bpe_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
     "ak_spm_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
     "ak_profile_enable": (I32, [I32]),

@@ -301,6 +301,8 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->slow_count);
     (void)hipFree(w->block_sums);
     (void)hipFree(w->pool_mem);
+    (void)hipFree(w->stage8);
+    (void)hipFree(w->acounts);
     delete w;
 }
 
@@ -394,15 +396,16 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const uint32_t *c, ui
     if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = sums[nb];
 }
 
-int ak::scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st) {
+int ak::scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st, const uint32_t *counts) {
+    if (!counts) counts = w->counts;
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 0) {
         HIP_TRY(hipMemsetAsync(out_offs, 0, 8, st));
         return AK_OK;
     }
-    k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, st>>>(w->counts, n, w->block_sums);
+    k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, st>>>(counts, n, w->block_sums);
     k_scan_sums<<<1, SCAN_BLOCK, 0, st>>>(w->block_sums, nb);
-    k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, st>>>(w->counts, n, w->block_sums, nb, out_offs);
+    k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, st>>>(counts, n, w->block_sums, nb, out_offs);
     HIP_TRY(hipGetLastError());
     return AK_OK;
 }
@@ -509,6 +512,20 @@ extern "C" int ak_spm_encode(const ak_spm *m, ak_ws *w, int flags, const uint8_t
     RowArgs a = make_args(in, offs, n, ids, cap, row_status);
     a.spm = m->dev;
     return dispatch(OP_SPM, flags, w, a, out_offs, (hipStream_t)stream);
+}
+
+extern "C" int ak_analyze(ak_ws *w, int flags, int matras, const uint8_t *in, const uint64_t *offs, uint64_t n,
+                          uint8_t *norm, uint64_t norm_cap, uint64_t *norm_offs, uint32_t *clusters, uint64_t cl_cap,
+                          uint64_t *cl_offs, uint32_t *runs, uint8_t *labels, uint64_t run_cap, uint64_t *run_offs,
+                          uint8_t *row_status, void *stream) {
+    int rc = check_common(w, in, offs, n, norm, norm_offs);
+    if (rc) return rc;
+    if (!cl_offs || !run_offs || (n && (!clusters || !runs || !labels))) return fail(AK_ERR_ARG, "ak_analyze: null buffer");
+    if (flags < 0 || flags > 3) return fail(AK_ERR_ARG, "ak_analyze: flags must be 0..3");
+    RowArgs a = make_args(in, offs, n, nullptr, 0, row_status);
+    a.matras = matras;
+    AnalyzeOut o{norm, norm_cap, norm_offs, clusters, cl_cap, cl_offs, runs, labels, run_cap, run_offs};
+    return launch_analyze(flags, w, a, o, (hipStream_t)stream);
 }
 
 extern "C" uint64_t ak_normalize_cap(uint64_t n, uint64_t total_bytes) { return 3 * total_bytes + 16 + 0 * n; }

@@ -44,6 +44,8 @@ struct AkWs {
     uint64_t cap_stage = 0;
     uint8_t *stage8 = nullptr;      // staged run labels (switches), same slots as stage
     uint64_t cap_stage8 = 0;
+    uint32_t *acounts = nullptr;    // analyze: cluster and run counts per row (2 n)
+    uint64_t cap_acounts = 0;
     uint32_t *tile_misc = nullptr;  // [0] fallback-list length, [1] slot-overflow flag, [2] second list length
     uint32_t *fb2 = nullptr;        // second fallback list (rows past the fast buffers)
     uint64_t cap_fb2 = 0;
@@ -63,7 +65,10 @@ int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st);
 int ws_stage8_reserve(AkWs *w, uint64_t need, hipStream_t st);
 int launch_stage_copy(AkWs *w, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, uint32_t *ids, uint64_t cap,
                       uint32_t mul, uint32_t add, hipStream_t st, uint8_t *labels = nullptr);
-int scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st);
+int scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st, const uint32_t *counts = nullptr);
+template <class T>
+int copy_staged(const T *stage, uint64_t stage_cap, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, T *out,
+                uint64_t cap, uint32_t mul, uint32_t add, hipStream_t st);
 int num_cus();
 
 __device__ __forceinline__ void stage_tables(uint2 *fast, uint16_t *sfast, const uint16_t *g_single, bool bpe) {
@@ -319,6 +324,13 @@ int launch_switches(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hi
 int launch_bpe(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_spm(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+
+struct AnalyzeOut {
+    uint8_t *norm; uint64_t norm_cap; uint64_t *norm_offs;
+    uint32_t *clusters; uint64_t cl_cap; uint64_t *cl_offs;
+    uint32_t *runs; uint8_t *labels; uint64_t run_cap; uint64_t *run_offs;
+};
+int launch_analyze(int flags, AkWs *w, const RowArgs &a, const AnalyzeOut &o, hipStream_t st);
 
 }  // namespace ak
 

@@ -280,6 +280,20 @@ int ws_stage8_reserve(AkWs *w, uint64_t need, hipStream_t st) {
     return AK_OK;
 }
 
+template <class T>
+int copy_staged(const T *stage, uint64_t stage_cap, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, T *out,
+                uint64_t cap, uint32_t mul, uint32_t add, hipStream_t st) {
+    const uint64_t ngroups = (n + COPY_G - 1) / COPY_G;
+    const unsigned cgrid = (unsigned)std::min<uint64_t>((ngroups + 3) / 4, (uint64_t)num_cus() * 8);
+    k_tile_copy<T><<<cgrid, 256, 0, st>>>(stage, offs, out_offs, n, out, cap, stage_cap, mul, add);
+    HIP_TRY(hipGetLastError());
+    return AK_OK;
+}
+template int copy_staged<uint8_t>(const uint8_t *, uint64_t, const uint64_t *, const uint64_t *, uint64_t, uint8_t *,
+                                  uint64_t, uint32_t, uint32_t, hipStream_t);
+template int copy_staged<uint32_t>(const uint32_t *, uint64_t, const uint64_t *, const uint64_t *, uint64_t, uint32_t *,
+                                   uint64_t, uint32_t, uint32_t, hipStream_t);
+
 int launch_stage_copy(AkWs *w, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, uint32_t *ids, uint64_t cap,
                       uint32_t mul, uint32_t add, hipStream_t st, uint8_t *labels) {
     const uint64_t ngroups = (n + COPY_G - 1) / COPY_G;

@@ -152,6 +152,34 @@ def switches_batch(buf, offs, flags=3, row_status=None):
     return ends[:total], labels[:total], oo
 
 
+def analyze_batch(buf, offs, flags=3, matras=False, row_status=None):
+    """explain()'s front half in one fused pass (include/akshar.h ak_analyze): returns
+    (norm u8, norm_offs, cluster ends i32, cl_offs, run ends i32, run labels u8, run_offs); cluster
+    and run ends index the NORMALIZED row's code points, as segment_akshars(norm) /
+    detect_code_switches(norm)."""
+    n = _check_inputs(buf, offs)
+    dev = buf.device
+    ws = workspace(dev.index)
+    nbytes = int(offs[-1].item()) if n else 0
+    L = _lib.lib()
+    caps = [nbytes + 64 if flags & AK_NORM_CLEAN else int(L.ak_normalize_cap(n, nbytes)),
+            int(L.ak_segment_cap(n, nbytes)), int(L.ak_segment_cap(n, nbytes))]
+    oo = [torch.empty(n + 1, dtype=torch.int64, device=dev) for _ in range(3)]
+    for _ in range(2):
+        norm = torch.empty(max(caps[0], 1), dtype=torch.uint8, device=dev)
+        cl = torch.empty(max(caps[1], 1), dtype=torch.int32, device=dev)
+        runs = torch.empty(max(caps[2], 1), dtype=torch.int32, device=dev)
+        labels = torch.empty(max(caps[2], 1), dtype=torch.uint8, device=dev)
+        check(L.ak_analyze(ws, flags, int(bool(matras)), _ptr(buf), _ptr(offs), n, _ptr(norm), caps[0], _ptr(oo[0]),
+                           _ptr(cl), caps[1], _ptr(oo[1]), _ptr(runs), _ptr(labels), caps[2], _ptr(oo[2]),
+                           _ptr(row_status), _stream(dev)), "ak_analyze")
+        tot = [int(o[-1].item()) for o in oo]
+        if all(t <= c for t, c in zip(tot, caps)):
+            break
+        caps = [max(t, c) for t, c in zip(tot, caps)]
+    return norm[:tot[0]], oo[0], cl[:tot[1]], oo[1], runs[:tot[2]], labels[:tot[2]], oo[2]
+
+
 import os as _os
 
 # 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (v1); AK_BPE_PATH overrides

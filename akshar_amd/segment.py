@@ -88,6 +88,25 @@ def segment_by_script(text):
     return [seg for seg, _ in detect_code_switches(text)]
 
 
+def analyze_batch(texts, flags=3, matras=False):
+    """explain()'s front half for many texts in ONE fused GPU pass (engine.analyze_batch,
+    include/akshar.h ak_analyze): per text (normalize_text(text), cluster END indices of the
+    normalized text, [(run end, label)] of the normalized text)."""
+    if not texts:
+        return [], [], []
+    buf, offs = engine.pack(texts)
+    norm, no, cl, co, runs, labels, ro = engine.analyze_batch(buf, offs, flags=flags, matras=matras)
+    raw = norm.cpu().numpy().tobytes()
+    no, cl, co = no.cpu().numpy(), cl.cpu().numpy(), co.cpu().numpy()
+    runs, labels, ro = runs.cpu().numpy(), labels.cpu().numpy(), ro.cpu().numpy()
+    norms, ends, rls = [], [], []
+    for i in range(len(texts)):
+        norms.append(raw[no[i]:no[i + 1]].decode("utf-8", "surrogatepass"))
+        ends.append([int(x) for x in cl[co[i]:co[i + 1]]])
+        rls.append([(int(e), _LABEL[int(lb)]) for e, lb in zip(runs[ro[i]:ro[i + 1]], labels[ro[i]:ro[i + 1]])])
+    return norms, ends, rls
+
+
 def composition_from(text, n_akshars, runs):
     """analyze_text_composition's arithmetic (segment.py:225-236) from cluster count + runs."""
     total = len(text)

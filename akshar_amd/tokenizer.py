@@ -15,7 +15,7 @@ from typing import List, Optional, Union
 from . import decode as _dec
 from . import engine
 from .normalize import normalize_batch
-from .segment import _split, composition_from, segment_batch, switches_batch
+from .segment import _split, analyze_batch, composition_from, segment_batch
 
 
 class aksharTokenizer:
@@ -90,14 +90,18 @@ class aksharTokenizer:
         return _dec.bpe_tokens(self.model.model, ids)
 
     def tokenize_batch(self, texts: List[str], return_metadata: bool = False):
-        norms = self.preprocess_batch(texts)
+        if not return_metadata:
+            if self.model is None:
+                norms = self.preprocess_batch(texts)
+                return [_split(n, e) for n, e in zip(norms, segment_batch(norms))]
+            return [self._tokens_for(ids) for ids in self.encode_batch(texts)]
+        # normalize + segment + script runs of every text in one fused pass (ak_analyze)
+        norms, ends, runs = analyze_batch(texts, self._flags)
         if self.model is None:
-            toks = [_split(n, e) for n, e in zip(norms, segment_batch(norms))]
+            toks = [_split(n, e) for n, e in zip(norms, ends)]
         else:
             toks = [self._tokens_for(ids) for ids in self.encode_batch(texts)]
-        if not return_metadata:
-            return toks
-        metas = [self._composition(n) for n in norms]
+        metas = [composition_from(n, len(e), r) for n, e, r in zip(norms, ends, runs)]
         out = []
         for text, norm, meta, t in zip(texts, norms, metas, toks):
             meta = dict(meta)
@@ -125,15 +129,8 @@ class aksharTokenizer:
         return "".join(tokens)
 
     # ---------------------------------------------------------------- analysis
-    @staticmethod
-    def _composition(norm):
-        n = len(segment_batch([norm])[0])
-        return composition_from(norm, n, switches_batch([norm])[0])
-
     def explain(self, text: str) -> dict:
-        norm = self.preprocess(text)
-        ends = segment_batch([norm])[0]
-        runs = switches_batch([norm])[0]
+        (norm,), (ends,), (runs,) = analyze_batch([text], self._flags)  # one fused pass
         akshars = _split(norm, ends)
         switches = list(zip(_split(norm, [e for e, _ in runs]), [lab for _, lab in runs]))
         stats = composition_from(norm, len(ends), runs)

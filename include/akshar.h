@@ -108,6 +108,17 @@ int ak_segment(ak_ws *ws, int flags, int matras, const uint8_t *in, const uint64
 int ak_switches(ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n, uint32_t *ends,
                 uint8_t *labels, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
 
+/* The front half of aksharTokenizer.explain(text) / tokenize(text, return_metadata=True)
+ * (tokenizer.py:248-276, :146-147; segment.py:210-236), fused into ONE pass per row:
+ * norm = normalize_text(text, flags) as UTF-8 (like ak_normalize), and on that normalized text
+ * segment_akshars(norm, matras) cluster ENDs (like ak_segment with AK_RAW on norm) and
+ * detect_code_switches(norm) run ENDs + labels (like ak_switches with AK_RAW on norm).
+ * Three outputs, each with its own capacity and u64[n+1] offsets ([n] = required total). */
+int ak_analyze(ak_ws *ws, int flags, int matras, const uint8_t *in, const uint64_t *offs, uint64_t n,
+               uint8_t *norm, uint64_t norm_cap, uint64_t *norm_offs, uint32_t *clusters, uint64_t cl_cap,
+               uint64_t *cl_offs, uint32_t *runs, uint8_t *labels, uint64_t run_cap, uint64_t *run_offs,
+               uint8_t *row_status, void *stream);
+
 /* aksharTokenizer(model, "bpe").encode(text) (tokenizer.py:167-193): normalize_text(flags) then
  * the HF pipeline; ids include <s> ... </s>. flags must include AK_NORM_CLEAN. */
 int ak_bpe_encode(const ak_bpe *m, ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,

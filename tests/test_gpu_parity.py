@@ -175,3 +175,46 @@ def test_tile_path_fallback_accounting(eng, bpe_model):
     ref, ro = O.OracleBPE(bpe_model).encode_batch(b2, offs2.astype(np.uint64))
     assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
     assert _cpu(st).tolist()[-1] == 1
+
+
+@pytest.mark.parametrize("matras,key", [(False, "ak"), (True, "ak_m")])
+def test_analyze_fused_golden(golden, gpacked, eng, matras, key):
+    """ak_analyze (one fused pass: normalize -> segment + switches of the normalized text) against
+    the golden norm / ak / sw fields (explain(): tokenizer.py:262-264)."""
+    norm, no, cl, co, runs, labels, ro = eng.analyze_batch(*gpacked, flags=3, matras=matras)
+    assert _bad(golden, "norm", rows_u8(_cpu(norm), _cpu(no))) == []
+    assert _bad(golden, key, [ends_to_lens(e) for e in rows_ints(_cpu(cl), _cpu(co))]) == []
+    assert _bad(golden, "sw", rows_runs(_cpu(runs), _cpu(labels), _cpu(ro))) == []
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2])
+def test_analyze_fused_equals_single_ops(golden, gpacked, eng, flags):
+    """Every normalize flag combination: the fused outputs == the single ops chained (normalize,
+    then segment / switches of the normalized rows with AK_RAW)."""
+    norm, no, cl, co, runs, labels, ro = eng.analyze_batch(*gpacked, flags=flags)
+    n1, o1 = eng.normalize_batch(*gpacked, flags=flags)
+    assert torch.equal(no, o1) and torch.equal(norm, n1)
+    pad = torch.zeros(((norm.numel() + 15) // 16) * 16 + 16, dtype=torch.uint8, device=norm.device)
+    pad[:norm.numel()] = norm
+    e2, o2 = eng.segment_batch(pad, o1, flags=eng.AK_RAW)
+    assert torch.equal(co, o2) and torch.equal(cl, e2)
+    e3, l3, o3 = eng.switches_batch(pad, o1, flags=eng.AK_RAW)
+    assert torch.equal(ro, o3) and torch.equal(runs, e3) and torch.equal(labels, l3)
+
+
+def test_analyze_synthetic_and_empty(eng):
+    from akshar_amd import synth
+    buf, offs = synth.generate(synth.KIND_HINGLISH, 20000, seed=77)
+    texts = [bytes(buf[offs[i]:offs[i + 1]]).decode("utf-8") for i in range(len(offs) - 1)]
+    texts[5] = ""
+    texts[6] = "!!! ... 123"
+    gb, go = eng.pack(texts)
+    norm, no, cl, co, runs, labels, ro = eng.analyze_batch(gb, go)
+    n1, o1 = eng.normalize_batch(gb, go)
+    assert torch.equal(norm, n1)
+    e2, o2 = eng.segment_batch(gb, go)
+    assert torch.equal(co, o2) and torch.equal(cl, e2)
+    e3, l3, o3 = eng.switches_batch(gb, go)
+    assert torch.equal(ro, o3) and torch.equal(runs, e3) and torch.equal(labels, l3)
+    z = eng.analyze_batch(*eng.pack([]))
+    assert all(int(t.numel()) == 0 for t in (z[0], z[2], z[4])) and int(z[1][-1]) == 0
