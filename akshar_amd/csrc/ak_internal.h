@@ -198,7 +198,7 @@ inline int launch_rows(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_t st) {
 }
 
 
-// ---- single-pass staged rows (SPM, segment, switches): the row pipeline runs ONCE, straight into a per-row staging
+// ---- single-pass staged rows (normalize, segment, switches, SPM): the row pipeline runs ONCE, straight into a per-row staging
 // slot of the workspace (row r owns [mul*offs[r] + add*r, mul*offs[r+1] + add*(r+1)): mul / add
 // bound the op's output per raw byte / per row), then counts -> offsets and one coalesced copy.
 // Halves the work of count -> scan -> emit for ops whose per-row cost is the pipeline itself.
@@ -281,18 +281,20 @@ inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_
     HIP_TRY(hipMemcpyAsync(&nbytes, a.offs + a.n, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const uint64_t need = (uint64_t)mul * nbytes + (uint64_t)add * a.n + 64;
-    rc = ws_stage_reserve(w, need, st);
-    if (rc) return rc;
+    if (OP != OP_NORMALIZE) {
+        rc = ws_stage_reserve(w, need, st);
+        if (rc) return rc;
+    }
     uint8_t *labels = a.labels;
-    if (labels) {
+    if (labels || OP == OP_NORMALIZE) {  // u8 outputs (run labels, normalized bytes) stage in stage8
         rc = ws_stage8_reserve(w, need, st);
         if (rc) return rc;
-        a.labels = w->stage8;
+        a.labels = labels ? w->stage8 : nullptr;
     }
-    uint32_t *ids = (uint32_t *)a.out;
+    void *out = a.out;
     const uint64_t cap = a.cap;
-    a.out = w->stage;
-    a.cap = w->cap_stage;
+    a.out = OP == OP_NORMALIZE ? (void *)w->stage8 : (void *)w->stage;
+    a.cap = OP == OP_NORMALIZE ? w->cap_stage8 : w->cap_stage;
     a.counts = w->counts;
     a.flags = w->flags;
     a.slow_list = w->slow_list;
@@ -313,7 +315,13 @@ inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_
     rc = scan_counts(w, a.n, out_offs, st);
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
-    return launch_stage_copy(w, a.offs, out_offs, a.n, ids, cap, mul, add, st, labels);
+    if constexpr (OP == OP_NORMALIZE) {
+        AK_PROF(AK_PROF_COPY, false, st);
+        rc = copy_staged<uint8_t>(w->stage8, w->cap_stage8, a.offs, out_offs, a.n, (uint8_t *)out, cap, mul, add, st);
+        AK_PROF(AK_PROF_COPY, true, st);
+        return rc;
+    }
+    return launch_stage_copy(w, a.offs, out_offs, a.n, (uint32_t *)out, cap, mul, add, st, labels);
 }
 
 

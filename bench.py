@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 METRIC = "MB of raw UTF-8 tokenized/sec @1 GPU (+ tokens/s); bit-exact vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SEED = 1234
-TRAFFIC_FILE = "r01_v6_tiles_pmc.json"  # PMC HBM bytes of the tile kernel at the default config
+TRAFFIC_FILE = "r01_v7_tiles_pmc.json"  # PMC HBM bytes of the tile kernel at the default config
 
 
 def parse():
