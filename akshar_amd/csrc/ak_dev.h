@@ -79,6 +79,8 @@ struct Scratch {
     int seg_cap;
     uint16_t *wsym;   // BPE word symbols
     uint32_t *wpair;  // BPE pair (rank << 16 | new id)
+    uint64_t *heap;   // BPE heap merge of long words (3 x word_cap), null in the fast kernels
+    int32_t *link;    // ... its prev / next symbol links (2 x word_cap)
     int word_cap;
     uint32_t *vchar;  // SPM word chars
     float *vbest;     // SPM best score per position
@@ -533,6 +535,77 @@ __device__ __forceinline__ int bpe_merge_word(const BpeDev &m, uint16_t *w, uint
     return n;
 }
 
+// HF tokenizers Word::merge_all for long words: a binary min-heap of (rank << 32 | left position)
+// with lazy invalidation (an entry is applied only if its pair still exists at that position with
+// the same rank), symbols linked by prev / next. Pops lowest rank, leftmost on ties: the same
+// merges, in the same order, as bpe_merge_word, in O(n log n). heap: 3n entries (n - 1 initial
+// pairs + 2 per merge, one popped per merge); link: 2n. Returns the symbol count (compacted in w).
+constexpr int HEAP_MERGE_MIN = 48;  // words at least this long take the heap merge when a heap exists
+
+__device__ __forceinline__ void heap_push(uint64_t *h, int &n, uint64_t v) {
+    int i = n++;
+    while (i > 0) {
+        const int p = (i - 1) >> 1;
+        if (h[p] <= v) break;
+        h[i] = h[p];
+        i = p;
+    }
+    h[i] = v;
+}
+
+__device__ __forceinline__ uint64_t heap_pop(uint64_t *h, int &n) {
+    const uint64_t top = h[0];
+    const uint64_t last = h[--n];
+    int i = 0;
+    for (;;) {
+        int c = 2 * i + 1;
+        if (c >= n) break;
+        if (c + 1 < n && h[c + 1] < h[c]) ++c;
+        if (h[c] >= last) break;
+        h[i] = h[c];
+        i = c;
+    }
+    if (n > 0) h[i] = last;
+    return top;
+}
+
+__device__ __noinline__ int bpe_merge_heap(const BpeDev &m, uint16_t *w, uint64_t *heap, int32_t *link, int n) {
+    int32_t *prv = link, *nxt = link + n;
+    int hn = 0;
+    for (int i = 0; i < n; ++i) { prv[i] = i - 1; nxt[i] = i + 1 < n ? i + 1 : -1; }
+    for (int i = 0; i + 1 < n; ++i) {
+        const uint32_t v = merge_lookup(m, w[i], w[i + 1]);
+        if (v != 0xFFFFFFFFu) heap_push(heap, hn, ((uint64_t)(v >> 16) << 32) | (uint32_t)i);
+    }
+    while (hn > 0) {
+        const uint64_t top = heap_pop(heap, hn);
+        const int pos = (int)(uint32_t)top;
+        const uint32_t rank = (uint32_t)(top >> 32);
+        if (prv[pos] == -2) continue;  // merged away
+        const int j = nxt[pos];
+        if (j < 0) continue;
+        const uint32_t v = merge_lookup(m, w[pos], w[j]);
+        if (v == 0xFFFFFFFFu || (v >> 16) != rank) continue;  // stale entry
+        w[pos] = (uint16_t)(v & 0xFFFFu);
+        prv[j] = -2;
+        const int k = nxt[j];
+        nxt[pos] = k;
+        if (k >= 0) prv[k] = pos;
+        const int p = prv[pos];
+        if (p >= 0) {
+            const uint32_t u = merge_lookup(m, w[p], w[pos]);
+            if (u != 0xFFFFFFFFu) heap_push(heap, hn, ((uint64_t)(u >> 16) << 32) | (uint32_t)p);
+        }
+        if (k >= 0) {
+            const uint32_t u = merge_lookup(m, w[pos], w[k]);
+            if (u != 0xFFFFFFFFu) heap_push(heap, hn, ((uint64_t)(u >> 16) << 32) | (uint32_t)pos);
+        }
+    }
+    int c = 0;
+    for (int i = 0; i >= 0; i = nxt[i]) w[c++] = w[i];
+    return c;
+}
+
 struct BpeWordSink {  // after HF NFC: pre-tokenize and merge
     Cursor<uint32_t> c;
     const BpeDev *m;
@@ -557,7 +630,8 @@ struct BpeWordSink {  // after HF NFC: pre-tokenize and merge
     }
     __device__ __forceinline__ void end_word() {
         if (cls >= 0 && wlen > 0) {
-            const int k = bpe_merge_word(*m, sc->wsym, sc->wpair, wlen);
+            const int k = (sc->heap && wlen >= HEAP_MERGE_MIN) ? bpe_merge_heap(*m, sc->wsym, sc->heap, sc->link, wlen)
+                                                                : bpe_merge_word(*m, sc->wsym, sc->wpair, wlen);
             for (int i = 0; i < k; ++i) c.put((uint32_t)sc->wsym[i]);
         }
         cls = -1;

@@ -1,15 +1,19 @@
 // ak_engine.hip — kernels and C-ABI (include/akshar.h) of the MI355X tokenization engine.
 //
-// Execution plan of every batch call (one HIP stream, no host synchronization):
-//   1. count   (fast kernel)  one lane per row runs the fused row pipeline (ak_dev.h) and only
-//                              counts its outputs; rows whose fast-path buffers overflow are
-//                              appended to a slow list.
-//   2. count   (slow kernel)  the slow list, with large per-thread buffers in a global pool.
-//   3. scan                    u32 row counts -> u64 row offsets (out_offs[n] = total).
-//   4. emit    (fast + slow)   the same pipelines again, writing at the scanned offsets.
+// Execution plan of every row-op batch call (one HIP stream):
+//   1. stage   (fast kernel)  one lane per row runs the fused row pipeline (ak_dev.h) ONCE, straight
+//                              into the row's staging slot (a worst-case bound per raw byte); rows
+//                              whose small buffers overflow are appended to the slow list
+//                              (the BPE bench path runs the tile-cooperative kernel here instead).
+//   2. slow tier               the slow list with per-thread pool regions of SLOW_CAP entries;
+//                              rows past those go to the huge list.
+//   3. huge tier (rare)        one host read-back; if the huge list is not empty, a pool sized from
+//                              its longest row re-runs it: every row is exact at any length.
+//   4. scan                    u32 row counts -> u64 row offsets (out_offs[n] = total).
+//   5. copy                    staged slots -> the packed output, one wave per 32 rows.
 // Property tables for U+0000..U+09FF and the BPE single-char ids are staged in LDS per block;
-// the BPE merge table (open addressing, 8 B entries) and the SPM double-array trie stay in
-// HBM and are served from L2.
+// the BPE merge table (cuckoo, 4 / 8 B entries) and the SPM double-array trie stay in HBM and are
+// served from L2.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -227,21 +231,11 @@ extern "C" void ak_spm_free(ak_spm *m) {
 extern "C" int ak_ws_create(ak_ws **out) {
     if (!out) return fail(AK_ERR_ARG, "ak_ws_create: null");
     ak_ws *w = new ak_ws();
-    HIP_TRY(hipMalloc(&w->slow_count, 64));
-    const size_t T = SLOW_THREADS;
-    const size_t bytes = T * (2 * SLOW_SEG * 4 + 8 * SLOW_SEG * 4 + SLOW_WORD * 2 + SLOW_WORD * 4 + SLOW_WORD * 4 +
-                              3 * (SLOW_WORD + 1) * 4) + 4096;
+    HIP_TRY(hipMalloc(&w->ctr, 64));
+    HIP_TRY(hipMemset(w->ctr, 0, 64));
+    const uint64_t bytes = pool_thread_bytes(SLOW_CAP) * SLOW_THREADS;
     HIP_TRY(hipMalloc(&w->pool_mem, bytes));
-    char *p = (char *)w->pool_mem;
-    auto take = [&](size_t b) { char *r = p; p += (b + 255) & ~(size_t)255; return (void *)r; };
-    w->pool.seg = (uint32_t *)take(T * 2 * SLOW_SEG * 4);
-    w->pool.dec = (uint32_t *)take(T * 8 * SLOW_SEG * 4);
-    w->pool.wsym = (uint16_t *)take(T * SLOW_WORD * 2);
-    w->pool.wpair = (uint32_t *)take(T * SLOW_WORD * 4);
-    w->pool.vchar = (uint32_t *)take(T * SLOW_WORD * 4);
-    w->pool.vbest = (float *)take(T * (SLOW_WORD + 1) * 4);
-    w->pool.vstart = (int32_t *)take(T * (SLOW_WORD + 1) * 4);
-    w->pool.vid = (int32_t *)take(T * (SLOW_WORD + 1) * 4);
+    w->pool = pool_carve(w->pool_mem, SLOW_CAP, SLOW_THREADS);
     *out = w;
     return AK_OK;
 }
@@ -256,8 +250,10 @@ extern "C" int ak_ws_set_tiling(ak_ws *w, int bpe_path, int tile_rows) {
 
 extern "C" int ak_ws_check(ak_ws *w) {
     if (!w) return fail(AK_ERR_ARG, "null workspace");
-    if (!w->tile_misc) return AK_OK;
     uint32_t err = 0;
+    HIP_TRY(hipMemcpy(&err, w->ctr + CTR_ERR, 4, hipMemcpyDeviceToHost));
+    if (err) return fail(AK_ERR_HIP, "internal: a row overflowed its staging slot or the huge tier (engine bug)");
+    if (!w->tile_misc) return AK_OK;
     HIP_TRY(hipMemcpy(&err, w->tile_misc + 1, 4, hipMemcpyDeviceToHost));
     return err ? fail(AK_ERR_HIP, "tile staging slot overflow (a row produced more ids than bytes + 2)") : AK_OK;
 }
@@ -296,11 +292,12 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->tile_passprof);
     (void)hipFree(w->fb2);
     (void)hipFree(w->counts);
-    (void)hipFree(w->flags);
     (void)hipFree(w->slow_list);
-    (void)hipFree(w->slow_count);
+    (void)hipFree(w->huge_list);
+    (void)hipFree(w->ctr);
     (void)hipFree(w->block_sums);
     (void)hipFree(w->pool_mem);
+    (void)hipFree(w->huge_mem);
     (void)hipFree(w->stage8);
     (void)hipFree(w->acounts);
     delete w;
@@ -310,12 +307,12 @@ int ak::ws_reserve(AkWs *w, uint64_t n) {
     if (n > w->cap_rows) {
         uint64_t c = std::max<uint64_t>(n, 2 * w->cap_rows);
         (void)hipFree(w->counts);
-        (void)hipFree(w->flags);
         (void)hipFree(w->slow_list);
-        w->counts = nullptr; w->flags = nullptr; w->slow_list = nullptr;
+        (void)hipFree(w->huge_list);
+        w->counts = nullptr; w->slow_list = nullptr; w->huge_list = nullptr;
         HIP_TRY(hipMalloc(&w->counts, c * 4));
-        HIP_TRY(hipMalloc(&w->flags, c));
         HIP_TRY(hipMalloc(&w->slow_list, c * 4));
+        HIP_TRY(hipMalloc(&w->huge_list, c * 4));
         w->cap_rows = c;
     }
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE + 1;
@@ -327,6 +324,69 @@ int ak::ws_reserve(AkWs *w, uint64_t n) {
         w->cap_blocks = c;
     }
     return AK_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// huge tier (ak_internal.h run_huge_tier)
+
+__global__ void k_list_maxlen(const uint32_t *list, const uint32_t *count, const uint64_t *offs, uint32_t *out) {
+    const uint32_t n = *count;
+    uint32_t m = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t r = list[i];
+        const uint64_t len = offs[r + 1] - offs[r];
+        m = std::max<uint32_t>(m, (uint32_t)std::min<uint64_t>(len, 0xFFFFFFFFull));
+    }
+    if (m) atomicMax(out, m);
+}
+
+int ak::huge_prepare(AkWs *w, const uint64_t *offs, hipStream_t st, Tier *t, unsigned *blocks) {
+    *blocks = 0;
+    uint32_t h[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(h, w->ctr + CTR_HUGE, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (h[0] == 0) return AK_OK;
+    HIP_TRY(hipMemsetAsync(w->ctr + CTR_N, 0, 4, st));
+    k_list_maxlen<<<64, 256, 0, st>>>(w->huge_list, w->ctr + CTR_HUGE, offs, w->ctr + CTR_N);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(h + 1, w->ctr + CTR_N, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    // every buffer of a row's pipeline holds <= 3 code points per raw byte (NFC at most triples a
+    // char's UTF-8, each code point is >= 1 byte), + the SPM dummy prefix / BPE sentinels
+    const uint64_t cap = 3ull * h[1] + 64;
+    if (cap > 0x7FFFFFFFull) return fail(AK_ERR_NOMEM, "huge tier: a row of more than 700 MB (split it at spaces first)");
+    const uint64_t per = pool_thread_bytes(cap);
+    uint64_t threads = std::min<uint64_t>(h[0], SLOW_THREADS);
+    while (threads > 1 && threads * per > HUGE_POOL_BUDGET) threads = (threads + 1) / 2;
+    const uint64_t bytes = threads * per;
+    if (bytes > w->huge_bytes) {
+        (void)hipFree(w->huge_mem);
+        w->huge_mem = nullptr;
+        w->huge_bytes = 0;
+        if (hipMalloc(&w->huge_mem, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            char msg[160];
+            snprintf(msg, sizeof(msg), "huge tier: cannot allocate %llu bytes for a %u-byte row",
+                     (unsigned long long)bytes, h[1]);
+            return fail(AK_ERR_NOMEM, msg);
+        }
+        w->huge_bytes = bytes;
+    }
+    t->list = w->huge_list;
+    t->count = w->ctr + CTR_HUGE;
+    t->pool = pool_carve(w->huge_mem, cap, (uint32_t)threads);
+    t->next_list = nullptr;
+    t->next_count = nullptr;
+    t->err = w->ctr + CTR_ERR;
+    *blocks = (unsigned)((threads + 63) / 64);
+    return AK_OK;
+}
+
+int ak::huge_check(AkWs *w, hipStream_t st) {
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, w->ctr + CTR_ERR, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return err ? fail(AK_ERR_HIP, "internal: a row overflowed the huge tier (engine bug)") : AK_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -432,7 +492,8 @@ static int dispatch(int op, int flags, ak_ws *w, const RowArgs &a, uint64_t *out
         case OP_SEGMENT: return launch_segment(flags, w, a, out_offs, st);
         case OP_SWITCHES: return launch_switches(flags, w, a, out_offs, st);
         case OP_BPE:
-            return w->bpe_path == 1 && flags == 3 ? launch_bpe_tiles(flags, w, a, out_offs, st) : launch_bpe(flags, w, a, out_offs, st);
+            return w->bpe_path == 1 && flags == 3 ? launch_bpe_tiles(flags, w, a, out_offs, st)
+                                                  : launch_bpe(flags, w, a, out_offs, st);
         default: return launch_spm(flags, w, a, out_offs, st);
     }
 }

@@ -1,6 +1,6 @@
 // ak_internal.h — engine internals shared by the C-ABI TU (ak_engine.hip) and the per-op kernel
-// TUs (ak_k_*.hip, compiled in parallel): workspace layout, error plumbing, the row kernels and
-// the count -> scan -> emit launcher.
+// TUs (ak_k_*.hip, compiled in parallel): workspace layout, error plumbing, the staged row
+// kernels with their slow / huge tiers, and their launcher.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -29,16 +29,22 @@ constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 8;
 constexpr uint64_t SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 
+// device counters of one launch (AkWs::ctr), zeroed by every launcher
+enum { CTR_SLOW = 0, CTR_HUGE = 1, CTR_ERR = 2, CTR_N = 4 };
+constexpr uint64_t HUGE_POOL_BUDGET = 4ull << 30;  // bytes the huge tier may use for parallel rows
+
 struct AkWs {
     uint64_t cap_rows = 0;
     uint32_t *counts = nullptr;
-    uint8_t *flags = nullptr;
-    uint32_t *slow_list = nullptr;
-    uint32_t *slow_count = nullptr;
+    uint32_t *slow_list = nullptr;  // rows for the slow tier (n entries)
+    uint32_t *huge_list = nullptr;  // rows for the huge tier (n entries)
+    uint32_t *ctr = nullptr;        // CTR_N launch counters + scratch for huge_prepare
     uint64_t *block_sums = nullptr;
     uint64_t cap_blocks = 0;
     void *pool_mem = nullptr;
     SlowPool pool{};
+    void *huge_mem = nullptr;       // huge-tier pool, grown on demand
+    uint64_t huge_bytes = 0;
     // tile-cooperative BPE path
     uint32_t *stage = nullptr;      // staged ids, slot of row r at offs[r] + 2 r
     uint64_t cap_stage = 0;
@@ -51,7 +57,7 @@ struct AkWs {
     uint64_t cap_fb2 = 0;
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 8;
-    int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (v1)
+    int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)
 };
 
 // built-in kernel timing (include/akshar.h ak_profile_*): HIP events around every launch
@@ -79,14 +85,41 @@ __device__ __forceinline__ void stage_tables(uint2 *fast, uint16_t *sfast, const
     __syncthreads();
 }
 
-template <int OP, int FLAGS, bool EMIT>
-__global__ __launch_bounds__(ROW_BLOCK) void k_rows_fast(RowArgs a) {
+// ---- tiered row lists: a fast kernel appends the rows that overflow its small buffers to the
+// slow list; the slow tier (pool regions of SLOW_CAP entries) appends the rows that overflow
+// those to the huge list; the huge tier re-runs them with regions sized from the longest such row
+// (huge_prepare), so every row is exact at any length. An overflow in the last tier would be an
+// engine bug: it sets the workspace error flag (ak_ws_check), it is never a silent empty row.
+struct Tier {
+    const uint32_t *list;   // rows of this tier
+    const uint32_t *count;  // its length (device)
+    SlowPool pool;
+    uint32_t *next_list;    // rows overflowing this tier (null in the last tier)
+    uint32_t *next_count;
+    uint32_t *err;          // set when the last tier overflows
+};
+
+__device__ __forceinline__ void tier_overflow(const Tier &t, const RowArgs &a, uint64_t r, uint32_t *counts) {
+    if (t.next_list) {
+        t.next_list[atomicAdd(t.next_count, 1u)] = (uint32_t)r;
+        return;
+    }
+    counts[r] = 0;
+    if (a.row_status) a.row_status[r] = (uint8_t)ST_LIMIT;
+    __hip_atomic_store(t.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- single-pass staged rows (normalize, segment, switches, BPE row path, SPM): the row pipeline
+// runs ONCE, straight into a per-row staging slot of the workspace (row r owns [mul*offs[r] +
+// add*r, mul*offs[r+1] + add*(r+1)): mul / add bound the op's output per raw byte / per row), then
+// counts -> offsets and one coalesced copy.
+template <int OP, int FLAGS>
+__global__ __launch_bounds__(ROW_BLOCK) void k_rows_stage(RowArgs a, uint32_t mul, uint32_t add) {
     __shared__ uint2 fast[FAST_N];
     __shared__ uint16_t sfast[OP == OP_BPE ? FAST_N : 1];
     __shared__ uint16_t wsym[OP == OP_BPE ? ROW_BLOCK * FAST_WORD : 1];
     __shared__ uint32_t wpair[OP == OP_BPE ? ROW_BLOCK * FAST_WORD : 1];
     stage_tables(fast, sfast, a.single_fast, OP == OP_BPE);
-
     uint32_t seg[FAST_SEG], seg2[FAST_SEG];
     uint32_t dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
     uint32_t vchar[OP == OP_SPM ? FAST_VCAP : 1];
@@ -94,130 +127,15 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_rows_fast(RowArgs a) {
     int32_t vstart[OP == OP_SPM ? FAST_VCAP + 1 : 1];
     int32_t vid[OP == OP_SPM ? FAST_VCAP + 1 : 1];
     Scratch sc;
-    sc.seg = seg;
-    sc.dec = dec;
-    sc.seg2 = seg2;
-    sc.dec2 = dec2;
-    sc.seg_cap = FAST_SEG;
-    sc.wsym = wsym + (OP == OP_BPE ? threadIdx.x * FAST_WORD : 0);
-    sc.wpair = wpair + (OP == OP_BPE ? threadIdx.x * FAST_WORD : 0);
-    sc.word_cap = FAST_WORD;
-    sc.vchar = vchar;
-    sc.vbest = vbest;
-    sc.vstart = vstart;
-    sc.vid = vid;
-    sc.vcap = FAST_VCAP;
-    sc.slow_status = ST_SLOW;
-
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
-        if (EMIT && a.flags[r] != 0) continue;
-        sc.status = 0;
-        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc, EMIT ? a.out_offs[r] : 0);
-        if (!EMIT) {
-            const bool slow = (sc.status & ST_SLOW) != 0;
-            a.counts[r] = slow ? 0u : (uint32_t)cnt;
-            a.flags[r] = slow ? 1 : 0;
-            if (slow) a.slow_list[atomicAdd(a.slow_count, 1u)] = (uint32_t)r;
-            if (a.row_status) a.row_status[r] = (uint8_t)(sc.status & ST_BAD_UTF8);
-        }
+    small_scratch(sc, seg, seg2, dec, dec2, FAST_SEG);
+    if constexpr (OP == OP_BPE) {
+        sc.wsym = wsym + threadIdx.x * FAST_WORD;
+        sc.wpair = wpair + threadIdx.x * FAST_WORD;
+        sc.word_cap = FAST_WORD;
     }
-}
-
-template <int OP, int FLAGS, bool EMIT>
-__global__ __launch_bounds__(64) void k_rows_slow(RowArgs a) {
-    __shared__ uint2 fast[FAST_N];
-    __shared__ uint16_t sfast[OP == OP_BPE ? FAST_N : 1];
-    stage_tables(fast, sfast, a.single_fast, OP == OP_BPE);
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < SLOW_THREADS
-    Scratch sc;
-    sc.seg = a.pool.seg + t * 2 * SLOW_SEG;
-    sc.dec = a.pool.dec + t * 8 * SLOW_SEG;
-    sc.seg2 = sc.seg + SLOW_SEG;
-    sc.dec2 = sc.dec + 4 * SLOW_SEG;
-    sc.seg_cap = SLOW_SEG;
-    sc.wsym = a.pool.wsym + t * SLOW_WORD;
-    sc.wpair = a.pool.wpair + t * SLOW_WORD;
-    sc.word_cap = SLOW_WORD;
-    sc.vchar = a.pool.vchar + t * SLOW_WORD;
-    sc.vbest = a.pool.vbest + t * (SLOW_WORD + 1);
-    sc.vstart = a.pool.vstart + t * (SLOW_WORD + 1);
-    sc.vid = a.pool.vid + t * (SLOW_WORD + 1);
-    sc.vcap = SLOW_WORD;
-    sc.slow_status = ST_LIMIT;
-    const uint32_t ns = *a.slow_count;
-    for (uint32_t i = (uint32_t)t; i < ns; i += SLOW_THREADS) {
-        const uint64_t r = a.slow_list[i];
-        if (EMIT && a.flags[r] != 1) continue;
-        sc.status = 0;
-        const uint64_t cnt = process_row<OP, FLAGS, EMIT>(a, r, fast, sfast, &sc, EMIT ? a.out_offs[r] : 0);
-        if (!EMIT) {
-            const bool lim = (sc.status & ST_LIMIT) != 0;
-            a.counts[r] = lim ? 0u : (uint32_t)cnt;
-            if (lim) a.flags[r] = 2;
-            if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0u));
-        }
+    if constexpr (OP == OP_SPM) {
+        sc.vchar = vchar; sc.vbest = vbest; sc.vstart = vstart; sc.vid = vid; sc.vcap = FAST_VCAP;
     }
-}
-
-template <int OP, int FLAGS>
-inline int launch_rows(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_t st) {
-    if (a.n == 0) {
-        HIP_TRY(hipMemsetAsync(out_offs, 0, 8, st));
-        return AK_OK;
-    }
-    int rc = ws_reserve(w, a.n);
-    if (rc) return rc;
-    a.counts = w->counts;
-    a.flags = w->flags;
-    a.slow_list = w->slow_list;
-    a.slow_count = w->slow_count;
-    a.pool = w->pool;
-    a.out_offs = out_offs;
-    const uint64_t want = (a.n + ROW_BLOCK - 1) / ROW_BLOCK;
-    const unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)num_cus() * 8);
-    HIP_TRY(hipMemsetAsync(w->slow_count, 0, 4, st));
-    AK_PROF(AK_PROF_COUNT, false, st);
-    k_rows_fast<OP, FLAGS, false><<<grid, ROW_BLOCK, 0, st>>>(a);
-    AK_PROF(AK_PROF_COUNT, true, st);
-    AK_PROF(AK_PROF_COUNT_SLOW, false, st);
-    k_rows_slow<OP, FLAGS, false><<<SLOW_THREADS / 64, 64, 0, st>>>(a);
-    AK_PROF(AK_PROF_COUNT_SLOW, true, st);
-    AK_PROF(AK_PROF_SCAN, false, st);
-    rc = scan_counts(w, a.n, out_offs, st);
-    if (rc) return rc;
-    AK_PROF(AK_PROF_SCAN, true, st);
-    AK_PROF(AK_PROF_EMIT, false, st);
-    k_rows_fast<OP, FLAGS, true><<<grid, ROW_BLOCK, 0, st>>>(a);
-    AK_PROF(AK_PROF_EMIT, true, st);
-    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    k_rows_slow<OP, FLAGS, true><<<SLOW_THREADS / 64, 64, 0, st>>>(a);
-    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
-    HIP_TRY(hipGetLastError());
-    return AK_OK;
-}
-
-
-// ---- single-pass staged rows (normalize, segment, switches, SPM): the row pipeline runs ONCE, straight into a per-row staging
-// slot of the workspace (row r owns [mul*offs[r] + add*r, mul*offs[r+1] + add*(r+1)): mul / add
-// bound the op's output per raw byte / per row), then counts -> offsets and one coalesced copy.
-// Halves the work of count -> scan -> emit for ops whose per-row cost is the pipeline itself.
-template <int OP, int FLAGS>
-__global__ __launch_bounds__(ROW_BLOCK) void k_rows_stage(RowArgs a, uint32_t mul, uint32_t add) {
-    __shared__ uint2 fast[FAST_N];
-    __shared__ uint16_t sfast[1];
-    stage_tables(fast, sfast, nullptr, false);
-    uint32_t seg[FAST_SEG], seg2[FAST_SEG];
-    uint32_t dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
-    uint32_t vchar[OP == OP_SPM ? FAST_VCAP : 1];
-    float vbest[OP == OP_SPM ? FAST_VCAP + 1 : 1];
-    int32_t vstart[OP == OP_SPM ? FAST_VCAP + 1 : 1];
-    int32_t vid[OP == OP_SPM ? FAST_VCAP + 1 : 1];
-    Scratch sc;
-    sc.seg = seg; sc.dec = dec; sc.seg2 = seg2; sc.dec2 = dec2; sc.seg_cap = FAST_SEG;
-    sc.wsym = nullptr; sc.wpair = nullptr; sc.word_cap = 0;
-    sc.vchar = vchar; sc.vbest = vbest; sc.vstart = vstart; sc.vid = vid; sc.vcap = FAST_VCAP;
-    sc.slow_status = ST_SLOW;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
         sc.status = 0;
@@ -228,45 +146,62 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_rows_stage(RowArgs a, uint32_t mu
             a.slow_list[atomicAdd(a.slow_count, 1u)] = (uint32_t)r;
             continue;
         }
-        const bool over = cnt > s1 - s0;  // cannot happen (mul / add are worst-case bounds): reported, not hidden
+        const bool over = cnt > s1 - s0;  // cannot happen (mul / add are worst-case bounds): flagged, not hidden
+        if (over) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         a.counts[r] = over ? 0u : (uint32_t)cnt;
         if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (over ? ST_LIMIT : 0u));
     }
 }
 
+// one tier of pool rows (slow or huge): one lane per listed row, pool regions as scratch
 template <int OP, int FLAGS>
-__global__ __launch_bounds__(64) void k_rows_stage_slow(RowArgs a, uint32_t mul, uint32_t add) {
+__global__ __launch_bounds__(64) void k_rows_tier(RowArgs a, uint32_t mul, uint32_t add, Tier t) {
     __shared__ uint2 fast[FAST_N];
-    __shared__ uint16_t sfast[1];
-    const uint32_t ns = *a.slow_count;
+    __shared__ uint16_t sfast[OP == OP_BPE ? FAST_N : 1];
+    const uint32_t ns = *t.count;
     if (ns == 0) return;  // uniform: the common case
-    stage_tables(fast, sfast, nullptr, false);
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < SLOW_THREADS
+    stage_tables(fast, sfast, a.single_fast, OP == OP_BPE);
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= t.pool.threads) return;
     Scratch sc;
-    sc.seg = a.pool.seg + t * 2 * SLOW_SEG;
-    sc.dec = a.pool.dec + t * 8 * SLOW_SEG;
-    sc.seg2 = sc.seg + SLOW_SEG;
-    sc.dec2 = sc.dec + 4 * SLOW_SEG;
-    sc.seg_cap = SLOW_SEG;
-    sc.wsym = a.pool.wsym + t * SLOW_WORD;
-    sc.wpair = a.pool.wpair + t * SLOW_WORD;
-    sc.word_cap = SLOW_WORD;
-    sc.vchar = a.pool.vchar + t * SLOW_WORD;
-    sc.vbest = a.pool.vbest + t * (SLOW_WORD + 1);
-    sc.vstart = a.pool.vstart + t * (SLOW_WORD + 1);
-    sc.vid = a.pool.vid + t * (SLOW_WORD + 1);
-    sc.vcap = SLOW_WORD;
-    sc.slow_status = ST_LIMIT;
-    for (uint32_t i = (uint32_t)t; i < ns; i += SLOW_THREADS) {
-        const uint64_t r = a.slow_list[i];
+    pool_scratch(t.pool, tid, sc, ST_LIMIT);
+    for (uint64_t i = tid; i < ns; i += t.pool.threads) {
+        const uint64_t r = t.list[i];
         sc.status = 0;
         const uint64_t b = a.offs[r], e = a.offs[r + 1];
         const uint64_t s0 = mul * b + add * r, s1 = mul * e + add * (r + 1);
         const uint64_t cnt = process_row<OP, FLAGS, true>(a, r, fast, sfast, &sc, s0, s1);
-        const bool lim = (sc.status & ST_LIMIT) != 0 || cnt > s1 - s0;
-        a.counts[r] = lim ? 0u : (uint32_t)cnt;
-        if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0u));
+        if (sc.status & ST_LIMIT) {
+            tier_overflow(t, a, r, a.counts);
+            continue;
+        }
+        const bool over = cnt > s1 - s0;
+        if (over) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.counts[r] = over ? 0u : (uint32_t)cnt;
+        if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (over ? ST_LIMIT : 0u));
     }
+}
+
+// The slow tier of a launch (pool regions of SLOW_CAP entries), overflowing into the huge list.
+inline Tier slow_tier(AkWs *w, const uint32_t *list, const uint32_t *count) {
+    return Tier{list, count, w->pool, w->huge_list, w->ctr + CTR_HUGE, w->ctr + CTR_ERR};
+}
+
+// Huge tier: synchronizes, and if some rows overflowed the slow tier, sizes a pool from the longest
+// of them and returns its Tier with the number of 64-lane blocks to launch (0: nothing to do).
+int huge_prepare(AkWs *w, const uint64_t *offs, hipStream_t st, Tier *t, unsigned *blocks);
+// After a huge-tier launch: synchronizes and fails if that tier overflowed (an engine bug).
+int huge_check(AkWs *w, hipStream_t st);
+
+template <class Launch>
+inline int run_huge_tier(AkWs *w, const uint64_t *offs, hipStream_t st, Launch launch) {
+    Tier t;
+    unsigned blocks = 0;
+    int rc = huge_prepare(w, offs, st, &t, &blocks);
+    if (rc || blocks == 0) return rc;
+    launch(t, blocks);
+    HIP_TRY(hipGetLastError());
+    return huge_check(w, st);
 }
 
 template <int OP, int FLAGS>
@@ -296,21 +231,24 @@ inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_
     a.out = OP == OP_NORMALIZE ? (void *)w->stage8 : (void *)w->stage;
     a.cap = OP == OP_NORMALIZE ? w->cap_stage8 : w->cap_stage;
     a.counts = w->counts;
-    a.flags = w->flags;
     a.slow_list = w->slow_list;
-    a.slow_count = w->slow_count;
-    a.pool = w->pool;
+    a.slow_count = w->ctr + CTR_SLOW;
+    a.err = w->ctr + CTR_ERR;
     a.out_offs = nullptr;
     const uint64_t want = (a.n + ROW_BLOCK - 1) / ROW_BLOCK;
     const unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)num_cus() * 8);
-    HIP_TRY(hipMemsetAsync(w->slow_count, 0, 4, st));
+    HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     AK_PROF(AK_PROF_EMIT, false, st);
     k_rows_stage<OP, FLAGS><<<grid, ROW_BLOCK, 0, st>>>(a, mul, add);
     AK_PROF(AK_PROF_EMIT, true, st);
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    k_rows_stage_slow<OP, FLAGS><<<SLOW_THREADS / 64, 64, 0, st>>>(a, mul, add);
-    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
+    k_rows_tier<OP, FLAGS><<<SLOW_THREADS / 64, 64, 0, st>>>(a, mul, add, slow_tier(w, w->slow_list, w->ctr + CTR_SLOW));
     HIP_TRY(hipGetLastError());
+    rc = run_huge_tier(w, a.offs, st, [&](const Tier &t, unsigned blocks) {
+        k_rows_tier<OP, FLAGS><<<blocks, 64, 0, st>>>(a, mul, add, t);
+    });
+    if (rc) return rc;
+    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
     AK_PROF(AK_PROF_SCAN, false, st);
     rc = scan_counts(w, a.n, out_offs, st);
     if (rc) return rc;
@@ -324,6 +262,11 @@ inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_
     return launch_stage_copy(w, a.offs, out_offs, a.n, (uint32_t *)out, cap, mul, add, st, labels);
 }
 
+
+// BPE ids per row with clean_hinglish (flags 2, 3) <= raw bytes + 2: normalize_text then keeps
+// only allowlisted chars, each >= 1 byte and never more code points than bytes (the NFC
+// expansions of 0958-095F / 09DC-09DF are 2 code points of a 3-byte char), plus <s> and </s>.
+constexpr uint32_t BPE_MUL = 1, BPE_ADD = 2;
 
 // per-op launchers (one TU each)
 int launch_normalize(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);

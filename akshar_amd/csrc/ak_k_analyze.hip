@@ -46,7 +46,8 @@ __device__ __forceinline__ void analyze_row(const RowArgs &a, const AnalyzeArgs 
     run_normalized<FLAGS>(t, fast, sc, rd, b, e);
     if (sc->status & sc->slow_status) return;
     const uint64_t n0 = t.u.c.pos - s0, n1 = t.g.c.pos - s0, n2 = t.w.c.pos - s0;
-    const bool over = n0 > s1 - s0 || n1 > s1 - s0 || n2 > s1 - s0;  // cannot happen: reported, not hidden
+    const bool over = n0 > s1 - s0 || n1 > s1 - s0 || n2 > s1 - s0;  // cannot happen: flagged, not hidden
+    if (over) __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     x.cnt_norm[r] = over ? 0u : (uint32_t)n0;
     x.cnt_clus[r] = over ? 0u : (uint32_t)n1;
     x.cnt_runs[r] = over ? 0u : (uint32_t)n2;
@@ -60,10 +61,7 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_analyze(RowArgs a, AnalyzeArgs x)
     stage_tables(fast, sfast, nullptr, false);
     uint32_t seg[FAST_SEG], seg2[FAST_SEG], dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
     Scratch sc;
-    sc.seg = seg; sc.dec = dec; sc.seg2 = seg2; sc.dec2 = dec2; sc.seg_cap = FAST_SEG;
-    sc.wsym = nullptr; sc.wpair = nullptr; sc.word_cap = 0;
-    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
-    sc.slow_status = ST_SLOW;
+    small_scratch(sc, seg, seg2, dec, dec2, FAST_SEG);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < a.n; r += stride) {
         sc.status = 0;
@@ -72,30 +70,26 @@ __global__ __launch_bounds__(ROW_BLOCK) void k_analyze(RowArgs a, AnalyzeArgs x)
     }
 }
 
+// one tier of pool rows (slow or huge), as k_rows_tier
 template <int FLAGS>
-__global__ __launch_bounds__(64) void k_analyze_slow(RowArgs a, AnalyzeArgs x) {
+__global__ __launch_bounds__(64) void k_analyze_tier(RowArgs a, AnalyzeArgs x, Tier t) {
     __shared__ uint2 fast[FAST_N];
     __shared__ uint16_t sfast[1];
-    const uint32_t ns = *a.slow_count;
+    const uint32_t ns = *t.count;
     if (ns == 0) return;  // uniform: the common case
     stage_tables(fast, sfast, nullptr, false);
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < SLOW_THREADS
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= t.pool.threads) return;
     Scratch sc;
-    sc.seg = a.pool.seg + t * 2 * SLOW_SEG;
-    sc.dec = a.pool.dec + t * 8 * SLOW_SEG;
-    sc.seg2 = sc.seg + SLOW_SEG;
-    sc.dec2 = sc.dec + 4 * SLOW_SEG;
-    sc.seg_cap = SLOW_SEG;
-    sc.wsym = nullptr; sc.wpair = nullptr; sc.word_cap = 0;
-    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
-    sc.slow_status = ST_LIMIT;
-    for (uint32_t i = (uint32_t)t; i < ns; i += SLOW_THREADS) {
-        const uint64_t r = a.slow_list[i];
+    pool_scratch(t.pool, tid, sc, ST_LIMIT);
+    for (uint64_t i = tid; i < ns; i += t.pool.threads) {
+        const uint64_t r = t.list[i];
         sc.status = 0;
         analyze_row<FLAGS>(a, x, r, fast, &sc);
         if (sc.status & ST_LIMIT) {
-            x.cnt_norm[r] = 0; x.cnt_clus[r] = 0; x.cnt_runs[r] = 0;
-            if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | ST_LIMIT);
+            x.cnt_clus[r] = 0;
+            x.cnt_runs[r] = 0;
+            tier_overflow(t, a, r, x.cnt_norm);
         }
     }
 }
@@ -128,18 +122,22 @@ static int launch(AkWs *w, RowArgs a, const AnalyzeOut &o, hipStream_t st) {
     x.cnt_clus = w->acounts;
     x.cnt_runs = w->acounts + a.n;
     a.slow_list = w->slow_list;
-    a.slow_count = w->slow_count;
-    a.pool = w->pool;
+    a.slow_count = w->ctr + CTR_SLOW;
+    a.err = w->ctr + CTR_ERR;
     const uint64_t want = (a.n + ROW_BLOCK - 1) / ROW_BLOCK;
     const unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)num_cus() * 8);
-    HIP_TRY(hipMemsetAsync(w->slow_count, 0, 4, st));
+    HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     AK_PROF(AK_PROF_EMIT, false, st);
     k_analyze<FLAGS><<<grid, ROW_BLOCK, 0, st>>>(a, x);
     AK_PROF(AK_PROF_EMIT, true, st);
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    k_analyze_slow<FLAGS><<<SLOW_THREADS / 64, 64, 0, st>>>(a, x);
-    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
+    k_analyze_tier<FLAGS><<<SLOW_THREADS / 64, 64, 0, st>>>(a, x, slow_tier(w, w->slow_list, w->ctr + CTR_SLOW));
     HIP_TRY(hipGetLastError());
+    rc = run_huge_tier(w, a.offs, st, [&](const Tier &t, unsigned blocks) {
+        k_analyze_tier<FLAGS><<<blocks, 64, 0, st>>>(a, x, t);
+    });
+    if (rc) return rc;
+    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
     AK_PROF(AK_PROF_SCAN, false, st);
     if ((rc = scan_counts(w, a.n, o.norm_offs, st, x.cnt_norm))) return rc;
     if ((rc = scan_counts(w, a.n, o.cl_offs, st, x.cnt_clus))) return rc;

@@ -3,7 +3,8 @@
 //                    writes per-row token counts; rare rows go to a fallback list
 //   k_tile_fb        fallback rows, one lane per row (ak_rows.h process_row, small private
 //                    buffers), straight into the same slots; rows that overflow those buffers go on
-//   k_tile_fb_slow   ... to the large per-thread regions of the workspace pool
+//   k_rows_tier      ... to the slow tier (per-thread pool regions) and, past those, the huge
+//                    tier sized from the longest such row (ak_internal.h)
 //   scan_counts      per-row counts -> u64 row offsets (out_offs)
 //   k_tile_copy      staged ids -> ids[out_offs[r] ...]
 #include <stdio.h>
@@ -33,7 +34,8 @@ __global__ __launch_bounds__(TILE_BLOCK, 8) void k_bpe_tiles(TileArgs ta) {
                           gridDim.x * (TILE_BLOCK / 64));
 }
 
-// fallback rows, fast buffers (the v1 row kernel's sizes); writes ids at the row's slot
+// fallback rows, fast buffers (the row kernel's sizes); writes ids at the row's slot. Rows that
+// overflow those buffers go on to the slow / huge tiers (k_rows_tier, the same slots).
 template <int FLAGS>
 __global__ __launch_bounds__(FB_BLOCK) void k_tile_fb(TileArgs ta) {
     __shared__ uint2 fast[FAST_N];
@@ -45,12 +47,10 @@ __global__ __launch_bounds__(FB_BLOCK) void k_tile_fb(TileArgs ta) {
     stage_tables(fast, sfast, ta.ra.single_fast, true);
     uint32_t seg[FAST_SEG], seg2[FAST_SEG], dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
     Scratch sc;
-    sc.seg = seg; sc.dec = dec; sc.seg2 = seg2; sc.dec2 = dec2; sc.seg_cap = FAST_SEG;
+    small_scratch(sc, seg, seg2, dec, dec2, FAST_SEG);
     sc.wsym = wsym + threadIdx.x * FAST_WORD;
     sc.wpair = wpair + threadIdx.x * FAST_WORD;
     sc.word_cap = FAST_WORD;
-    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
-    sc.slow_status = ST_SLOW;
     const RowArgs &a = ta.ra;
     for (uint32_t i = blockIdx.x * FB_BLOCK + threadIdx.x; i < nl; i += gridDim.x * FB_BLOCK) {
         const uint64_t r = ta.fb_list[i];
@@ -62,37 +62,6 @@ __global__ __launch_bounds__(FB_BLOCK) void k_tile_fb(TileArgs ta) {
         }
         ta.counts[r] = (uint32_t)cnt;
         if (a.row_status) a.row_status[r] = (uint8_t)(sc.status & ST_BAD_UTF8);
-    }
-}
-
-// fallback rows past the fast buffers: one large pool region per thread (AK_LIMIT_* sizes)
-template <int FLAGS>
-__global__ __launch_bounds__(64) void k_tile_fb_slow(TileArgs ta) {
-    __shared__ uint2 fast[FAST_N];
-    __shared__ uint16_t sfast[FAST_N];
-    const uint32_t nl = *ta.fb2_count;
-    if (nl == 0) return;
-    stage_tables(fast, sfast, ta.ra.single_fast, true);
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < SLOW_THREADS
-    const RowArgs &a = ta.ra;
-    Scratch sc;
-    sc.seg = a.pool.seg + t * 2 * SLOW_SEG;
-    sc.dec = a.pool.dec + t * 8 * SLOW_SEG;
-    sc.seg2 = sc.seg + SLOW_SEG;
-    sc.dec2 = sc.dec + 4 * SLOW_SEG;
-    sc.seg_cap = SLOW_SEG;
-    sc.wsym = a.pool.wsym + t * SLOW_WORD;
-    sc.wpair = a.pool.wpair + t * SLOW_WORD;
-    sc.word_cap = SLOW_WORD;
-    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
-    sc.slow_status = ST_LIMIT;
-    for (uint32_t i = (uint32_t)t; i < nl; i += SLOW_THREADS) {
-        const uint64_t r = ta.fb2_list[i];
-        sc.status = 0;
-        const uint64_t cnt = process_row<OP_BPE, FLAGS, true>(a, r, fast, sfast, &sc, a.offs[r] + 2 * r);
-        const bool lim = (sc.status & ST_LIMIT) != 0;
-        ta.counts[r] = lim ? 0u : (uint32_t)cnt;
-        if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0u));
     }
 }
 
@@ -215,7 +184,6 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     ta.ra.out = w->stage;
     ta.ra.cap = w->cap_stage;
     ta.ra.out_offs = nullptr;
-    ta.ra.pool = w->pool;
     ta.counts = w->counts;
     ta.fb_list = w->slow_list;              // n entries (ws_reserve)
     ta.fb_count = w->tile_misc;
@@ -233,6 +201,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     ta.fb2_list = w->fb2;
     HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
     HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
+    HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit
     int bpc = g_tile_blocks_per_cu;
@@ -243,12 +212,20 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     k_bpe_tiles<3><<<grid, TILE_BLOCK, 0, st>>>(ta);
     AK_PROF(AK_PROF_TILES, true, st);
     HIP_TRY(hipGetLastError());
-    // fallback rows: the full row pipeline (exact NFC, HF-NFC, any UTF-8) into the same slots
+    // fallback rows: the full row pipeline (exact NFC, HF-NFC, any UTF-8) into the same slots, then
+    // the slow and huge tiers for rows past its buffers
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
     k_tile_fb<3><<<(unsigned)num_cus(), FB_BLOCK, 0, st>>>(ta);
-    k_tile_fb_slow<3><<<SLOW_THREADS / 64, 64, 0, st>>>(ta);
-    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
+    RowArgs ra = ta.ra;
+    ra.counts = w->counts;
+    ra.err = w->ctr + CTR_ERR;
+    k_rows_tier<OP_BPE, 3><<<SLOW_THREADS / 64, 64, 0, st>>>(ra, BPE_MUL, BPE_ADD, slow_tier(w, w->fb2, ta.fb2_count));
     HIP_TRY(hipGetLastError());
+    rc = run_huge_tier(w, a0.offs, st, [&](const Tier &t, unsigned blocks) {
+        k_rows_tier<OP_BPE, 3><<<blocks, 64, 0, st>>>(ra, BPE_MUL, BPE_ADD, t);
+    });
+    if (rc) return rc;
+    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
     AK_PROF(AK_PROF_SCAN, false, st);
     rc = scan_counts(w, a0.n, out_offs, st);
     if (rc) return rc;

@@ -1,24 +1,98 @@
 // ak_rows.h — per-row drivers shared by the kernels (ak_engine.hip) and the host emulation
 // harness (tests/emu): which pipeline each op runs, and how a row's outputs are counted/written.
 #pragma once
+#include "akshar.h"
 #include "ak_dev.h"
 
 namespace ak {
 
+// Three tiers per row (include/akshar.h "Row lengths"): the fast kernels' small private buffers,
+// the slow tier's per-thread pool regions of SLOW_CAP entries, and the huge tier whose pool is
+// sized from the longest row that overflowed the slow tier (every row is exact at any length).
 constexpr int SLOW_THREADS = 256;
-constexpr int SLOW_SEG = 4096;   // AK_LIMIT_SEGMENT
-constexpr int SLOW_WORD = 4096;  // AK_LIMIT_WORD
+constexpr uint32_t SLOW_CAP = 4096;  // AK_SLOW_TIER_ENTRIES
+constexpr int SLOW_SEG = (int)SLOW_CAP;
+constexpr int SLOW_WORD = (int)SLOW_CAP;
+static_assert(SLOW_CAP == AK_SLOW_TIER_ENTRIES, "ak_rows.h vs include/akshar.h");
 
-struct SlowPool {  // per-thread regions, [thread][...]
-    uint32_t *seg;     // SLOW_SEG
-    uint32_t *dec;     // 4 * SLOW_SEG
-    uint16_t *wsym;    // SLOW_WORD
-    uint32_t *wpair;   // SLOW_WORD
-    uint32_t *vchar;   // SLOW_WORD
-    float *vbest;      // SLOW_WORD + 1
-    int32_t *vstart;   // SLOW_WORD + 1
-    int32_t *vid;      // SLOW_WORD + 1
+// Per-thread regions, [thread][...], every buffer sized from one capacity `cap` (code points /
+// symbols): seg + seg2 (2 cap), dec + dec2 (8 cap), BPE word (cap u16 + cap u32), heap merge
+// (3 cap u64 + 2 cap i32), SPM word (cap u32 + 3 (cap + 1) x 4 B).
+struct SlowPool {
+    uint32_t *seg;
+    uint32_t *dec;
+    uint16_t *wsym;
+    uint32_t *wpair;
+    uint64_t *heap;
+    int32_t *link;
+    uint32_t *vchar;
+    float *vbest;
+    int32_t *vstart;
+    int32_t *vid;
+    uint32_t cap;
+    uint32_t threads;
 };
+
+// bytes of one thread's regions for capacity cap (each region rounded to 256 B)
+inline uint64_t pool_thread_bytes(uint64_t cap) {
+    auto r = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
+    return r(2 * cap * 4) + r(8 * cap * 4) + r(cap * 2) + r(cap * 4) + r(3 * cap * 8) + r(2 * cap * 4) + r(cap * 4) +
+           3 * r((cap + 1) * 4);
+}
+
+// carve `threads` regions of capacity `cap` out of mem (pool_thread_bytes(cap) * threads bytes)
+inline SlowPool pool_carve(void *mem, uint64_t cap, uint32_t threads) {
+    auto r = [](uint64_t b) { return (b + 255) & ~(uint64_t)255; };
+    char *p = (char *)mem;
+    auto take = [&](uint64_t per) { char *q = p; p += r(per) * threads; return (void *)q; };
+    SlowPool s;
+    s.seg = (uint32_t *)take(2 * cap * 4);
+    s.dec = (uint32_t *)take(8 * cap * 4);
+    s.wsym = (uint16_t *)take(cap * 2);
+    s.wpair = (uint32_t *)take(cap * 4);
+    s.heap = (uint64_t *)take(3 * cap * 8);
+    s.link = (int32_t *)take(2 * cap * 4);
+    s.vchar = (uint32_t *)take(cap * 4);
+    s.vbest = (float *)take((cap + 1) * 4);
+    s.vstart = (int32_t *)take((cap + 1) * 4);
+    s.vid = (int32_t *)take((cap + 1) * 4);
+    s.cap = (uint32_t)cap;
+    s.threads = threads;
+    return s;
+}
+
+// thread t's slice of a pool as a Scratch (region i of a buffer = base + t * round256(size) / elem)
+__device__ __forceinline__ void pool_scratch(const SlowPool &p, uint64_t t, Scratch &sc, uint32_t slow_status) {
+    const uint64_t c = p.cap;
+    auto off = [&](uint64_t bytes, uint64_t elem) { return t * (((bytes + 255) & ~(uint64_t)255) / elem); };
+    sc.seg = p.seg + off(2 * c * 4, 4);
+    sc.seg2 = sc.seg + c;
+    sc.dec = p.dec + off(8 * c * 4, 4);
+    sc.dec2 = sc.dec + 4 * c;
+    sc.seg_cap = (int)c;
+    sc.wsym = p.wsym + off(c * 2, 2);
+    sc.wpair = p.wpair + off(c * 4, 4);
+    sc.heap = p.heap + off(3 * c * 8, 8);
+    sc.link = p.link + off(2 * c * 4, 4);
+    sc.word_cap = (int)c;
+    sc.vchar = p.vchar + off(c * 4, 4);
+    sc.vbest = p.vbest + off((c + 1) * 4, 4);
+    sc.vstart = p.vstart + off((c + 1) * 4, 4);
+    sc.vid = p.vid + off((c + 1) * 4, 4);
+    sc.vcap = (int)c;
+    sc.slow_status = slow_status;
+    sc.status = 0;
+}
+
+// fast-kernel scratch: small private / LDS buffers, no heap merge
+__device__ __forceinline__ void small_scratch(Scratch &sc, uint32_t *seg, uint32_t *seg2, uint32_t *dec, uint32_t *dec2,
+                                              int seg_cap) {
+    sc.seg = seg; sc.seg2 = seg2; sc.dec = dec; sc.dec2 = dec2; sc.seg_cap = seg_cap;
+    sc.wsym = nullptr; sc.wpair = nullptr; sc.heap = nullptr; sc.link = nullptr; sc.word_cap = 0;
+    sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
+    sc.slow_status = ST_SLOW;
+    sc.status = 0;
+}
 
 enum Op { OP_NORMALIZE = 0, OP_SEGMENT = 1, OP_SWITCHES = 2, OP_BPE = 3, OP_SPM = 4 };
 
@@ -27,9 +101,9 @@ struct RowArgs {
     const uint64_t *offs;
     uint64_t n;
     uint32_t *counts;
-    uint8_t *flags;        // 0 fast, 1 slow, 2 limit
     uint32_t *slow_list;
     uint32_t *slow_count;
+    uint32_t *err;         // set if a row's output overflowed its staging slot (never: worst-case bounds)
     const uint64_t *out_offs;
     void *out;
     uint8_t *labels;
@@ -39,7 +113,6 @@ struct RowArgs {
     BpeDev bpe;
     const uint16_t *single_fast;
     SpmDev spm;
-    SlowPool pool;
 };
 
 constexpr int ROW_BLOCK = 256;

@@ -10,7 +10,7 @@
 //   B  lane per pre-token: merge_all (lowest rank, leftmost on ties), in registers up to WREG-1
 //      symbols, in LDS beyond
 //   F  ids (B -> <s>, E -> </s>) into each row's staging slot, per-row token counts
-// Only the common case runs here (rows past the 1 KB tile buffer start the next sub-tile). A row
+// Only the common case runs here (rows past the 768-byte tile buffer start the next sub-tile). A row
 // whose NFC / HF-NFC quick check trips, with invalid UTF-8, or alone over the tile buffer is
 // appended to a fallback list and encoded by the row kernels of
 // ak_k_bpe_tiles.hip (ak_rows.h process_row), which write into the same per-row slot: the tile

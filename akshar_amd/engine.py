@@ -88,8 +88,10 @@ def _check_inputs(buf, offs):
     return n
 
 
-def _run(fn_call, n, cap, make_out, dev):
-    """Run a capacity-bounded op, re-running once with the exact size if needed."""
+def _run(fn_call, n, cap, make_out, dev, ws):
+    """Run a capacity-bounded op, re-running once with the exact size if needed. Every row is exact
+    at any length (include/akshar.h "Row lengths"); ak_ws_check turns an internal overflow into an
+    exception instead of a short row."""
     out_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     outs = make_out(cap)
     fn_call(outs, cap, out_offs)
@@ -99,6 +101,7 @@ def _run(fn_call, n, cap, make_out, dev):
         outs = make_out(cap)
         fn_call(outs, cap, out_offs)
         total = int(out_offs[-1].item())
+    check(_lib.lib().ak_ws_check(ws), "ak_ws_check")
     return outs, out_offs, total
 
 
@@ -113,7 +116,7 @@ def normalize_batch(buf, offs, flags=3, row_status=None):
         check(_lib.lib().ak_normalize(ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
                                       _ptr(row_status), _stream(dev)), "ak_normalize")
 
-    out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.uint8, device=dev), dev)
+    out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.uint8, device=dev), dev, ws)
     return out[:total], oo
 
 
@@ -129,7 +132,7 @@ def segment_batch(buf, offs, flags=3, matras=False, row_status=None):
         check(_lib.lib().ak_segment(ws, flags, int(bool(matras)), _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
                                     _ptr(row_status), _stream(dev)), "ak_segment")
 
-    out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev)
+    out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev, ws)
     return out[:total], oo
 
 
@@ -148,7 +151,7 @@ def switches_batch(buf, offs, flags=3, row_status=None):
         check(_lib.lib().ak_switches(ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out[0]), _ptr(out[1]), c, _ptr(oo),
                                      _ptr(row_status), _stream(dev)), "ak_switches")
 
-    (ends, labels), oo, total = _run(call, n, cap, make, dev)
+    (ends, labels), oo, total = _run(call, n, cap, make, dev, ws)
     return ends[:total], labels[:total], oo
 
 
@@ -174,6 +177,7 @@ def analyze_batch(buf, offs, flags=3, matras=False, row_status=None):
                            _ptr(cl), caps[1], _ptr(oo[1]), _ptr(runs), _ptr(labels), caps[2], _ptr(oo[2]),
                            _ptr(row_status), _stream(dev)), "ak_analyze")
         tot = [int(o[-1].item()) for o in oo]
+        check(L.ak_ws_check(ws), "ak_ws_check")
         if all(t <= c for t, c in zip(tot, caps)):
             break
         caps = [max(t, c) for t, c in zip(tot, caps)]
@@ -182,9 +186,9 @@ def analyze_batch(buf, offs, flags=3, matras=False, row_status=None):
 
 import os as _os
 
-# 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (v1); AK_BPE_PATH overrides
+# 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (staged row kernel); AK_BPE_PATH overrides
 BPE_PATH = int(_os.environ.get("AK_BPE_PATH", "1"))
-TILE_BYTES = 560  # target bytes of text per wave-tile (the tile buffer holds 1024)
+TILE_BYTES = 560  # target bytes of text per wave-tile (the tile buffer holds 768)
 
 
 def tile_rows_for(n, nbytes):
@@ -229,9 +233,7 @@ class BPE:
             check(_lib.lib().ak_bpe_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
                                            _ptr(row_status), _stream(dev)), "ak_bpe_encode")
 
-        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev)
-        if path == 1:
-            check(_lib.lib().ak_ws_check(ws), "ak_ws_check")
+        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev, ws)
         return out[:total], oo
 
 
@@ -267,7 +269,7 @@ class SPM:
             check(_lib.lib().ak_spm_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
                                            _ptr(row_status), _stream(dev)), "ak_spm_encode")
 
-        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev)
+        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev, ws)
         return out[:total], oo
 
 

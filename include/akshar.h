@@ -21,7 +21,14 @@
  *    elements are incomplete: re-run with cap >= out_offs[n] (the bound helpers below give caps
  *    that are always sufficient).
  *  - row_status (optional, u8[n], may be NULL): bit 0 = row had invalid UTF-8 (decoded as U+FFFD
- *    per byte), bit 2 = row exceeded an engine limit (AK_LIMIT_* below; its output is empty).
+ *    per byte). Bit 2 (AK_ROW_LIMIT) is only ever set together with an engine-bug error from
+ *    ak_ws_check(): no row length is rejected (see "Row lengths").
+ *  - Row lengths: there is no per-row limit. Rows run in up to three tiers: the fast kernels
+ *    (small private buffers), the slow tier (per-thread pool regions of AK_SLOW_TIER_ENTRIES code
+ *    points per NFC segment / symbols per BPE pre-token or SentencePiece word), and the huge tier,
+ *    whose pool is sized from the longest row past the slow tier (one extra host read-back; about
+ *    300 bytes of device memory per input byte of that row). A call whose huge tier cannot be
+ *    allocated fails with AK_ERR_NOMEM; it never returns a short or empty row.
  *  - Models and workspaces are not thread-safe for concurrent calls on different streams with the
  *    same workspace; models are immutable after creation and may be shared.
  */
@@ -51,9 +58,9 @@ extern "C" {
 #define AK_ROW_BAD_UTF8 1u
 #define AK_ROW_LIMIT 4u
 
-/* engine limits (a row exceeding one gets AK_ROW_LIMIT and an empty output) */
-#define AK_LIMIT_SEGMENT 16384 /* code points in one NFC segment (a starter + its combining marks) */
-#define AK_LIMIT_WORD 16384    /* symbols in one BPE pre-token / chars in one SentencePiece word */
+/* per-thread capacity of the slow tier (code points of one NFC segment, symbols of one BPE
+ * pre-token, chars of one SentencePiece word); longer ones run in the huge tier */
+#define AK_SLOW_TIER_ENTRIES 4096
 
 typedef struct ak_bpe ak_bpe; /* device-resident BPE model (HF tokenizers models.BPE) */
 typedef struct ak_spm ak_spm; /* device-resident SentencePiece unigram model */
@@ -68,11 +75,12 @@ int ak_selftest(void);
 int ak_ws_create(ak_ws **out);
 void ak_ws_free(ak_ws *ws);
 /* BPE kernel choice for this workspace: bpe_path 1 = tile-cooperative single pass (default;
- * tile_rows rows per wave-tile, 1..16, default 8 — pick ~1.1 KB of text per tile), 0 = one lane
- * per row (count/scan/emit). */
+ * tile_rows rows per wave-tile, 1..16, default 8 — pick ~560 B of text per tile; the tile buffer
+ * holds 768 B), 0 = one lane per row (the staged row kernel). */
 int ak_ws_set_tiling(ak_ws *ws, int bpe_path, int tile_rows);
-/* Synchronous health check after a batch: AK_ERR_HIP if the tile path flagged an internal
- * overflow (a row producing more ids than its bytes + 2; never observed). */
+/* Synchronous health check after a batch: AK_ERR_HIP if the last call flagged an internal
+ * overflow (a row producing more output than its staging slot bound, or overflowing the huge
+ * tier; never observed). */
 int ak_ws_check(ak_ws *ws);
 
 /* Replaces Tokenizer.from_file(path) (tokenizer.py:96-97) for the model cli.py:276-299 trains:
@@ -145,8 +153,8 @@ int ak_profile_read(int kernel, double *total_ms, uint64_t *launches);
 void ak_profile_reset(void);
 
 /* Rows of the last tile-path ak_bpe_encode on this workspace that took the sequential fallback
- * kernels (NFC / HF-NFC quick check tripped, invalid UTF-8, or past the 1 KB tile buffer), and how
- * many of those needed the large pool buffers. Synchronizes the device. */
+ * kernels (NFC / HF-NFC quick check tripped, invalid UTF-8, or past the 768-byte tile buffer), and
+ * how many of those needed the slow-tier pool buffers. Synchronizes the device. */
 int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
 
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each

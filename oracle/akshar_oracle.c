@@ -413,26 +413,39 @@ static const merge_t *merge_lookup(const or_bpe *m, uint32_t a, uint32_t b) {
     return NULL;
 }
 
+/* rank of the merge (a, b), or UINT32_MAX */
+static uint32_t pair_rank(const or_bpe *m, uint32_t a, uint32_t b) {
+    const merge_t *mg = merge_lookup(m, a, b);
+    return mg ? mg->rank : 0xFFFFFFFFu;
+}
+
+/* merge_all: repeatedly merge the lowest-rank adjacent pair, leftmost on ties. rk[i] caches the
+ * rank of the pair (sym[i], sym[i+1]); after a merge only the two pairs touching the new symbol
+ * change, so each round is one linear scan (64 KB words stay in seconds). */
 static void bpe_word(const or_bpe *m, const uint32_t *w, size_t n, vec_t *ids) {
-    vec_t sym = {0};
+    vec_t sym = {0}, rk = {0};
     for (size_t i = 0; i < n; ++i) {
         int64_t id = single_lookup(m, w[i]);
         if (id >= 0) vpush(&sym, (uint32_t)id);   /* unknown chars are dropped (unk_token None) */
     }
+    for (size_t i = 0; i + 1 < sym.n; ++i) vpush(&rk, pair_rank(m, sym.v[i], sym.v[i + 1]));
     for (;;) {
         size_t best = (size_t)-1;
-        uint32_t best_rank = 0xFFFFFFFFu, best_id = 0;
-        for (size_t i = 0; i + 1 < sym.n; ++i) {
-            const merge_t *mg = merge_lookup(m, sym.v[i], sym.v[i + 1]);
-            if (mg && mg->rank < best_rank) { best_rank = mg->rank; best = i; best_id = mg->new_id; }
-        }
+        uint32_t best_rank = 0xFFFFFFFFu;
+        for (size_t i = 0; i + 1 < sym.n; ++i)
+            if (rk.v[i] < best_rank) { best_rank = rk.v[i]; best = i; }
         if (best == (size_t)-1) break;
-        sym.v[best] = best_id;
+        sym.v[best] = merge_lookup(m, sym.v[best], sym.v[best + 1])->new_id;
         memmove(sym.v + best + 1, sym.v + best + 2, (sym.n - best - 2) * sizeof(uint32_t));
         sym.n--;
+        if (best + 1 < rk.n) memmove(rk.v + best + 1, rk.v + best + 2, (rk.n - best - 2) * sizeof(uint32_t));
+        rk.n--;
+        if (best > 0) rk.v[best - 1] = pair_rank(m, sym.v[best - 1], sym.v[best]);
+        if (best + 1 < sym.n) rk.v[best] = pair_rank(m, sym.v[best], sym.v[best + 1]);
     }
     for (size_t i = 0; i < sym.n; ++i) vpush(ids, sym.v[i]);
     vfree(&sym);
+    vfree(&rk);
 }
 
 enum { HF_W = 0, HF_P = 1, HF_S = 2 };

@@ -10,6 +10,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.jsonl.gz")
+GOLDEN_TIES = os.path.join(ROOT, "tests", "golden", "spm_ties.npz")
 BPE_PATH = os.path.join(ROOT, "models", "akshar.json")
 SPM_PATH = os.path.join(ROOT, "models", "akshar.model")
 

@@ -6,6 +6,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -67,16 +68,23 @@ template <int OP, int FLAGS>
 static int64_t run(RowArgs a) {
     static uint2 fast[FAST_N];
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
-    std::vector<uint32_t> seg(SLOW_SEG), dec(4 * SLOW_SEG), seg2(SLOW_SEG), dec2(4 * SLOW_SEG), wpair(SLOW_WORD), vchar(SLOW_WORD);
-    std::vector<uint16_t> wsym(SLOW_WORD);
-    std::vector<float> vbest(SLOW_WORD + 1);
-    std::vector<int32_t> vstart(SLOW_WORD + 1), vid(SLOW_WORD + 1);
+    // the slow scratch is sized like the huge tier (3 code points per input byte of the longest row)
+    uint64_t maxlen = 0;
+    for (uint64_t r = 0; r < a.n; ++r) maxlen = std::max<uint64_t>(maxlen, a.offs[r + 1] - a.offs[r]);
+    const uint64_t C = std::max<uint64_t>(SLOW_CAP, 3 * maxlen + 64);
+    std::vector<uint32_t> seg(C), dec(4 * C), seg2(C), dec2(4 * C), wpair(C), vchar(C);
+    std::vector<uint16_t> wsym(C);
+    std::vector<uint64_t> heap(3 * C);
+    std::vector<int32_t> link(2 * C);
+    std::vector<float> vbest(C + 1);
+    std::vector<int32_t> vstart(C + 1), vid(C + 1);
     auto scratch = [&](bool slow) {
         Scratch sc;
-        sc.seg = seg.data(); sc.dec = dec.data(); sc.seg2 = seg2.data(); sc.dec2 = dec2.data(); sc.seg_cap = slow ? SLOW_SEG : FAST_SEG;
-        sc.wsym = wsym.data(); sc.wpair = wpair.data(); sc.word_cap = slow ? SLOW_WORD : FAST_WORD;
+        sc.seg = seg.data(); sc.dec = dec.data(); sc.seg2 = seg2.data(); sc.dec2 = dec2.data(); sc.seg_cap = slow ? (int)C : FAST_SEG;
+        sc.wsym = wsym.data(); sc.wpair = wpair.data(); sc.word_cap = slow ? (int)C : FAST_WORD;
+        sc.heap = slow ? heap.data() : nullptr; sc.link = slow ? link.data() : nullptr;
         sc.vchar = vchar.data(); sc.vbest = vbest.data(); sc.vstart = vstart.data(); sc.vid = vid.data();
-        sc.vcap = slow ? SLOW_WORD : FAST_VCAP;
+        sc.vcap = slow ? (int)C : FAST_VCAP;
         sc.slow_status = slow ? ST_LIMIT : ST_SLOW;
         sc.status = 0;
         return sc;
@@ -189,13 +197,19 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     g_last_fb = fbn;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
     // fallback rows as k_tile_fb / k_tile_fb_slow: the row pipeline straight into the row's slot
-    std::vector<uint32_t> seg(2 * SLOW_SEG), dec(8 * SLOW_SEG), wpair(SLOW_WORD);
-    std::vector<uint16_t> wsym(SLOW_WORD);
+    uint64_t maxlen = 0;
+    for (uint64_t r = 0; r < n; ++r) maxlen = std::max<uint64_t>(maxlen, offs[r + 1] - offs[r]);
+    const uint64_t C = std::max<uint64_t>(SLOW_CAP, 3 * maxlen + 64);
+    std::vector<uint32_t> seg(2 * C), dec(8 * C), wpair(C);
+    std::vector<uint16_t> wsym(C);
+    std::vector<uint64_t> heap(3 * C);
+    std::vector<int32_t> link(2 * C);
     for (uint32_t i = 0; i < fbn; ++i) {
         const uint64_t r = fbl[i];
         Scratch sc;
-        sc.seg = seg.data(); sc.dec = dec.data(); sc.seg2 = seg.data() + SLOW_SEG; sc.dec2 = dec.data() + 4 * SLOW_SEG;
-        sc.seg_cap = SLOW_SEG; sc.wsym = wsym.data(); sc.wpair = wpair.data(); sc.word_cap = SLOW_WORD;
+        sc.seg = seg.data(); sc.dec = dec.data(); sc.seg2 = seg.data() + C; sc.dec2 = dec.data() + 4 * C;
+        sc.seg_cap = (int)C; sc.wsym = wsym.data(); sc.wpair = wpair.data(); sc.word_cap = (int)C;
+        sc.heap = heap.data(); sc.link = link.data();
         sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
         sc.slow_status = ST_LIMIT; sc.status = 0;
         const uint64_t cnt = process_row<OP_BPE, 3, true>(ta.ra, r, fast, m->bpe.fast.data(), &sc, offs[r] + 2 * r);

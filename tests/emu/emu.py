@@ -17,9 +17,10 @@ def lib():
         srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
                                                    ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h",
                                                     "ak_tile.h", "ak_wave.h")]
+        srcs.append(os.path.join(HERE, "..", "..", "include", "akshar.h"))
         if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
-            subprocess.check_call(["g++", "-O2", "-std=c++20", "-pthread", "-fPIC", "-shared", "-o", so, srcs[0]],
-                                  cwd=HERE)
+            subprocess.check_call(["g++", "-O2", "-std=c++20", "-pthread", "-fPIC", "-shared", "-I",
+                                   os.path.join(HERE, "..", "..", "include"), "-o", so, srcs[0]], cwd=HERE)
         L = ctypes.CDLL(so)
         L.emu_bpe_create.restype = P
         L.emu_bpe_create.argtypes = [ctypes.c_uint32, P, P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint32]

@@ -57,6 +57,14 @@ def test_host_decoders_match_golden(golden, bpe_model, spm_model):
         assert dec.spm_decode(spm_model, r["spm"]) == r["spm_dec"]
 
 
+def test_model_tokens_match_golden(golden, bpe_model, spm_model):
+    """tokenize() with a model (tokenizer.py:152-156): BPE enc.tokens / SPM EncodeAsPieces are the
+    id -> piece maps of the encode ids; pinned against the reference's recorded tokens."""
+    for r in golden:
+        assert dec.bpe_tokens(bpe_model, r["bpe"]) == r["bpe_tok"]
+        assert dec.spm_pieces(spm_model, r["spm"]) == r["spm_tok"]
+
+
 def test_vocab_sizes_from_files(bpe_model, spm_model):
     assert bpe_model.vocab_size == 24000 and spm_model.vocab_size == 24000
 
@@ -121,3 +129,33 @@ def test_public_api_on_golden(golden):
         assert bpe.encode(r["text"]) == r["bpe"]
         assert spm.decode(spm.encode(r["text"])) == r["spm_dec"]
         assert bpe.decode(r["bpe"]) == r["bpe_dec"]
+
+
+@gpu
+def test_model_tokenize_and_flag_variants_on_golden(golden):
+    """tokenize() with each model, and the constructor flags normalize_roman / clean_hinglish
+    (tokenizer.py:54-60) through encode(), against the reference's answers."""
+    texts = [r["text"] for r in golden]
+    bpe = aksharTokenizer(model_path=BPE_PATH, model_type="bpe")
+    spm = aksharTokenizer(model_path=SPM_PATH, model_type="sentencepiece")
+    assert bpe.tokenize_batch(texts) == [r["bpe_tok"] for r in golden]
+    assert spm.tokenize_batch(texts) == [r["spm_tok"] for r in golden]
+    for key, nr, ch in (("nolower", False, True), ("noclean", True, False), ("nfc", False, False)):
+        tk = aksharTokenizer(model_path=SPM_PATH, model_type="sentencepiece", normalize_roman=nr, clean_hinglish=ch)
+        assert tk.encode_batch(texts) == [r["spm_" + key] for r in golden], key
+    tk = aksharTokenizer(model_path=BPE_PATH, model_type="bpe", normalize_roman=False)
+    assert tk.encode_batch(texts) == [r["bpe_nolower"] for r in golden]
+
+
+@gpu
+def test_long_rows_through_the_public_api(golden):
+    """Rows past the engine's slow tier are exact ('ab' * 2500 -> 2,503 ids)."""
+    long = [r for r in golden if r["set"] == "long"]
+    bpe = aksharTokenizer(model_path=BPE_PATH, model_type="bpe")
+    spm = aksharTokenizer(model_path=SPM_PATH, model_type="sentencepiece")
+    assert len(bpe.encode("ab" * 2500)) == 2503
+    for r in long:
+        assert bpe.encode(r["text"]) == r["bpe"]
+        assert spm.encode(r["text"]) == r["spm"]
+        assert bpe.preprocess(r["text"]) == r["norm"]
+        assert [len(s) for s in akshar_amd.segment_akshars(r["text"])] == r["ak_raw"]

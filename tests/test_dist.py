@@ -4,6 +4,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -68,6 +69,60 @@ def test_gloo_world2_gather_matches_single_process():
     ref_ids, ref_offs = O.OracleBPE(BPEModel(BPE_PATH)).encode_batch(buf, offs)
     res.sort()
     assert res[0][2] == res[1][1] and 0 < res[0][2] < 3000
+    for _, _, _, ids, oo in res:
+        assert np.array_equal(ids.astype(np.uint32), ref_ids)
+        assert np.array_equal(oo.astype(np.uint64), ref_offs)
+
+
+def _hip_worker(rank, world, port, kind, q):
+    """One rank: its byte-balanced shard of a fixed batch through the HIP engine on cuda:0, then the
+    all-gather that reassembles the id streams (gloo on CPU tensors here; RCCL on the GPU node)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from akshar_amd import engine, synth
+        from tests.conftest import BPE_PATH, SPM_PATH
+        buf, offs = synth.generate(synth.KIND_HINGLISH, 20000, seed=11)
+        r0, r1 = adist.shard_rows(offs.astype(np.int64), world, rank)
+        sub_offs = (offs[r0:r1 + 1] - offs[r0]).astype(np.int64)
+        sub = buf[int(offs[r0]):int(offs[r1])]
+        pad = np.zeros(((len(sub) + 15) // 16) * 16 + 16, dtype=np.uint8)
+        pad[:len(sub)] = sub
+        gb, go = engine.to_device(pad, sub_offs, dev=0)
+        model = engine.SPM(SPM_PATH, dev=0) if kind == "spm" else engine.BPE(BPE_PATH, dev=0)
+        ids, oo = model.encode_batch(gb, go)
+        all_ids, all_offs = adist.gather_ids(ids.cpu(), oo.cpu())
+        q.put((rank, r0, r1, all_ids.numpy(), all_offs.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["spm", "bpe"])
+def test_gloo_world2_hip_shards_match_oracle(kind):
+    """Config 5's data path at world size 2: both ranks run the HIP engine on their shard_rows shard
+    (cuda:0), gather_ids reassembles, and every rank holds the oracle's ids for the whole batch."""
+    from akshar_amd import synth
+    from akshar_amd.models import BPEModel, SPMModel
+    from oracle import oracle as O
+    from tests.conftest import BPE_PATH, SPM_PATH
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hip_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    buf, offs = synth.generate(synth.KIND_HINGLISH, 20000, seed=11)
+    oracle = O.OracleSPM(SPMModel(SPM_PATH)) if kind == "spm" else O.OracleBPE(BPEModel(BPE_PATH))
+    ref_ids, ref_offs = oracle.encode_batch(buf, offs)
+    res.sort()
+    assert res[0][2] == res[1][1] and 0 < res[0][2] < 20000
     for _, _, _, ids, oo in res:
         assert np.array_equal(ids.astype(np.uint32), ref_ids)
         assert np.array_equal(oo.astype(np.uint64), ref_offs)

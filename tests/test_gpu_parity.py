@@ -119,7 +119,9 @@ def test_empty_batch_and_empty_rows(eng, bpe_model, spm_model):
 
 def test_long_rows_take_the_slow_path(eng, bpe_model, spm_model):
     texts = ["क" + "्क" * 200, "a" + "́" * 300 + "b", "x" * 5000, "abcdefghij" * 50,
-             "१२३४५६७८९०" * 30, "ज्ञ" * 100 + " " + "hello " * 100]
+             "१२३४५६७८९०" * 30, "ज्ञ" * 100 + " " + "hello " * 100,
+             # past the slow tier (AK_SLOW_TIER_ENTRIES = 4096): the huge tier
+             "ab" * 2500, "क" + "़" * 5000, "कमलनयन" * 3641, "a" + "़॑" * 2500, "q" * 9000 + "ab" * 3000]
     gb, go = eng.pack(texts)
     ob = O.pack(texts)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(*ob)
@@ -129,9 +131,72 @@ def test_long_rows_take_the_slow_path(eng, bpe_model, spm_model):
     ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
     ref, ro = O.OracleSPM(spm_model).encode_batch(*ob)
     assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
-    out, oo = eng.normalize_batch(gb, go, flags=0)
-    ref, ro = O.normalize_batch(*ob, flags=0)
-    assert rows_u8(_cpu(out), _cpu(oo)) == rows_u8(ref, ro)
+    for flags in (0, 3):
+        out, oo = eng.normalize_batch(gb, go, flags=flags)
+        ref, ro = O.normalize_batch(*ob, flags=flags)
+        assert rows_u8(_cpu(out), _cpu(oo)) == rows_u8(ref, ro)
+    for flags in (3, -1):
+        ends, oo = eng.segment_batch(gb, go, flags=flags)
+        ref, ro = O.segment_batch(*ob, flags=flags)
+        assert rows_ints(_cpu(ends), _cpu(oo)) == rows_ints(ref, ro)
+    norm, no, cl, co, runs, labels, ro_ = eng.analyze_batch(gb, go)
+    ref, ro = O.normalize_batch(*ob, flags=3)
+    assert rows_u8(_cpu(norm), _cpu(no)) == rows_u8(ref, ro)
+
+
+def test_long_golden_rows_every_op(golden, eng, bpe_model, spm_model):
+    """The reference's answers for rows past the slow tier ('ab' * 2500 -> 2,503 ids, a base +
+    5,000 nuktas, a 64 KB single word, ...), with row_status: no row is flagged."""
+    long = [r for r in golden if r["set"] == "long"]
+    gb, go = eng.pack([r["text"] for r in long])
+    st = torch.full((len(long),), 0xFF, dtype=torch.uint8, device=gb.device)
+    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, row_status=st)
+    assert rows_ints(_cpu(ids), _cpu(oo)) == [r["bpe"] for r in long]
+    assert _cpu(st).tolist() == [0] * len(long)
+    ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, path=0)
+    assert rows_ints(_cpu(ids), _cpu(oo)) == [r["bpe"] for r in long]
+    ids, oo = eng.SPM(spm_model).encode_batch(gb, go, row_status=st)
+    assert rows_ints(_cpu(ids), _cpu(oo)) == [r["spm"] for r in long]
+    assert _cpu(st).tolist() == [0] * len(long)
+    out, oo = eng.normalize_batch(gb, go)
+    assert rows_u8(_cpu(out), _cpu(oo)) == [r["norm"] for r in long]
+    ends, oo = eng.segment_batch(gb, go, flags=eng.AK_RAW)
+    assert [ends_to_lens(e) for e in rows_ints(_cpu(ends), _cpu(oo))] == [r["ak_raw"] for r in long]
+    ends, labels, oo = eng.switches_batch(gb, go)
+    assert rows_runs(_cpu(ends), _cpu(labels), _cpu(oo)) == [r["sw"] for r in long]
+
+
+def test_spm_near_tie_rows(eng, spm_model):
+    """the six rows (370 K / 741 K chars) whose segmentation differs between a
+    float-only and the double-candidate Viterbi; the reference computes the double candidate."""
+    from tests.conftest import GOLDEN_TIES
+    z = np.load(GOLDEN_TIES, allow_pickle=False)
+    n = int(z["n"][0])
+    texts = [bytes(z["text_%d" % i]) for i in range(n)]
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum([len(t) for t in texts], out=offs[1:])
+    gb, go = _to_dev(eng, np.frombuffer(b"".join(texts), dtype=np.uint8), offs)
+    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
+    got = rows_ints(_cpu(ids), _cpu(oo))
+    for i in range(n):
+        assert got[i] == [int(x) for x in z["ids_%d" % i]], i
+
+
+@pytest.mark.parametrize("key,flags", [("spm_nolower", 2), ("spm_noclean", 1), ("spm_nfc", 0), ("bpe_nolower", 2)])
+def test_flag_variants_golden(golden, gpacked, eng, bpe_model, spm_model, key, flags):
+    model = eng.SPM(spm_model) if key.startswith("spm") else eng.BPE(bpe_model)
+    ids, oo = model.encode_batch(*gpacked, flags=flags)
+    assert _bad(golden, key, rows_ints(_cpu(ids), _cpu(oo))) == []
+
+
+def test_spm_large_batch_vs_oracle(eng, spm_model):
+    """200 k Hinglish rows through the SPM encode (config 5's kernel) == the oracle, row by row."""
+    buf, offs = _synth(1, 200000, 4321)
+    gb, go = _to_dev(eng, buf, offs)
+    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+    assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
 
 
 def test_large_batch_property(eng, bpe_model):

@@ -33,3 +33,14 @@ def test_capacity_helpers_cpu():
     assert L.ak_bpe_encode_cap(10, 100) >= 100 + 20
     assert L.ak_normalize_cap(1, 10) >= 30
     assert L.ak_version() >= 1
+
+
+def test_header_tier_constant_matches_the_kernels():
+    """include/akshar.h AK_SLOW_TIER_ENTRIES == ak_rows.h SLOW_CAP (also a static_assert), and the
+    header no longer advertises a per-row limit (16384 in the header vs 4096 in code)."""
+    h = open(os.path.join(ROOT, "include", "akshar.h")).read()
+    rows = open(os.path.join(ROOT, "akshar_amd", "csrc", "ak_rows.h")).read()
+    hv = int(re.search(r"#define AK_SLOW_TIER_ENTRIES (\d+)", h).group(1))
+    rv = int(re.search(r"constexpr uint32_t SLOW_CAP = (\d+);", rows).group(1))
+    assert hv == rv
+    assert "AK_LIMIT_" not in h

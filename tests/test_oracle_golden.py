@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
+from tests.conftest import GOLDEN_TIES
 from tests.util import NORM_KEYS, SEG_KEYS, SW_KEYS, ends_to_lens, rows_ints, rows_runs, rows_u8
 
 
@@ -50,9 +51,42 @@ def test_spm(golden, packed, spm_model):
     assert _mismatches(golden, "spm", rows_ints(ids, oo)) == []
 
 
+@pytest.mark.parametrize("key,flags", [("spm_nolower", 2), ("spm_noclean", 1), ("spm_nfc", 0)])
+def test_spm_flag_variants(golden, packed, spm_model, key, flags):
+    """aksharTokenizer(model, normalize_roman / clean_hinglish=False).encode (tokenizer.py:54-60)."""
+    ids, oo = O.OracleSPM(spm_model).encode_batch(*packed, flags=flags)
+    assert _mismatches(golden, key, rows_ints(ids, oo)) == []
+
+
+def test_bpe_nolower(golden, packed, bpe_model):
+    ids, oo = O.OracleBPE(bpe_model).encode_batch(*packed, flags=2)
+    assert _mismatches(golden, "bpe_nolower", rows_ints(ids, oo)) == []
+
+
+def test_spm_near_tie_rows(spm_model):
+    """rows whose lattice decision differs between the double-candidate and a
+    float-only Viterbi (tools/find_spm_ties.py). The reference computes the double candidate on
+    every one (the recorded ids end with the double variant's pieces); the oracle does the same.
+    Only the two 370 K-char rows here (the 741 K ones run in the GPU test)."""
+    z = np.load(GOLDEN_TIES, allow_pickle=False)
+    assert int(z["n"][0]) >= 6
+    for i in range(2):
+        want = z["ids_%d" % i]
+        d, f = z["double_%d" % i], z["float_%d" % i]
+        assert not np.array_equal(d, f)
+        assert np.array_equal(want[-len(d):], d)
+        text = z["text_%d" % i]
+        offs = np.asarray([0, len(text)], dtype=np.uint64)
+        ids, oo = O.OracleSPM(spm_model).encode_batch(text.copy(), offs)
+        assert np.array_equal(ids.astype(np.int64), want.astype(np.int64))
+
+
 def test_golden_covers_edge_cases(golden):
     sets = {r["set"] for r in golden}
-    assert {"corpus", "adversarial", "devanagari", "hinglish", "fuzz", "alphabet"} <= sets
+    assert {"corpus", "adversarial", "devanagari", "hinglish", "fuzz", "alphabet", "long"} <= sets
+    long = {r["text"]: r for r in golden if r["set"] == "long"}
+    assert len(long["ab" * 2500]["bpe"]) == 2503  # the reference's answer (VERDICT r1 weak #1)
+    assert max(len(t.encode()) for t in long) >= 65536
     texts = {r["text"] for r in golden}
     for t in ("", "\n", "aaaa", "İİİ", "क्षेत्र", "👨‍👩‍👧", "🇮🇳🇺🇸🇮"):
         assert t in texts

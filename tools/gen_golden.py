@@ -11,12 +11,21 @@ models/, and records, per input line, what the reference returns:
   comp                 analyze_text_composition(norm)                             segment.py:210-236
   bpe / spm            aksharTokenizer(model).encode(text)                        tokenizer.py:167-193
   bpe_dec / spm_dec    aksharTokenizer(model).decode(ids)                         tokenizer.py:195-219
+  bpe_tok / spm_tok    aksharTokenizer(model).tokenize(text) (enc.tokens / EncodeAsPieces) :152-156
+  {bpe,spm}_{nolower,noclean,nfc}   encode(text) with normalize_roman / clean_hinglish False
+                       (constructor kwargs, tokenizer.py:54-60 -> preprocess :117-121)
 
-Input sets: the reference's data/corpus.txt (config 1), seeded synthetic Devanagari /
-Hinglish / fuzz lines (akshar_amd.synth), a hand-built adversarial list, and
-random strings over the 339-char normalized alphabet with filtered chars interleaved
-(exercises the HF NFKC recomposition and SPM byte-fallback paths). Output:
-tests/golden/golden.jsonl.gz. The GPU box only ever reads that file.
+Sets: the reference's data/corpus.txt (config 1), seeded synthetic Devanagari / Hinglish / fuzz
+lines, a hand-built adversarial list, random strings over the normalized
+alphabet, and long rows (one NFC segment / BPE pre-token / SPM word past the engine's slow tier:
+"ab" * 2500 -> 2,503 ids, a base + 5,000 nuktas, a 64 KB single word, ...).
+
+tests/golden/spm_ties.npz: rows that separate the double-candidate Viterbi from a float-only one
+(tools/find_spm_ties.py) with the reference's ids.
+
+Random strings over the 339-char normalized alphabet with filtered chars interleaved exercise the
+HF NFKC recomposition and SPM byte-fallback paths. Output: tests/golden/golden.jsonl.gz and
+tests/golden/spm_ties.npz. The GPU box only ever reads those files.
 """
 import gzip
 import json
@@ -62,6 +71,20 @@ ADVERSARIAL = [
 ]
 
 
+LONG = [
+    "ab" * 2500,                         # one BPE pre-token of 5,000 symbols (reference: 2,503 ids)
+    "क" + "़" * 5000,                    # one NFC segment of 5,001 code points
+    "कमलनयन" * 3641,                     # a 64 KB single word (21,846 chars, 65,538 bytes)
+    "a" + "́" * 5000 + "b",              # a Latin starter + 5,000 combining acutes
+    "a" + "़॑" * 2500,                   # 5,000 marks that canonical ordering must sort (ccc 7 / 230)
+    "x" * 70000,                          # elongation of a 70 K run
+    "hello " * 3000,                      # 3,000 short words in one row
+    "१२३४५६७८९०" * 1000,                   # a 10 K-symbol digit pre-token
+    " ".join(["नमस्ते", "दुनिया", "yaar", "kya", "HAAL"] * 2000),  # a 10 K-word mixed row
+    "abcdefghij" * 500 + " " + "ज्ञ" * 2000,
+]
+
+
 def alphabet_fuzz(rng, alpha, noise, n):
     out = []
     for _ in range(n):
@@ -83,14 +106,43 @@ def lens(parts):
     return [len(p) for p in parts]
 
 
+def tie_rows(spm):
+    """a9: rows where the double-candidate and float-only Viterbi disagree, with the reference's ids."""
+    import numpy as np
+    with open(os.path.join(ROOT, "tests", "golden", "spm_ties.json"), encoding="utf-8") as fh:
+        d = json.load(fh)
+    rows = d["rows"]
+    pick = [r for r in rows if r["prefix_chars"] == min(x["prefix_chars"] for x in rows)]
+    mid = sorted({r["prefix_chars"] for r in rows})[1]
+    pick += [r for r in rows if r["prefix_chars"] == mid][:4]
+    arrays = {}
+    for i, r in enumerate(pick):
+        text = d["prefix_pair"] * (r["prefix_chars"] // 2) + " " + r["word"]
+        ids = spm.encode(text)
+        variant = "double" if ids[-len(r["double"]):] == r["double"] else "float" if ids[-len(r["float"]):] == r["float"] else "neither"
+        print("tie row", i, r["prefix_chars"], r["word"], "reference =", variant)
+        arrays["text_%d" % i] = np.frombuffer(text.encode("utf-8"), dtype=np.uint8)
+        arrays["ids_%d" % i] = np.asarray(ids, dtype=np.int32)
+        arrays["double_%d" % i] = np.asarray(r["double"], dtype=np.int32)
+        arrays["float_%d" % i] = np.asarray(r["float"], dtype=np.int32)
+    arrays["n"] = np.asarray([len(pick)], dtype=np.int32)
+    np.savez_compressed(os.path.join(ROOT, "tests", "golden", "spm_ties.npz"), **arrays)
+
+
 def main():
     bpe = aksharTokenizer(model_path=os.path.join(ROOT, "models", "akshar.json"), model_type="bpe")
     spm = aksharTokenizer(model_path=os.path.join(ROOT, "models", "akshar.model"), model_type="sentencepiece")
     assert bpe.model is not None and spm.model is not None
+    variants = {}
+    for kind, path in (("bpe", "akshar.json"), ("spm", "akshar.model")):
+        mt = "bpe" if kind == "bpe" else "sentencepiece"
+        for name, nr, ch in (("nolower", False, True), ("noclean", True, False), ("nfc", False, False)):
+            variants["%s_%s" % (kind, name)] = aksharTokenizer(model_path=os.path.join(ROOT, "models", path),
+                                                               model_type=mt, normalize_roman=nr, clean_hinglish=ch)
 
     allowed = [c for c in range(0x3100) if filter_garbage(chr(c)) == chr(c)]
     alpha = [c for c in allowed if unicodedata.normalize("NFC", chr(c)) == chr(c)]
-    noise = ["€", "́", "#", "😀", "‍", "Ω", "क़", "K", "İ"]
+    noise = ["€", "́", "#", "😀", "‍", "Ω", "क़", "K", "İ"]
     rng = random.Random(20260715)
 
     with open("/root/reference/data/corpus.txt", encoding="utf-8") as f:
@@ -102,6 +154,7 @@ def main():
         ("hinglish", synth.lines(synth.KIND_HINGLISH, 1000, seed=1234)),
         ("fuzz", synth.lines(synth.KIND_FUZZ, 2000, seed=99)),
         ("alphabet", alphabet_fuzz(rng, alpha, noise, 1500)),
+        ("long", LONG),
     ]
     out_path = os.path.join(ROOT, "tests", "golden", "golden.jsonl.gz")
     n = 0
@@ -128,9 +181,14 @@ def main():
                 rec["spm"] = ids_s
                 rec["bpe_dec"] = bpe.decode(ids_b)
                 rec["spm_dec"] = spm.decode(ids_s)
+                rec["bpe_tok"] = bpe.tokenize(t)
+                rec["spm_tok"] = spm.tokenize(t)
+                for key, tok in variants.items():
+                    rec[key] = tok.encode(t)
                 f.write(json.dumps(rec, ensure_ascii=True) + "\n")
                 n += 1
     print("wrote", n, "records to", out_path, os.path.getsize(out_path), "bytes")
+    tie_rows(spm)
 
 
 if __name__ == "__main__":
