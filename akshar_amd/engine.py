@@ -88,11 +88,20 @@ def _check_inputs(buf, offs):
     return n
 
 
-def _run(fn_call, n, cap, make_out, dev, ws):
+def _run(fn_call, n, cap, make_out, dev, ws, out=None, out_offs=None):
     """Run a capacity-bounded op, re-running once with the exact size if needed. Every row is exact
     at any length (include/akshar.h "Row lengths"); ak_ws_check turns an internal overflow into an
-    exception instead of a short row."""
-    out_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    exception instead of a short row. With a caller-provided `out` (and `out_offs`), the output is
+    written in place and a short capacity raises instead of re-running."""
+    if out_offs is None:
+        out_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    if out is not None:
+        fn_call(out, out.numel(), out_offs)
+        total = int(out_offs[-1].item())
+        if total > out.numel():
+            raise AksharError("output buffer too small: %d elements needed, %d given" % (total, out.numel()))
+        check(_lib.lib().ak_ws_check(ws), "ak_ws_check")
+        return out, out_offs, total
     outs = make_out(cap)
     fn_call(outs, cap, out_offs)
     total = int(out_offs[-1].item())
@@ -218,7 +227,10 @@ class BPE:
         if h:
             _lib.lib().ak_bpe_free(h)
 
-    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, path=None):
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, path=None, out=None,
+                     out_offs=None):
+        """Device rows -> (int32 ids, int64 row offsets). `out` / `out_offs` (optional, int32 /
+        int64 device tensors, the latter n + 1 long) receive the result in place."""
         n = _check_inputs(buf, offs)
         dev = buf.device
         ws = workspace(dev.index)
@@ -233,7 +245,8 @@ class BPE:
             check(_lib.lib().ak_bpe_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
                                            _ptr(row_status), _stream(dev)), "ak_bpe_encode")
 
-        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev, ws)
+        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev, ws,
+                              out, out_offs)
         return out[:total], oo
 
 
@@ -256,7 +269,8 @@ class SPM:
         if h:
             _lib.lib().ak_spm_free(h)
 
-    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None):
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, out=None, out_offs=None):
+        """Device rows -> (int32 ids, int64 row offsets); `out` / `out_offs` as BPE.encode_batch."""
         n = _check_inputs(buf, offs)
         dev = buf.device
         ws = workspace(dev.index)
@@ -269,7 +283,8 @@ class SPM:
             check(_lib.lib().ak_spm_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
                                            _ptr(row_status), _stream(dev)), "ak_spm_encode")
 
-        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev, ws)
+        out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.int32, device=dev), dev, ws,
+                              out, out_offs)
         return out[:total], oo
 
 

@@ -1,23 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark: the reference's encode hot path on MI355X (BASELINE.json metric).
 
-Workload: 10 M synthetic Hinglish sentences per GPU, encoded end to end
-exactly as `aksharTokenizer(model_path="models/akshar.json", model_type="bpe").encode(line)`
-(tokenizer.py:167-193): normalize_text (NFC, roman lowercasing, allowlist, elongation collapse)
--> HF NFKC -> Whitespace pre-tokenizer -> 24k BPE merges -> <s> ... </s>. Rows are packed UTF-8
-+ int64 offsets already resident in HBM when timing starts; ids + row offsets are written back
-to HBM. One step = one encode of the whole per-GPU batch.
+Workloads (`--workload`):
+  cfg4 (default)  10 M synthetic Hinglish sentences PER GPU, encoded end to end exactly as
+                  `aksharTokenizer(model_path="models/akshar.json", model_type="bpe").encode(line)`
+                  (tokenizer.py:167-193): normalize_text -> HF NFKC -> Whitespace pre-tokenizer ->
+                  24k BPE merges -> <s> ... </s>. Weak scaling: every rank encodes its own 10 M
+                  rows, no data-path collective. One step = one encode of the per-GPU batch.
+  cfg5            ONE fixed batch of --rows (default 100 M) synthetic Hinglish sentences (the same
+                  rows for every N: row i is generated from its global index), cut into contiguous
+                  byte-balanced shards (rank 0 sizes every row and broadcasts the cuts, the
+                  akshar_amd.dist.shard_rows rule), each rank's shard encoded with the 24k unigram
+                  SentencePiece model (`model_type="sentencepiece"`) in chunks straight into one
+                  per-rank id buffer, then ONE all-gather reassembles the whole batch's id streams
+                  on every rank (akshar_amd.dist.gather_ids: RCCL over xGMI). Strong scaling. One
+                  step = encode of the shard + the gather (gather_ms reported separately).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--gather]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N (one rank/GPU;
-  each rank encodes its own 10 M-row shard: weak scaling, no data-path collective; --gather adds
-  the RCCL all-gather that reassembles the id streams on every rank, timed separately).
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg4|cfg5] [--rows R]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Prints ONE JSON line (rank 0) with value = whole-job MB/s of raw UTF-8 input, tokens/s,
-the dominant kernel's HBM roofline (HIP events around its launches on the encode stream) and
-the CPU baseline (the oracle restatement, 1 thread, timed on a bounded sample on this host).
+Rows are packed UTF-8 + int64 offsets already resident in HBM when the timed region starts. Prints
+ONE JSON line (rank 0): value = whole-job MB/s of raw UTF-8 input (max-over-ranks time), tokens/s,
+the dominant kernel's HBM roofline (SURVEY.md §8(d) read bytes / its average launch time from HIP
+events on the encode stream; PMC traffic from profiles/), the CPU baseline (the oracle, 1 thread
+and all host cores, on a bounded sample) and end-to-end host->host rates (N = 1 only).
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -30,9 +39,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MB of raw UTF-8 tokenized/sec @1 GPU (+ tokens/s); bit-exact vs CPU ref"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 SEED = 1234
-TRAFFIC_FILE = "r01_v7_tiles_pmc.json"  # PMC HBM bytes of the tile kernel at the default config
+KERNEL_NAMES = {"tiles": "k_bpe_tiles<3> (tile-cooperative BPE encode)",
+                "spm_tiles": "k_spm_tiles<3> (tile-cooperative SentencePiece encode)",
+                "emit": "k_rows_stage<OP,3> (staged row kernel, one lane per row)"}
 
 
 def parse():
@@ -40,12 +51,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=10_000_000, help="rows per GPU (config 4: 10 M)")
-    ap.add_argument("--gather", action="store_true", help="also all-gather the id streams (RCCL)")
-    ap.add_argument("--cpu-rows", type=int, default=400_000, help="CPU baseline sample (rows)")
+    ap.add_argument("--workload", choices=("cfg4", "cfg5"), default="cfg4")
+    ap.add_argument("--rows", type=int, default=None, help="cfg4: rows per GPU (10 M); cfg5: rows of the batch (100 M)")
+    ap.add_argument("--chunk-rows", type=int, default=25_000_000, help="cfg5: rows per encode call")
+    ap.add_argument("--gather", action="store_true", help="cfg4: also all-gather the id streams (RCCL)")
+    ap.add_argument("--cpu-rows", type=int, default=400_000, help="CPU baseline sample (rows, single thread)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-others", action="store_true", help="skip the config 2/3/5 side measurements")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host->host rates")
     return ap.parse_args()
+
+
+T_START = time.perf_counter()
 
 
 def log(rank, msg):
@@ -54,39 +71,97 @@ def log(rank, msg):
         print("[bench %.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
 
 
-T_START = time.perf_counter()
+# ------------------------------------------------------------------------------------------ CPU
+def cpu_info():
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, avail
 
 
-def cpu_baseline(args, buf, offs):
-    """The oracle (plain C, one thread) on the first --cpu-rows rows of rank 0's shard."""
-    from akshar_amd.models import BPEModel
+def cpu_threads():
+    """Host threads this process may use: the affinity set, capped by OMP_NUM_THREADS (16 on the GPU
+    box, whose nproc shows the whole machine)."""
+    _, _, avail = cpu_info()
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(avail, cap) if cap > 0 else avail)
+
+
+def cpu_baseline(args, buf, offs, kind):
+    """The oracle (oracle/akshar_oracle.c) on bounded samples of the same batch: one thread, then
+    all host threads (row ranges on a thread pool; ctypes releases the GIL in the C calls)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from akshar_amd.models import BPEModel, SPMModel
     from oracle import oracle as O
-    n = min(args.cpu_rows, len(offs) - 1)
-    sub_offs = offs[:n + 1].astype(np.uint64)
-    sub = buf[:int(sub_offs[-1])]
-    ob = O.OracleBPE(BPEModel(os.path.join(ROOT, "models", "akshar.json")))
+    model = (O.OracleBPE(BPEModel(os.path.join(ROOT, "models", "akshar.json"))) if kind == "bpe"
+             else O.OracleSPM(SPMModel(os.path.join(ROOT, "models", "akshar.model"))))
+
+    def run(r0, r1):
+        sub_offs = (offs[r0:r1 + 1] - offs[r0]).astype(np.uint64)
+        sub = buf[int(offs[r0]):int(offs[r1])]
+        ids, _ = model.encode_batch(sub, sub_offs)
+        return len(sub), len(ids)
+
+    n1 = min(args.cpu_rows, len(offs) - 1)
     t = time.perf_counter()
-    ids, _ = ob.encode_batch(sub, sub_offs)
-    dt = time.perf_counter() - t
-    return {"value": round(len(sub) / 1e6 / dt, 3), "unit": "MB/s", "cores": 1, "kind": "port",
-            "tokens_per_s": round(len(ids) / dt, 1),
-            "sample": "first %d rows (%.1f MB) of the same synthetic Hinglish batch, oracle/akshar_oracle.c "
-                      "or_bpe_encode single-threaded, %.1f s" % (n, len(sub) / 1e6, dt)}
+    b1, i1 = run(0, n1)
+    dt1 = time.perf_counter() - t
+    T = cpu_threads()
+    nT = min(len(offs) - 1, n1 * T // 2)
+    cuts = [nT * k // T for k in range(T + 1)]
+    t = time.perf_counter()
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(lambda k: run(cuts[k], cuts[k + 1]), range(T)))
+    dtT = time.perf_counter() - t
+    bT, iT = sum(r[0] for r in res), sum(r[1] for r in res)
+    cpu_model, nproc, avail = cpu_info()
+    single = {"value": round(b1 / 1e6 / dt1, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+              "tokens_per_s": round(i1 / dt1, 1),
+              "sample": "first %d rows (%.1f MB) of the timed batch, oracle/akshar_oracle.c %s encode, one thread, %.1f s"
+                        % (n1, b1 / 1e6, kind, dt1)}
+    calib = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if os.path.exists(calib):
+        c = json.load(open(calib)).get(kind)
+        if c:
+            single["python_reference_equivalent_mb_s"] = round(single["value"] / c["oracle_over_reference"], 3)
+            single["calibration"] = "profiles/cpu_calibration.json: oracle / Python reference = %.2f on the same rows " \
+                                    "(build container)" % c["oracle_over_reference"]
+    return {"value": round(bT / 1e6 / dtT, 3), "unit": "MB/s", "cores": T, "kind": "port",
+            "tokens_per_s": round(iT / dtT, 1),
+            "sample": "first %d rows (%.1f MB) of the timed batch split over %d threads, oracle/akshar_oracle.c %s "
+                      "encode, %.1f s" % (nT, bT / 1e6, T, kind, dtT),
+            "cpu_model": cpu_model, "nproc": nproc, "affinity_cpus": avail, "single_thread": single}
 
 
+# ------------------------------------------------------------------------------------------ side configs
 def other_configs(dev, rows=1_000_000):
-    """SURVEY.md §8 configs 2, 3 and 5 on this GPU (1 M synthetic rows each, inputs in HBM): the
-    single-GPU rates of the other rows of the scope table, reported beside the headline line."""
+    """SURVEY.md §8 configs 2, 3 and 5 on this GPU (1 M synthetic rows each, inputs in HBM): device
+    time of each op's kernels (the library's HIP events) and the wall time of the Python call."""
     from akshar_amd import engine, synth
 
     def timed(fn, reps=3):
         fn()
         torch.cuda.synchronize()
+        engine.profile_enable(True)
+        engine.profile_reset()
         t = time.perf_counter()
         for _ in range(reps):
             fn()
         torch.cuda.synchronize()
-        return (time.perf_counter() - t) / reps
+        wall = (time.perf_counter() - t) / reps
+        prof = engine.profile_read()
+        engine.profile_enable(False)
+        return sum(v[0] for v in prof.values()) / reps / 1e3, wall
 
     out = {}
     spm = engine.SPM(os.path.join(ROOT, "models", "akshar.model"), dev=dev)
@@ -102,18 +177,74 @@ def other_configs(dev, rows=1_000_000):
                "switches": lambda: engine.switches_batch(gb, go),
                "spm_encode": lambda: spm.encode_batch(gb, go),
                "analyze_fused": lambda: engine.analyze_batch(gb, go)}
-        res = {k: round(mb / timed(f), 1) for k, f in ops.items()}
+        res = {}
+        for k, f in ops.items():
+            kt, wt = timed(f)
+            res[k] = {"kernels_mb_s": round(mb / kt, 1), "call_mb_s": round(mb / wt, 1)}
         res["rows"], res["mb"] = rows, round(mb, 1)
         out[name] = res
     d, h = out["devanagari"], out["hinglish"]
-    t3 = sum(1.0 / h[k] for k in ("normalize", "switches", "segment"))
-    return {"unit": "MB/s of raw UTF-8 (1 M synthetic rows, inputs in HBM, one-lane-per-row staged kernels)",
-            "cfg2_segment_devanagari": d["segment"], "cfg2_segment_devanagari_raw": d["segment_raw"],
-            "cfg3_normalize_switches_segment_hinglish": h["analyze_fused"],
-            "cfg3_as_three_separate_ops": round(1.0 / t3, 1),
-            "cfg5_spm_encode_hinglish_per_gpu": h["spm_encode"], "detail": out}
+    return {"unit": "MB/s of raw UTF-8 (1 M synthetic rows, inputs in HBM); kernels_mb_s = bytes / summed device "
+                    "time of the op's kernels, call_mb_s = bytes / wall time of the Python call",
+            "cfg2_segment_devanagari": d["segment"]["kernels_mb_s"],
+            "cfg3_normalize_switches_segment_hinglish": h["analyze_fused"]["kernels_mb_s"],
+            "cfg5_spm_encode_hinglish_per_gpu": h["spm_encode"]["kernels_mb_s"], "detail": out}
 
 
+# ------------------------------------------------------------------------------------------ end to end
+def end_to_end(dev, model, host_buf, host_offs, kind):
+    """Host -> host rates (PCIe included; never `value`): (a) packed numpy rows -> numpy ids + row
+    offsets (H2D, encode, D2H); (b) list[str] -> list[list[int]] through the drop-in class."""
+    from akshar_amd import engine, synth
+    from akshar_amd.tokenizer import aksharTokenizer
+    nbytes = int(host_offs[-1])
+    pad = np.zeros(((nbytes + 15) // 16) * 16 + 16, dtype=np.uint8)
+    pad[:nbytes] = host_buf
+    offs64 = host_offs.astype(np.int64)
+
+    def arrays():
+        gb, go = engine.to_device(pad, offs64, dev=dev)
+        ids, oo = model.encode_batch(gb, go, nbytes=nbytes)
+        return ids.cpu().numpy(), oo.cpu().numpy()
+
+    arrays()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    ids, _ = arrays()
+    dt_a = time.perf_counter() - t
+    n_list = 200_000
+    texts = synth.lines(synth.KIND_HINGLISH, n_list, seed=SEED + 3)
+    lb = sum(len(x.encode()) for x in texts)
+    mp = os.path.join(ROOT, "models", "akshar.json" if kind == "bpe" else "akshar.model")
+    tk = aksharTokenizer(model_path=mp, model_type="bpe" if kind == "bpe" else "sentencepiece")
+    tk.encode_batch(texts[:1000])
+    t = time.perf_counter()
+    res = tk.encode_batch(texts)
+    dt_l = time.perf_counter() - t
+    return {"arrays_mb_s": round(nbytes / 1e6 / dt_a, 1), "arrays_tokens_per_s": round(len(ids) / dt_a, 1),
+            "arrays": "numpy bytes + offsets (%d rows, %.0f MB) -> H2D -> encode -> D2H numpy ids + offsets, %.1f ms"
+                      % (len(host_offs) - 1, nbytes / 1e6, dt_a * 1e3),
+            "list_mb_s": round(lb / 1e6 / dt_l, 2), "list_tokens_per_s": round(sum(len(r) for r in res) / dt_l, 1),
+            "list": "aksharTokenizer.encode_batch(list of %d str) -> list[list[int]] (UTF-8 packing, H2D, encode, D2H, "
+                    "Python int lists), %.1f ms" % (n_list, dt_l * 1e3)}
+
+
+# ------------------------------------------------------------------------------------------ PMC traffic
+def pmc_traffic(kernel, rows, nbytes):
+    """HBM bytes per launch of `kernel` measured by rocprofv3 PMC on the same launch shape (newest
+    profiles/*_pmc.json whose kernel, rows and bytes match), or (None, None)."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if t.get("kernel_class") == kernel and t.get("rows") == rows and t.get("bytes") == nbytes:
+            return int(t["hbm_bytes_per_launch"]), "profiles/%s (rocprofv3 FETCH_SIZE x1024 x2 + WRITE_SIZE x1024, " \
+                                                   "same launch shape)" % os.path.basename(path)
+    return None, None
+
+
+# ------------------------------------------------------------------------------------------ main
 def main():
     args = parse()
     dist = args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1
@@ -132,28 +263,93 @@ def main():
             tdist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    cdev = dev if (not dist or tdist.get_backend() == "nccl") else torch.device("cpu")
 
     from akshar_amd import engine, synth
-    rows = args.rows
-    log(rank, "generating %d rows" % rows)
-    buf, offs = synth.generate(synth.KIND_HINGLISH, rows, seed=SEED, first=rank * rows)
-    log(rank, "generated %.1f MB" % (offs[-1] / 1e6))
+    cfg5 = args.workload == "cfg5"
+    if not cfg5:
+        rows = args.rows or 10_000_000
+        r0 = rank * rows
+        log(rank, "cfg4: generating %d rows per GPU" % rows)
+    else:
+        total_rows = args.rows or 100_000_000
+        log(rank, "cfg5: sizing %d rows" % total_rows)
+        cuts = torch.zeros(world + 1, dtype=torch.int64)
+        if rank == 0:  # byte-balanced contiguous shards (dist.shard_rows rule) from the row lengths
+            from akshar_amd import dist as adist
+            lens = np.empty(total_rows, dtype=np.uint64)
+            synth._lib().ak_synth_sizes(SEED, synth.KIND_HINGLISH, 0, total_rows, lens.ctypes.data)
+            offs_all = np.zeros(total_rows + 1, dtype=np.int64)
+            np.cumsum(lens, out=offs_all[1:])
+            del lens
+            cuts = torch.tensor([adist.shard_rows(offs_all, world, k)[0] for k in range(world)] + [total_rows],
+                                dtype=torch.int64)
+            del offs_all
+        if dist:
+            cc = cuts.to(cdev)
+            tdist.broadcast(cc, 0)
+            cuts = cc.cpu()
+        r0, r1 = int(cuts[rank]), int(cuts[rank + 1])
+        rows = r1 - r0
+        log(rank, "cfg5: rank shard rows [%d, %d)" % (r0, r1))
+    buf, offs = synth.generate(synth.KIND_HINGLISH, rows, seed=SEED, first=r0)
     nbytes = int(offs[-1])
+    log(rank, "generated %.1f MB" % (nbytes / 1e6))
     pad = np.zeros(((nbytes + 15) // 16) * 16 + 16, dtype=np.uint8)
     pad[:nbytes] = buf
     gbuf, goffs = engine.to_device(pad, offs.astype(np.int64), dev=local)
-    bpe = engine.BPE(os.path.join(ROOT, "models", "akshar.json"), dev=local)
-    cap = nbytes // 2 + 2 * rows + 1024
+    kind = "spm" if cfg5 else "bpe"
+    model = (engine.SPM(os.path.join(ROOT, "models", "akshar.model"), dev=local) if cfg5
+             else engine.BPE(os.path.join(ROOT, "models", "akshar.json"), dev=local))
+    # id capacity: BPE <= bytes + 2 per row (tile path bound), measured ~0.2 ids per byte for both
+    # models; the encode raises (never truncates) if a caller buffer is short
+    cap = (nbytes // 4 if cfg5 else nbytes // 2) + 2 * rows + 1024
+    if cfg5:  # chunks of the shard encoded straight into one per-rank buffer
+        ch = max(1, args.chunk_rows)
+        chunks = []
+        for c0 in range(0, rows, ch):
+            c1 = min(rows, c0 + ch)
+            b0, b1 = int(offs[c0]), int(offs[c1])
+            chunks.append((c0, c1, b0, b1, goffs[c0:c1 + 1] - b0))
+        ids_all = torch.empty(cap, dtype=torch.int32, device=dev)
+        offs_all = torch.empty(rows + 1, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
+    gather_s = [0.0]
 
     def step():
-        return bpe.encode_batch(gbuf, goffs, cap=cap, nbytes=nbytes)
+        if not cfg5:
+            ids, oo = model.encode_batch(gbuf, goffs, cap=cap, nbytes=nbytes)
+            if dist and args.gather:
+                from akshar_amd import dist as adist
+                tg = time.perf_counter()
+                adist.gather_ids(ids, oo)
+                torch.cuda.synchronize()
+                gather_s[0] += time.perf_counter() - tg
+            return ids, oo
+        pos = 0
+        for c0, c1, b0, b1, co in chunks:
+            # rows [c0, c1) start at byte b0 (16-aligned or not: the engine reads aligned blocks)
+            ids, oo = model.encode_batch(gbuf[b0:], co, nbytes=b1 - b0, out=ids_all[pos:],
+                                         out_offs=offs_all[c0:c1 + 1])
+            if pos:
+                offs_all[c0:c1 + 1] += pos
+            pos += ids.numel()
+        ids, oo = ids_all[:pos], offs_all
+        if dist:
+            from akshar_amd import dist as adist
+            torch.cuda.synchronize()
+            tg = time.perf_counter()
+            adist.gather_ids(ids, oo)
+            torch.cuda.synchronize()
+            gather_s[0] += time.perf_counter() - tg
+        return ids, oo
 
     for i in range(args.warmup):
         ids, oo = step()
         torch.cuda.synchronize()
         log(rank, "warmup %d done" % i)
     n_ids = int(ids.numel())
+    gather_s[0] = 0.0
 
     engine.profile_enable(True)
     engine.profile_reset()
@@ -169,29 +365,24 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     prof = engine.profile_read()
-    passes = engine.profile_tile_passes(local)
-    fb_rows = engine.fallback_rows(local)
+    passes = engine.profile_tile_passes(local) if not cfg5 else {}
+    fb_rows = engine.fallback_rows(local) if not cfg5 else (0, 0)
     engine.profile_enable(False)
 
-    gather_ms = None
-    if dist and args.gather:
-        from akshar_amd import dist as adist
-        torch.cuda.synchronize()
-        tg = time.perf_counter()
-        adist.gather_ids(ids, oo)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
-
     if dist:
-        rdev = dev if tdist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
+        t = torch.tensor([elapsed, gather_s[0]], dtype=torch.float64, device=cdev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([nbytes, n_ids], dtype=torch.float64, device=rdev)
+        elapsed, gmax = float(t[0]), float(t[1])
+        tot = torch.tensor([nbytes, n_ids], dtype=torch.float64, device=cdev)
         tdist.all_reduce(tot)
         job_bytes, job_ids = float(tot[0]), float(tot[1])
+        imb = torch.tensor([nbytes], dtype=torch.float64, device=cdev)
+        mx, mn = imb.clone(), imb.clone()
+        tdist.all_reduce(mx, op=tdist.ReduceOp.MAX)
+        tdist.all_reduce(mn, op=tdist.ReduceOp.MIN)
+        byte_imbalance = float(mx) / max(float(mn), 1.0)
     else:
-        job_bytes, job_ids = float(nbytes), float(n_ids)
+        job_bytes, job_ids, gmax, byte_imbalance = float(nbytes), float(n_ids), gather_s[0], 1.0
 
     ms_step = elapsed / args.steps * 1e3
     value = job_bytes * args.steps / elapsed / 1e6
@@ -199,64 +390,69 @@ def main():
 
     # dominant kernel: per-launch algorithmic bytes / its average launch duration (HIP events the
     # library records around its own launches on the encode stream)
-    kern = max(("count", "emit", "tiles"), key=lambda k: prof[k][0])
+    kern = max(("emit", "tiles", "spm_tiles"), key=lambda k: prof.get(k, (0.0, 0))[0])
     k_ms, k_n = prof[kern]
-    avg_s = k_ms / max(k_n, 1) / 1e3
-    read_bytes = nbytes + 8 * (rows + 1)  # raw UTF-8 rows + u64 row offsets
-    if kern == "count":
-        write_bytes = 4 * rows  # u32 count per row
-    elif kern == "emit":
-        write_bytes = 4 * n_ids + 8 * (rows + 1)  # u32 ids + u64 row offsets
-    else:
-        write_bytes = 4 * n_ids + 4 * rows  # u32 ids into the row slots + u32 count per row
-    algo = read_bytes + write_bytes
-    achieved = algo / avg_s / 1e9 if avg_s > 0 else 0.0
-    kname = {"count": "k_rows_fast<OP_BPE,3,false> (count pass)", "emit": "k_rows_fast<OP_BPE,3,true> (emit pass)",
-             "tiles": "k_bpe_tiles<3> (tile-cooperative encode)"}[kern]
-    traffic, traffic_src = None, None
-    tfile = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
-    if kern == "tiles" and os.path.exists(tfile):
-        t = json.load(open(tfile))
-        if t.get("rows") == rows and t.get("bytes") == nbytes:  # the same launch shape, measured by PMC
-            traffic = int(t["hbm_bytes_per_launch"])
-            traffic_src = "profiles/%s (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same 10 M-row launch)" % TRAFFIC_FILE
+    k_n = max(k_n, 1)
+    avg_s = k_ms / k_n / 1e3
+    launches_per_step = k_n / args.steps
+    rows_l = rows / launches_per_step
+    bytes_l = nbytes / launches_per_step
+    ids_l = n_ids / launches_per_step
+    read_bytes = bytes_l + 8 * (rows_l + 1)  # raw UTF-8 rows + u64 row offsets
+    write_bytes = 4 * ids_l + 4 * rows_l     # u32 ids into the row slots + u32 count per row
+    achieved = read_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(kern, int(round(rows_l)), int(round(bytes_l)))
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": kname,
-                "kernel_avg_ms": round(avg_s * 1e3, 3), "algorithmic_bytes_per_launch": int(algo),
-                "read_frac": round(read_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0,
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": KERNEL_NAMES[kern],
+                "kernel_avg_ms": round(avg_s * 1e3, 3), "launches_per_step": launches_per_step,
+                "achieved_is": "SURVEY.md §8(d) read bytes (sum B + 8 (N + 1)) per launch / average launch time",
+                "read_bytes_per_launch": int(read_bytes),
+                "total_algorithmic_bytes_per_launch": int(read_bytes + write_bytes),
+                "total_frac": round((read_bytes + write_bytes) / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0,
                 "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in prof.items() if v[1]}}
     if traffic_src:
         roofline["traffic_source"] = traffic_src
+        roofline["traffic_over_algorithmic"] = round(traffic / (read_bytes + write_bytes), 3)
     if passes:
         roofline["tile_pass_cycle_frac"] = passes
         roofline["fallback_rows_per_step"] = fb_rows[0]
 
-    others = None
-    if rank == 0 and not args.no_others:
+    others = e2e = cpu = None
+    if rank == 0 and world == 1 and not args.no_others:
         log(rank, "other configs")
         others = other_configs(local)
-
-    cpu = None
-    if rank == 0 and not args.no_cpu:
-        log(rank, "timed region done (%.1f ms/step); CPU baseline" % (elapsed / args.steps * 1e3))
-        cpu = cpu_baseline(args, buf, offs)
+    if rank == 0 and world == 1 and not args.no_e2e:
+        log(rank, "end to end")
+        e2e = end_to_end(local, model, buf, offs, kind)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        log(rank, "timed region done (%.1f ms/step); CPU baseline" % ms_step)
+        cpu = cpu_baseline(args, buf, offs, kind)
 
     if rank == 0:
+        if cfg5:
+            wl = ("cfg5: one batch of %d synthetic Hinglish sentences, byte-balanced contiguous shards over %d GPU(s), "
+                  "normalize_text + 24k unigram SentencePiece encode (models/akshar.model) in chunks of %d rows, "
+                  "+ all-gather of the id streams (N > 1), inputs resident in HBM" % (total_rows, world, args.chunk_rows))
+        else:
+            wl = ("cfg4: %d synthetic Hinglish sentences per GPU, normalize_text + 24k BPE encode (models/akshar.json), "
+                  "inputs resident in HBM" % rows)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic (akshar_amd.synth, seed %d)" % SEED,
-            "tokens_per_s": round(toks, 1),
-            "config": {"workload": "cfg4: %d synthetic Hinglish sentences per GPU, normalize_text + 24k BPE encode "
-                                   "(models/akshar.json), inputs resident in HBM" % rows,
-                       "rows_per_gpu": rows, "bytes_per_gpu": nbytes, "ids_per_gpu": n_ids,
-                       "parallelism": "dp%d (row shards, no data-path collective)" % world},
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "strong" if cfg5 else "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (akshar_amd.synth, seed %d)" % SEED, "tokens_per_s": round(toks, 1),
+            "config": {"workload": wl, "rows_per_gpu": rows, "bytes_per_gpu": nbytes, "ids_per_gpu": n_ids,
+                       "parallelism": ("dp%d (byte-balanced row shards + all-gather)" if cfg5 else
+                                       "dp%d (row shards, no data-path collective)") % world},
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if cfg5 or args.gather:
+            line["gather_ms"] = round(gmax / args.steps * 1e3, 3)
+            line["shard_byte_imbalance"] = round(byte_imbalance, 5)
+        if e2e:
+            line["end_to_end"] = e2e
         if others:
             line["other_configs"] = others
-        if gather_ms is not None:
-            line["gather_ms"] = round(gather_ms, 3)
         print(json.dumps(line), flush=True)
     if dist:
         tdist.barrier()
