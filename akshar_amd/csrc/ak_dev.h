@@ -687,6 +687,8 @@ struct SpmDev {
     int32_t unk_id;
     float unk_score;       // min_score - 10
     float max_score;
+    float abs_score_max;   // largest |score| a lattice node can add (pieces, unk): the tile path's rounding bound
+    uint16_t ws_code;      // tile path W entry of U+2581 (0x8000 | code, or the code point if no piece holds it)
 };
 
 // word chars are stored as 0x80000000 | code for chars some piece holds, the plain code point

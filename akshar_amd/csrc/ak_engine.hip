@@ -211,6 +211,8 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.unk_id = unk_id;
     m->dev.unk_score = t.min_score - 10.0f;
     m->dev.max_score = t.max_score;
+    m->dev.abs_score_max = t.abs_score_max;
+    m->dev.ws_code = t.ws_code;
     *out = m;
     return AK_OK;
 }
@@ -494,7 +496,8 @@ static int dispatch(int op, int flags, ak_ws *w, const RowArgs &a, uint64_t *out
         case OP_BPE:
             return w->bpe_path == 1 && flags == 3 ? launch_bpe_tiles(flags, w, a, out_offs, st)
                                                   : launch_bpe(flags, w, a, out_offs, st);
-        default: return launch_spm(flags, w, a, out_offs, st);
+        default:
+            return w->bpe_path == 1 && flags == 3 ? launch_spm_tiles(w, a, out_offs, st) : launch_spm(flags, w, a, out_offs, st);
     }
 }
 

@@ -14,6 +14,8 @@ static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
 static inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
 static inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
 static inline float __int_as_float(int v) { float f; memcpy(&f, &v, 4); return f; }
+static inline float __uint_as_float(uint32_t v) { float f; memcpy(&f, &v, 4); return f; }
+static inline uint32_t __float_as_uint(float f) { uint32_t v; memcpy(&v, &f, 4); return v; }
 #define __HIP_MEMORY_SCOPE_AGENT 0
 template <class T>
 static inline T __hip_atomic_exchange(T *p, T v, int, int) { return __atomic_exchange_n(p, v, __ATOMIC_SEQ_CST); }

@@ -275,6 +275,7 @@ int launch_switches(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hi
 int launch_bpe(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_spm(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+int launch_spm_tiles(AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 
 struct AnalyzeOut {
     uint8_t *norm; uint64_t norm_cap; uint64_t *norm_offs;

@@ -1,0 +1,151 @@
+// ak_k_spm_tiles.hip — the tile-cooperative SentencePiece encode (ak_tile_spm.h) and its launcher:
+//   k_spm_tiles      every wave encodes whole tiles of rows into per-row staging slots (row r at
+//                    2 offs[r] + 2 r: a row's ids never exceed 2 x its bytes + 1) and writes per-row
+//                    id counts; rare rows (NFC / invalid UTF-8 / over the tile / a close lattice
+//                    call) go to a fallback list
+//   k_spm_tile_fb    fallback rows, one lane per row (ak_rows.h process_row: the exact sequential
+//                    lattice with the carried base), into the same slots; rows past its buffers go
+//   k_rows_tier      ... to the slow and huge tiers (ak_internal.h)
+//   scan_counts      per-row counts -> u64 row offsets (out_offs)
+//   k_tile_copy      staged ids -> ids[out_offs[r] ...]
+#include <stdlib.h>
+
+#include "ak_internal.h"
+#include "ak_tile_spm.h"
+
+namespace ak {
+
+constexpr int SPM_TILE_BLOCK = 256;           // 4 waves per block
+constexpr uint32_t SPM_T_MUL = 2, SPM_T_ADD = 2;  // staging slot of row r: 2 offs[r] + 2 r
+constexpr int SPM_FB_BLOCK = 256;
+
+template <int FLAGS>
+__global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
+    __shared__ uint32_t hot_tab[HOT_N];
+    __shared__ uint16_t scode[HOT_N];
+    __shared__ SpmWaveMem wm[SPM_TILE_BLOCK / 64];
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
+        const uint32_t cp = hot_cp(i);
+        hot_tab[i] = hot_of(prop_global(cp));
+        const uint32_t c = spm_code(ta.ra.spm, cp);
+        scode[i] = (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
+    }
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6;
+    spm_tiles_wave<FLAGS>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
+                          gridDim.x * (SPM_TILE_BLOCK / 64));
+}
+
+// fallback rows with the fast row kernel's private buffers, straight into the row's tile slot
+template <int FLAGS>
+__global__ __launch_bounds__(SPM_FB_BLOCK) void k_spm_tile_fb(TileArgs ta) {
+    __shared__ uint2 fast[FAST_N];
+    __shared__ uint16_t sfast[1];
+    const uint32_t nl = *ta.fb_count;
+    if (nl == 0) return;  // uniform: the common case
+    stage_tables(fast, sfast, nullptr, false);
+    uint32_t seg[FAST_SEG], seg2[FAST_SEG], dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
+    uint32_t vchar[FAST_VCAP];
+    float vbest[FAST_VCAP + 1];
+    int32_t vstart[FAST_VCAP + 1], vid[FAST_VCAP + 1];
+    Scratch sc;
+    small_scratch(sc, seg, seg2, dec, dec2, FAST_SEG);
+    sc.vchar = vchar; sc.vbest = vbest; sc.vstart = vstart; sc.vid = vid; sc.vcap = FAST_VCAP;
+    const RowArgs &a = ta.ra;
+    for (uint32_t i = blockIdx.x * SPM_FB_BLOCK + threadIdx.x; i < nl; i += gridDim.x * SPM_FB_BLOCK) {
+        const uint64_t r = ta.fb_list[i];
+        sc.status = 0;
+        const uint64_t s0 = SPM_T_MUL * a.offs[r] + SPM_T_ADD * r, s1 = SPM_T_MUL * a.offs[r + 1] + SPM_T_ADD * (r + 1);
+        const uint64_t cnt = process_row<OP_SPM, FLAGS, true>(a, r, fast, sfast, &sc, s0, s1);
+        if (sc.status & ST_SLOW) {
+            ta.fb2_list[atomicAdd(ta.fb2_count, 1u)] = (uint32_t)r;
+            continue;
+        }
+        const bool over = cnt > s1 - s0;
+        if (over) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ta.counts[r] = over ? 0u : (uint32_t)cnt;
+        if (a.row_status) a.row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (over ? ST_LIMIT : 0u));
+    }
+}
+
+static int g_spm_blocks_per_cu = 0;
+
+int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t st) {
+    if (a0.n == 0) {
+        HIP_TRY(hipMemsetAsync(out_offs, 0, 8, st));
+        return AK_OK;
+    }
+    int rc = ws_reserve(w, a0.n);
+    if (rc) return rc;
+    uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging area
+    HIP_TRY(hipMemcpyAsync(&nbytes, a0.offs + a0.n, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    rc = ws_stage_reserve(w, SPM_T_MUL * nbytes + SPM_T_ADD * a0.n + 64, st);
+    if (rc) return rc;
+    const int R = w->tile_rows;
+    const uint64_t ntiles = (a0.n + (uint64_t)R - 1) / (uint64_t)R;
+    if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
+        HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
+        HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
+    }
+    if (g_prof_on && !w->tile_passprof) {
+        HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
+        HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
+    }
+    if (!g_spm_blocks_per_cu) {
+        int b = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spm_tiles<3>, SPM_TILE_BLOCK, 0));
+        g_spm_blocks_per_cu = std::max(1, b);
+    }
+    if (w->cap_fb2 < a0.n) {
+        (void)hipFree(w->fb2);
+        w->fb2 = nullptr;
+        HIP_TRY(hipMalloc(&w->fb2, a0.n * 4));
+        w->cap_fb2 = a0.n;
+    }
+    TileArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    ta.ra = a0;
+    ta.ra.out = w->stage;
+    ta.ra.cap = w->cap_stage;
+    ta.ra.out_offs = nullptr;
+    ta.counts = w->counts;
+    ta.fb_list = w->slow_list;
+    ta.fb_count = w->tile_misc;
+    ta.err = w->tile_misc + 1;
+    ta.fb2_list = w->fb2;
+    ta.fb2_count = w->tile_misc + 2;
+    ta.passprof = g_prof_on ? w->tile_passprof : nullptr;
+    ta.ntiles = ntiles;
+    ta.rows = R;
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
+    HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
+    HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
+    const uint64_t wpb = SPM_TILE_BLOCK / 64;
+    int bpc = g_spm_blocks_per_cu;
+    if (const char *e = getenv("AK_SPM_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));  // development aid
+    const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)num_cus() * (uint64_t)bpc);
+    AK_PROF(AK_PROF_SPM_TILES, false, st);
+    k_spm_tiles<3><<<grid, SPM_TILE_BLOCK, 0, st>>>(ta);
+    AK_PROF(AK_PROF_SPM_TILES, true, st);
+    HIP_TRY(hipGetLastError());
+    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
+    k_spm_tile_fb<3><<<(unsigned)num_cus(), SPM_FB_BLOCK, 0, st>>>(ta);
+    RowArgs ra = ta.ra;
+    ra.counts = w->counts;
+    ra.err = w->ctr + CTR_ERR;
+    k_rows_tier<OP_SPM, 3><<<SLOW_THREADS / 64, 64, 0, st>>>(ra, SPM_T_MUL, SPM_T_ADD, slow_tier(w, w->fb2, ta.fb2_count));
+    HIP_TRY(hipGetLastError());
+    rc = run_huge_tier(w, a0.offs, st, [&](const Tier &t, unsigned blocks) {
+        k_rows_tier<OP_SPM, 3><<<blocks, 64, 0, st>>>(ra, SPM_T_MUL, SPM_T_ADD, t);
+    });
+    if (rc) return rc;
+    AK_PROF(AK_PROF_EMIT_SLOW, true, st);
+    AK_PROF(AK_PROF_SCAN, false, st);
+    rc = scan_counts(w, a0.n, out_offs, st);
+    if (rc) return rc;
+    AK_PROF(AK_PROF_SCAN, true, st);
+    return launch_stage_copy(w, a0.offs, out_offs, a0.n, (uint32_t *)a0.out, a0.cap, SPM_T_MUL, SPM_T_ADD, st);
+}
+
+}  // namespace ak

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 #include <utility>
 #include <vector>
@@ -108,6 +109,8 @@ struct SpmTables {
     std::vector<uint16_t> cmap;       // pages of 128 codes; page 0 all zero
     std::vector<uint32_t> code_cp;    // code -> code point (code 0 unused)
     float min_score = 0, max_score = 0;
+    float abs_score_max = 0;          // largest |score| one lattice node adds (normal, user defined, unk)
+    uint16_t ws_code = 0;             // tile-path W entry of U+2581 (0x8000 | code, or 0x2581 if no piece holds it)
 };
 
 constexpr uint32_t SPM_CMAP_PAGES = 0x110000u >> 7;
@@ -256,6 +259,18 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
     out.root_base = base[0];
     out.min_score = min_score;
     out.max_score = max_score;
+    // the tile path's rounding bound (ak_tile_spm.h): normal scores, user-defined scores
+    // (length x max_score - 0.1, as the lattice computes them) and the unk score (min - 10)
+    double amax = std::fabs((double)(min_score - 10.0f));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (types[i] == 1) amax = std::max(amax, std::fabs((double)scores[i]));
+        else if (types[i] == 4)
+            amax = std::max(amax, std::fabs((double)((float)(piece_offs[i + 1] - piece_offs[i]) * max_score) - 0.1));
+    }
+    out.abs_score_max = (float)(amax * (1.0 + 1e-6));
+    const uint16_t wpg = out.cmap_page[0x2581u >> 7];
+    const uint16_t wc = wpg ? out.cmap[(size_t)wpg * 128 + (0x2581u & 127u)] : 0;
+    out.ws_code = wc ? (uint16_t)(0x8000u | wc) : (uint16_t)0x2581u;
     return "";
 }
 

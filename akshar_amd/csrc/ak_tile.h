@@ -248,19 +248,34 @@ __device__ __forceinline__ int bpe_merge_lds(const BpeDev &m, uint16_t *W, int s
     return n;
 }
 
-template <int FLAGS>
-__device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *sfast,
-                        TileWaveMem &M, PassClock &pc) {
-    static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
+// Rows [r0, k) of the tile that fit the BCAP-byte buffer (k = 0: the single row r0 is over it and
+// goes to the fallback kernels), their staged bytes' aligned base a0, and the length of V.
+struct TileRows {
+    int k;          // rows staged (0 or more)
+    int nr;         // rows this call consumes: k, or 1 when row r0 alone is over the buffer
+    uint64_t S0;    // byte offset of row r0
+    uint64_t a0;    // S0 rounded down to 16
+    uint32_t vlen;  // entries of V
+};
+
+// Shared front end of the tile kernels (BPE, SentencePiece):
+//   stage: 16-byte coalesced loads of the tile's bytes into LDS;
+//   D1: per row, 64 bytes per step: the positions of the UTF-8 lead bytes -> P (in M.w);
+//   D2: the whole tile's chars, 64 per step: decode, hot word, nfc_trig, normalize_text map -> V
+//       (M.v) with V_B / V_E sentinels around each row.
+// A row whose NFC quick check trips or that holds invalid UTF-8 is marked in M.fb (the caller sends
+// it to the fallback kernels). Row r's staging slot starts at slot_mul * (offs[r] - S0) +
+// slot_add * (r - r0) relative to the tile's slot base (M.rowslot).
+template <int BCAP, class Mem>
+__device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, uint64_t rend, const uint32_t *H, Mem &M,
+                                               uint32_t slot_mul, uint32_t slot_add) {
     const int lane = w_lane();
-    const RowArgs &a = ta.ra;
-    const BpeDev &m = a.bpe;
     const int nr0 = (int)(rend - r0);
     const uint64_t myoff = lane <= nr0 ? a.offs[r0 + lane] : 0ull;
     const uint64_t S0 = w_bcast(myoff, 0);
-    const bool fits = lane >= 1 && lane <= nr0 && (myoff - S0) <= (uint64_t)T_BCAP;
+    const bool fits = lane >= 1 && lane <= nr0 && (myoff - S0) <= (uint64_t)BCAP;
     const int k = w_popc(w_ballot(fits));  // rows 0..k-1 fit the tile buffer
-    // rows past the buffer are the caller's next sub-tile; a single row over T_BCAP bytes falls back
+    // rows past the buffer are the caller's next sub-tile; a single row over BCAP bytes falls back
     const int nr = k ? k : 1;
     const uint64_t S1 = w_bcast(myoff, k);
     const uint64_t a0 = S0 & ~15ull;
@@ -274,13 +289,12 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     if (lane < nr) {
         M.fb[lane] = lane >= k ? 1 : 0;
         M.rowend[lane] = (uint16_t)(nextoff - a0);
-        M.rowslot[lane] = (uint32_t)(myoff - S0) + 2u * (uint32_t)lane;
+        M.rowslot[lane] = slot_mul * (uint32_t)(myoff - S0) + slot_add * (uint32_t)lane;
     }
     w_sync();
 
-    pc.mark(TP_STAGE);
     // ---------------- pass D1: per row, 64 bytes per step: the positions of the UTF-8 lead bytes ->
-    // P (in W, free until pass N), each row opened by a mark entry. A row that starts with a
+    // P (in W, free until the next pass), each row opened by a mark entry. A row that starts with a
     // continuation byte is invalid UTF-8: fallback (stray continuation bytes inside a row are caught
     // in D2: the chars' lengths must tile the row).
     uint16_t *P = M.w;
@@ -308,7 +322,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     // window), hot word, nfc_trig against the previous char (a mark = row start), then the
     // normalize_text map (lower / allowlist) -> V with <s>/</s> sentinels around each row. If no
     // char of a row trips nfc_trig, NFC is the identity on it; a row that trips is marked for the
-    // fallback kernels (pass F skips it).
+    // fallback kernels.
     uint32_t vpos = 0;
     {
         uint32_t carry_h = H_ROWSTART, rows = 0;
@@ -355,8 +369,22 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             ++vpos;
         }
     }
-    const uint32_t vlen = vpos;
     w_sync();
+    return TileRows{k, nr, S0, a0, vpos};
+}
+
+template <int FLAGS>
+__device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *sfast,
+                        TileWaveMem &M, PassClock &pc) {
+    static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
+    const int lane = w_lane();
+    const RowArgs &a = ta.ra;
+    const BpeDev &m = a.bpe;
+    pc.mark(TP_STAGE);
+    const TileRows tr = tile_front<T_BCAP>(a, r0, rend, H, M, 1u, 2u);
+    const int nr = tr.nr;
+    const uint64_t S0 = tr.S0;
+    const uint32_t vlen = tr.vlen;
 
     pc.mark(TP_D);
     // ---------------- pass N (fused): remove_elongations, HF NFKC, Whitespace pre-tokenizer and

@@ -1,0 +1,308 @@
+// ak_tile_spm.h — tile-cooperative SentencePiece unigram encode.
+//
+// One wave64 owns a tile of consecutive rows (<= S_BCAP bytes). The shared front end (ak_tile.h
+// tile_front: stage, decode, NFC proof, normalize_text map) produces V; then
+//   W  elongation collapse + the identity normalizer's whitespace rule (strip, collapse, dummy
+//      prefix, ' ' -> "▁") + the SPM code of every char, compacted into W; word starts ("▁")
+//      listed with their rows
+//   V  lane per "▁word": the unigram Viterbi over the word (the code-point trie in HBM / L2,
+//      best / back per position in LDS), backtrack into forward links
+//   F  ids (pieces; byte fallback for unk chars) into each row's staging slot, per-row counts
+// Words run in parallel from base 0 instead of from the row's carried float score. The carried base
+// only enters a word's decisions through float rounding, so a word whose every lattice node's
+// winner beats the other candidates by more than a rounding bound tau (below) makes the same
+// decisions from any base the row can carry; a row with a closer call goes to the exact sequential
+// row kernels (ak_dev.h SpmSink), which carry the base as sentencepiece does. The result is
+// bit-identical to the reference either way (tests: golden, near-tie rows, oracle at scale).
+//
+// tau: at node e every candidate's value under base b differs from its base-0 value + b by at most
+// (depth + 1) (ulp_M + ulp_0) / 2 (one rounding per stored score), and the leader is stored as a
+// float (+ ulp_M / 2). With M >= every |score| the row can reach by this word's end (chars from the
+// row start x the largest |piece or unk score|), ulp_M, ulp_0 <= M 2^-23, and the running check
+// (each candidate against the leader's stored value, which is <= the true margin + ulp_0 / 2),
+// tau = (L + 3) M 2^-22 for a word of L chars is sufficient.
+// Reference semantics: normalize.py:117-148, tokenizer.py:190-191, cli.py:232-248.
+#pragma once
+#include "ak_tile.h"
+
+namespace ak {
+
+constexpr int S_BCAP = 512;                 // staged bytes per tile
+constexpr int S_E = S_BCAP + 2 * T_MAXR + 64;  // entries of V
+constexpr int S_W = S_E + T_MAXR + 16;      // entries of W (chars, "▁", row sentinels)
+constexpr int S_WORDS = 256;                // words per tile (more: the tile's rows fall back)
+
+constexpr uint16_t W_CODED = 0x8000;  // W entry: 0x8000 | dense code (a char some piece holds), else the code point
+constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: the trie walk stops there)
+constexpr uint16_t W_END = 0x7FFF;
+constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
+
+struct SpmWaveMem {
+    alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
+    uint16_t v[S_E];                         // V; after pass W: nxt (u8 per W position)
+    uint16_t w[S_W];                         // P (pass D1), then W
+    float best[S_W];                         // Viterbi best score per W position (word-local)
+    uint32_t back[S_W];                      // best piece ending here: id << 8 | chars
+    uint8_t wrow[S_WORDS];                   // row of each word
+    uint8_t fb[T_MAXR];
+    uint16_t rowend[T_MAXR];
+    uint32_t rowslot[T_MAXR];
+    uint16_t rowpos[T_MAXR + 1];             // W position of each row's W_B (+ end)
+    uint32_t rowcnt[T_MAXR];
+    uint32_t rowfirst[T_MAXR];               // tile-stream position of the row's first id
+    uint64_t passacc[10];
+};
+static_assert(S_WORDS * 2 <= S_BCAP + 32, "word starts live in the byte buffer");
+static_assert(S_W + 2 * S_WORDS <= 2 * S_E, "nxt + word id counts live in V");
+
+// W entry of a normalized char: LDS code table for the hot range, the model's paged map otherwise
+__device__ __forceinline__ uint16_t spm_wcode(const SpmDev &m, const uint16_t *scode, uint32_t cp) {
+    if (cp < HOT_LO) return scode[cp];
+    if (cp - 0x900u < 0x100u) return scode[cp - 0x900u + HOT_LO];
+    const uint32_t c = spm_code(m, cp);
+    return (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
+}
+
+__device__ __forceinline__ uint32_t spm_wcp(const SpmDev &m, uint16_t x) {
+    return (x & W_CODED) ? m.code_cp[x & 0x7FFFu] : (uint32_t)x;
+}
+
+template <int FLAGS>
+__device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
+                        SpmWaveMem &M, PassClock &pc) {
+    static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
+    const int lane = w_lane();
+    const RowArgs &a = ta.ra;
+    const SpmDev &m = a.spm;
+    pc.mark(TP_STAGE);
+    const TileRows tr = tile_front<S_BCAP>(a, r0, rend, H, M, 2u, 2u);
+    const int nr = tr.nr;
+    const uint32_t vlen = tr.vlen;
+    pc.mark(TP_D);
+
+    // ---------------- pass W: elongation (drop x when x == prev and (prev == prev2 or next == x),
+    // '\n' exempt), then the identity normalizer over the kept elements: a non-space char is
+    // preceded by "▁" iff the previous kept element is ' ' or the row start (strip + collapse +
+    // dummy prefix; spaces themselves vanish), chars -> W codes; word starts -> the word list.
+    uint16_t *starts = (uint16_t *)M.bytes;
+    uint8_t *nxt = (uint8_t *)M.v;            // after this pass
+    uint8_t *wrow = M.wrow;
+    uint32_t wlen = 0, nw = 0;
+    {
+        uint16_t carry = V_B;
+        uint32_t rs = 0;
+        for (uint32_t base = 0; base < vlen; base += 64) {
+            const uint32_t kk = base + (uint32_t)lane;
+            const bool in = kk < vlen;
+            const uint16_t x = in ? M.v[kk] : V_DEAD;
+            const uint16_t pa = in && kk >= 1 ? M.v[kk - 1] : V_DEAD;
+            const uint16_t pb = in && kk >= 2 ? M.v[kk - 2] : V_DEAD;
+            const uint16_t nx = in && kk + 1 < vlen ? M.v[kk + 1] : V_DEAD;
+            const bool special = x >= V_SPECIAL;
+            const bool drop = in && !special && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
+            const bool keep = in && !drop;
+            const uint64_t KM = w_ballot(keep);
+            const uint64_t pk = KM & w_lanemask_lt();
+            const uint16_t xl = (uint16_t)w_shfl((uint32_t)x, pk ? msb64(pk) : 0);
+            const uint16_t prevk = pk ? xl : carry;
+            const uint64_t RM = w_ballot(keep && x == V_B);
+            const uint32_t row = rs + w_rank_incl(RM) - 1;
+            const bool ischar = keep && !special && x != (uint16_t)' ';
+            const bool ws = ischar && (prevk == (uint16_t)' ' || prevk == V_B);
+            const uint32_t cnt = ischar ? (ws ? 2u : 1u) : (keep && special ? 1u : 0u);
+            const uint16_t code = ischar ? spm_wcode(m, scode, x) : (uint16_t)0;
+            uint32_t tot;
+            const uint32_t ex = w_exscan(cnt, &tot);
+            const uint32_t p = wlen + ex;
+            if (ischar) {
+                if (ws) M.w[p] = m.ws_code;
+                M.w[p + (ws ? 1 : 0)] = code;
+            } else if (keep && special) {
+                M.w[p] = x == V_B ? W_B : W_END;
+                if (x == V_B) M.rowpos[row] = (uint16_t)p;
+            }
+            const uint64_t WM = w_ballot(ws);
+            const uint32_t j = nw + w_rank(WM);
+            if (ws && j < (uint32_t)S_WORDS) { starts[j] = (uint16_t)p; wrow[j] = (uint8_t)row; }
+            nw += (uint32_t)w_popc(WM);
+            wlen += tot;
+            rs += (uint32_t)w_popc(RM);
+            if (KM) carry = (uint16_t)w_bcast((uint32_t)x, msb64(KM));
+        }
+        if (lane == 0) M.rowpos[rs] = (uint16_t)wlen;
+        if (nw > (uint32_t)S_WORDS || wlen > (uint32_t)S_W) {  // never in text: the tile's rows fall back
+            if (lane < nr) M.fb[lane] = 1;
+            nw = 0;
+        }
+        if (lane < nr) { M.rowcnt[lane] = 0; M.rowfirst[lane] = 0; }
+    }
+    w_sync();
+    pc.mark(TP_E);
+
+    // ---------------- pass V: lane per word, Viterbi from base 0 with the running margin check,
+    // backtrack into forward links nxt[s] = chars of the piece at s; the word's id count -> wcnt.
+    // A word owns best / back at (p0, p1] (its start node p0 is the previous word's end node: the
+    // base 0 stays in a register) and nxt at [p0, p1).
+    uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
+    for (uint32_t jb = 0; jb < nw; jb += 64) {
+        const uint32_t j = jb + (uint32_t)lane;
+        const bool act = j < nw;
+        const int row = act ? (int)wrow[j] : 0;
+        const int p0 = act ? (int)starts[j] : 0;
+        int p1 = 0;
+        if (act) p1 = (j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1;
+        for (int i = p0 + 1; i <= p1; ++i) M.back[i] = BK_NONE;
+        float minm = 3.0e38f;
+        for (int s = p0; s < p1; ++s) {
+            const float till = s == p0 ? 0.0f : M.best[s];
+            bool has_single = false;
+            int node = 0, nb = m.root_base;
+            for (int k = s; k < p1; ++k) {
+                const uint32_t v = M.w[k];
+                if (!(v & W_CODED)) break;
+                const int t = nb + (int)(v & 0x7FFFu);
+                const int4 e = m.trie[t];
+                if (e.x != node) break;
+                node = t;
+                nb = e.y;
+                const int value = e.z;
+                if (value < 0) continue;
+                const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
+                if (kind == 2) continue;
+                const int id = value & 0xFFFFFF;
+                const double score = kind == 1 ? (double)((float)e.w * m.max_score) - 0.1 : (double)__int_as_float(e.w);
+                const double cand = score + (double)till;
+                const int ee = k + 1;
+                const uint32_t bk = M.back[ee];
+                if (bk == BK_NONE || cand > (double)M.best[ee]) {
+                    if (bk != BK_NONE) minm = fminf(minm, (float)(cand - (double)M.best[ee]));
+                    M.best[ee] = (float)cand;
+                    M.back[ee] = ((uint32_t)id << 8) | (uint32_t)(ee - s);
+                } else {
+                    minm = fminf(minm, (float)((double)M.best[ee] - cand));
+                }
+                if (k == s) has_single = true;  // sentencepiece: a piece of exactly the first char
+            }
+            if (!has_single) {
+                const int ee = s + 1;
+                const float cand = m.unk_score + till;
+                const uint32_t bk = M.back[ee];
+                if (bk == BK_NONE || cand > M.best[ee]) {
+                    if (bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
+                    M.best[ee] = cand;
+                    M.back[ee] = ((uint32_t)m.unk_id << 8) | 1u;
+                } else {
+                    minm = fminf(minm, M.best[ee] - cand);
+                }
+            }
+        }
+        if (act) {
+            // rounding bound of this word (header comment): M = (chars from the row start to the word
+            // end + 1) x the largest |score|
+            const float Mb = (float)(p1 - (int)M.rowpos[row] + 1) * m.abs_score_max + 1.0f;
+            const float tau = (float)(p1 - p0 + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
+            if (!(minm > tau)) M.fb[row] = 1;
+            uint32_t cnt = 0;
+            for (int e = p1; e > p0;) {
+                const uint32_t bk = M.back[e];
+                const int d = (int)(bk & 0xFFu);
+                const int s = e - d;
+                nxt[s] = (uint8_t)d;
+                const int id = (int)(bk >> 8);
+                cnt += id == m.unk_id ? (uint32_t)utf8_len(spm_wcp(m, M.w[s])) : 1u;
+                e = s;
+            }
+            wcnt[j] = (uint16_t)cnt;
+        }
+    }
+    w_sync();
+    pc.mark(TP_B);
+
+    // ---------------- fallback rows: append to the list (rare: one atomic per tile that has any)
+    {
+        const bool isfb = lane < nr && M.fb[lane];
+        const uint64_t FM = w_ballot(isfb);
+        if (FM) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(ta.fb_count, (uint32_t)w_popc(FM));
+            base = w_bcast(base, 0);
+            if (isfb) ta.fb_list[base + w_rank(FM)] = (uint32_t)(r0 + (uint64_t)lane);
+        }
+    }
+    pc.mark(TP_FBC);
+
+    // ---------------- pass F: ids -> each row's staging slot (a word's ids follow its row's earlier
+    // words), per-row counts
+    const uint64_t sbase = 2 * tr.S0 + 2 * r0;
+    uint32_t *stage = (uint32_t *)a.out + sbase;
+    const uint64_t scap = a.cap > sbase ? a.cap - sbase : 0;
+    bool over = false;
+    uint32_t pos = 0;
+    for (uint32_t jb = 0; jb < nw; jb += 64) {
+        const uint32_t j = jb + (uint32_t)lane;
+        const bool act = j < nw;
+        const int row = act ? (int)wrow[j] : 0;
+        const bool live = act && !M.fb[row];
+        const int p0 = act ? (int)starts[j] : 0;
+        const uint32_t c = live ? (uint32_t)wcnt[j] : 0u;
+        uint32_t tot;
+        const uint32_t P = pos + w_exscan(c, &tot);
+        const bool first = act && (j == 0 || (int)wrow[j - 1] != row);
+        const bool last_of_row = !(j + 1 < nw && (int)wrow[j + 1] == row);
+        if (live && first) M.rowfirst[row] = P;
+        w_sync();
+        if (live && last_of_row) M.rowcnt[row] = P + c - M.rowfirst[row];  // a row's words are consecutive
+        if (live) {
+            const int p1 = !last_of_row ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1;
+            uint64_t d = (uint64_t)M.rowslot[row] + (P - M.rowfirst[row]);
+            for (int s = p0; s < p1;) {
+                const int e = s + (int)nxt[s];
+                const uint32_t id = M.back[e] >> 8;
+                if ((int)id == m.unk_id) {  // an unk node is one char: byte fallback
+                    const uint32_t cp = spm_wcp(m, M.w[s]);
+                    const int cl = utf8_len(cp);
+                    uint32_t bytes[4];
+                    if (cl == 1) { bytes[0] = cp; }
+                    else if (cl == 2) { bytes[0] = 0xC0u | (cp >> 6); bytes[1] = 0x80u | (cp & 63u); }
+                    else if (cl == 3) { bytes[0] = 0xE0u | (cp >> 12); bytes[1] = 0x80u | ((cp >> 6) & 63u); bytes[2] = 0x80u | (cp & 63u); }
+                    else { bytes[0] = 0xF0u | (cp >> 18); bytes[1] = 0x80u | ((cp >> 12) & 63u); bytes[2] = 0x80u | ((cp >> 6) & 63u); bytes[3] = 0x80u | (cp & 63u); }
+                    for (int q = 0; q < cl; ++q, ++d) {
+                        if (d < scap) stage[d] = (uint32_t)m.byte_ids[bytes[q]];
+                        else over = true;
+                    }
+                } else {
+                    if (d < scap) stage[d] = id;
+                    else over = true;
+                    ++d;
+                }
+                s = e;
+            }
+        }
+        pos += tot;
+    }
+    if (w_ballot(over) && lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    w_sync();
+    if (lane < nr && !M.fb[lane]) {
+        ta.counts[r0 + lane] = M.rowcnt[lane];
+        if (a.row_status) a.row_status[r0 + lane] = 0;
+    }
+    w_sync();
+    pc.mark(TP_F);
+    return nr;
+}
+
+template <int FLAGS>
+__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M,
+                               uint32_t wave_gid, uint32_t nwaves) {
+    PassClock pc;
+    pc.init(ta.passprof != nullptr, M.passacc);
+    for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {
+        pc.mark(TP_LOOP);
+        const uint64_t r0 = t * (uint64_t)ta.rows;
+        const uint64_t r1 = r0 + (uint64_t)ta.rows < ta.ra.n ? r0 + (uint64_t)ta.rows : ta.ra.n;
+        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r1, H, scode, M, pc);
+    }
+    pc.flush(ta.passprof);
+}
+
+}  // namespace ak

@@ -197,14 +197,15 @@ import os as _os
 
 # 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (staged row kernel); AK_BPE_PATH overrides
 BPE_PATH = int(_os.environ.get("AK_BPE_PATH", "1"))
-TILE_BYTES = 560  # target bytes of text per wave-tile (the tile buffer holds 768)
+TILE_BYTES = 560      # BPE: target bytes of text per wave-tile (the tile buffer holds 768)
+SPM_TILE_BYTES = 380  # SentencePiece: target bytes per tile (the tile buffer holds 512)
 
 
-def tile_rows_for(n, nbytes):
+def tile_rows_for(n, nbytes, target=TILE_BYTES):
     if n == 0:
         return 8
     avg = max(nbytes / n, 1.0)
-    return int(min(16, max(1, round(TILE_BYTES / avg))))
+    return int(min(16, max(1, round(target / avg))))
 
 
 class BPE:
@@ -269,8 +270,10 @@ class SPM:
         if h:
             _lib.lib().ak_spm_free(h)
 
-    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, out=None, out_offs=None):
-        """Device rows -> (int32 ids, int64 row offsets); `out` / `out_offs` as BPE.encode_batch."""
+    def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, out=None, out_offs=None,
+                     path=None):
+        """Device rows -> (int32 ids, int64 row offsets); `out` / `out_offs` as BPE.encode_batch.
+        path 1 = tile-cooperative kernel (flags 3), 0 = the staged row kernel."""
         n = _check_inputs(buf, offs)
         dev = buf.device
         ws = workspace(dev.index)
@@ -278,6 +281,8 @@ class SPM:
             nbytes = int(offs[-1].item()) if n else 0
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
+        path = BPE_PATH if path is None else path
+        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows_for(n, nbytes, SPM_TILE_BYTES)), "ak_ws_set_tiling")
 
         def call(out, c, oo):
             check(_lib.lib().ak_spm_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),

@@ -14,6 +14,7 @@
 #include "../../akshar_amd/csrc/ak_model_build.h"
 #include "../../akshar_amd/csrc/ak_rows.h"
 #include "../../akshar_amd/csrc/ak_tile.h"
+#include "../../akshar_amd/csrc/ak_tile_spm.h"
 
 #include <thread>
 
@@ -59,6 +60,8 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->sdev.unk_id = unk_id;
     m->sdev.unk_score = m->spm.min_score - 10.0f;
     m->sdev.max_score = m->spm.max_score;
+    m->sdev.abs_score_max = m->spm.abs_score_max;
+    m->sdev.ws_code = m->spm.ws_code;
     return m;
 }
 
@@ -222,5 +225,73 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
     for (uint64_t r = 0; r < n; ++r)
         for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = stage[offs[r] + 2 * r + i];
+    return (int64_t)out_offs[n];
+}
+
+// ------------------------------------------------------------------------------------------
+// tile-cooperative SentencePiece kernel: one emulated wave, then the fallback rows through the
+// sequential row pipeline into the same slots (2 offs[r] + 2 r), scan and copy
+
+extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
+                                 uint32_t *out, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, int rows) {
+    EmuModel *m = (EmuModel *)model;
+    if (flags != 3) return -1;
+    static uint2 fast[FAST_N];
+    static uint32_t hot_tab[HOT_N];
+    static uint16_t scode[HOT_N];
+    for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
+    for (uint32_t i = 0; i < HOT_N; ++i) {
+        const uint32_t cp = hot_cp(i);
+        hot_tab[i] = hot_of(prop_global(cp));
+        const uint32_t c = spm_code(m->sdev, cp);
+        scode[i] = (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
+    }
+    if (n == 0) { out_offs[0] = 0; return 0; }
+    std::vector<uint32_t> stage(2 * offs[n] + 2 * n + 64), counts(n), fbl(n), fb2(n);
+    uint32_t fbn = 0, fb2n = 0, err = 0;
+    TileArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = stage.size();
+    ta.ra.row_status = row_status; ta.ra.spm = m->sdev;
+    ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
+    ta.fb2_count = &fb2n; ta.err = &err;
+    ta.ntiles = (n + rows - 1) / rows; ta.rows = rows;
+    SpmWaveMem *M = new SpmWaveMem();
+    EmuWave W;
+    std::vector<std::thread> th;
+    for (int lane = 0; lane < 64; ++lane)
+        th.emplace_back([&, lane] {
+            t_lane = lane;
+            t_wave = &W;
+            spm_tiles_wave<3>(ta, hot_tab, scode, *M, 0, 1);
+        });
+    for (auto &x : th) x.join();
+    delete M;
+    if (err) return -1;
+    g_last_fb = fbn;
+    if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
+    uint64_t maxlen = 0;
+    for (uint64_t r = 0; r < n; ++r) maxlen = std::max<uint64_t>(maxlen, offs[r + 1] - offs[r]);
+    const uint64_t C = std::max<uint64_t>(SLOW_CAP, 3 * maxlen + 64);
+    std::vector<uint32_t> seg(2 * C), dec(8 * C), vchar(C);
+    std::vector<float> vbest(C + 1);
+    std::vector<int32_t> vstart(C + 1), vid(C + 1);
+    for (uint32_t i = 0; i < fbn; ++i) {
+        const uint64_t r = fbl[i];
+        Scratch sc;
+        sc.seg = seg.data(); sc.dec = dec.data(); sc.seg2 = seg.data() + C; sc.dec2 = dec.data() + 4 * C;
+        sc.seg_cap = (int)C; sc.wsym = nullptr; sc.wpair = nullptr; sc.heap = nullptr; sc.link = nullptr; sc.word_cap = 0;
+        sc.vchar = vchar.data(); sc.vbest = vbest.data(); sc.vstart = vstart.data(); sc.vid = vid.data(); sc.vcap = (int)C;
+        sc.slow_status = ST_LIMIT; sc.status = 0;
+        const uint64_t s0 = 2 * offs[r] + 2 * r, s1 = 2 * offs[r + 1] + 2 * (r + 1);
+        const uint64_t cnt = process_row<OP_SPM, 3, true>(ta.ra, r, fast, nullptr, &sc, s0, s1);
+        if ((sc.status & ST_LIMIT) || cnt > s1 - s0) return -2;
+        counts[r] = (uint32_t)cnt;
+        if (row_status) row_status[r] = (uint8_t)(sc.status & ST_BAD_UTF8);
+    }
+    out_offs[0] = 0;
+    for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
+    for (uint64_t r = 0; r < n; ++r)
+        for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = stage[2 * offs[r] + 2 * r + i];
     return (int64_t)out_offs[n];
 }

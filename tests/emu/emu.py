@@ -16,7 +16,7 @@ def lib():
         so = os.path.join(HERE, "_emu.so")
         srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
                                                    ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h",
-                                                    "ak_tile.h", "ak_wave.h")]
+                                                    "ak_tile.h", "ak_tile_spm.h", "ak_wave.h")]
         srcs.append(os.path.join(HERE, "..", "..", "include", "akshar.h"))
         if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
             subprocess.check_call(["g++", "-O2", "-std=c++20", "-pthread", "-fPIC", "-shared", "-I",
@@ -29,6 +29,8 @@ def lib():
         L.emu_free.argtypes = [P]
         L.emu_bpe_tiles.restype = ctypes.c_int64
         L.emu_bpe_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
+        L.emu_spm_tiles.restype = ctypes.c_int64
+        L.emu_spm_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
         L.emu_last_fallback_rows.restype = ctypes.c_uint32
         L.emu_run.restype = ctypes.c_int64
         L.emu_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_uint64, P, P,
@@ -89,6 +91,21 @@ def bpe_tiles(model, buf, offs, flags=3, rows=8):
     oo = np.zeros(n + 1, dtype=np.uint64)
     st = np.zeros(max(n, 1), dtype=np.uint8)
     tot = lib().emu_bpe_tiles(model.h, flags, buf.ctypes.data, offs.ctypes.data, n, out.ctypes.data, cap,
+                              oo.ctypes.data, st.ctypes.data, rows)
+    assert 0 <= tot <= cap, tot
+    return out[:tot], oo, st[:n]
+
+
+def spm_tiles(model, buf, offs, flags=3, rows=4):
+    """The tile-cooperative SentencePiece kernel on one emulated wave -> (ids, out_offs, row_status)."""
+    buf = pad(buf)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    n = len(offs) - 1
+    cap = int(offs[-1]) * 3 + 4 * n + 64
+    out = np.zeros(cap, dtype=np.uint32)
+    oo = np.zeros(n + 1, dtype=np.uint64)
+    st = np.zeros(max(n, 1), dtype=np.uint8)
+    tot = lib().emu_spm_tiles(model.h, flags, buf.ctypes.data, offs.ctypes.data, n, out.ctypes.data, cap,
                               oo.ctypes.data, st.ctypes.data, rows)
     assert 0 <= tot <= cap, tot
     return out[:tot], oo, st[:n]

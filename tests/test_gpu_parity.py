@@ -60,8 +60,10 @@ def test_bpe_golden(golden, gpacked, eng, bpe_model, path):
     assert _bad(golden, "bpe", rows_ints(_cpu(ids), _cpu(oo))) == []
 
 
-def test_spm_golden(golden, gpacked, eng, spm_model):
-    ids, oo = eng.SPM(spm_model).encode_batch(*gpacked)
+@pytest.mark.parametrize("path", [1, 0])
+def test_spm_golden(golden, gpacked, eng, spm_model, path):
+    """path 1 = tile-cooperative kernel (word-parallel lattice), 0 = the staged row kernel."""
+    ids, oo = eng.SPM(spm_model).encode_batch(*gpacked, path=path)
     assert _bad(golden, "spm", rows_ints(_cpu(ids), _cpu(oo))) == []
 
 
@@ -100,10 +102,11 @@ def test_synthetic_vs_oracle(eng, bpe_model, spm_model, kind, n, seed):
         ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, path=path)
         assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
         assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
-    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
     ref, ro = O.OracleSPM(spm_model).encode_batch(*ob)
-    assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
-    assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    for path in (1, 0):
+        ids, oo = eng.SPM(spm_model).encode_batch(gb, go, path=path)
+        assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+        assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
 
 
 def test_empty_batch_and_empty_rows(eng, bpe_model, spm_model):
@@ -128,9 +131,10 @@ def test_long_rows_take_the_slow_path(eng, bpe_model, spm_model):
     for path in (1, 0):
         ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, path=path)
         assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
-    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
     ref, ro = O.OracleSPM(spm_model).encode_batch(*ob)
-    assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
+    for path in (1, 0):
+        ids, oo = eng.SPM(spm_model).encode_batch(gb, go, path=path)
+        assert rows_ints(_cpu(ids), _cpu(oo)) == rows_ints(ref, ro)
     for flags in (0, 3):
         out, oo = eng.normalize_batch(gb, go, flags=flags)
         ref, ro = O.normalize_batch(*ob, flags=flags)
@@ -190,13 +194,16 @@ def test_flag_variants_golden(golden, gpacked, eng, bpe_model, spm_model, key, f
 
 
 def test_spm_large_batch_vs_oracle(eng, spm_model):
-    """200 k Hinglish rows through the SPM encode (config 5's kernel) == the oracle, row by row."""
+    """200 k Hinglish rows through the SPM encode (config 5's kernel) == the oracle, row by row;
+    the tile path sends almost no row to the sequential kernels."""
     buf, offs = _synth(1, 200000, 4321)
     gb, go = _to_dev(eng, buf, offs)
     ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
+    fb, _ = eng.fallback_rows()
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
     assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
     assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    assert fb < 200000 // 100
 
 
 def test_large_batch_property(eng, bpe_model):
