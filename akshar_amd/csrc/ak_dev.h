@@ -684,6 +684,7 @@ struct SpmDev {
     const uint32_t *code_cp;    // code -> cp
     const int32_t *byte_ids;
     int32_t root_base;
+    uint32_t n_nodes;
     int32_t unk_id;
     float unk_score;       // min_score - 10
     float max_score;

@@ -207,6 +207,7 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.cmap = m->d_cmap;
     m->dev.code_cp = m->d_code_cp;
     m->dev.root_base = t.root_base;
+    m->dev.n_nodes = t.n_nodes;
     m->dev.byte_ids = m->d_byte_ids;
     m->dev.unk_id = unk_id;
     m->dev.unk_score = t.min_score - 10.0f;

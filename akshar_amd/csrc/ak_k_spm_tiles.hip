@@ -17,13 +17,15 @@ namespace ak {
 
 constexpr int SPM_TILE_BLOCK = 256;           // 4 waves per block
 constexpr uint32_t SPM_T_MUL = 2, SPM_T_ADD = 2;  // staging slot of row r: 2 offs[r] + 2 r
-constexpr int SPM_FB_BLOCK = 256;
+constexpr int SPM_FB_BLOCK = 64;
 
 template <int FLAGS>
 __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
+    __shared__ int4 root[SPM_ROOT_CAP];
     __shared__ SpmWaveMem wm[SPM_TILE_BLOCK / 64];
+    for (uint32_t i = threadIdx.x; i < SPM_ROOT_CAP; i += SPM_TILE_BLOCK) root[i] = spm_root_entry(ta.ra.spm, i);
     for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
         const uint32_t cp = hot_cp(i);
         hot_tab[i] = hot_of(prop_global(cp));
@@ -32,25 +34,32 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     }
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
-    spm_tiles_wave<FLAGS>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
+    spm_tiles_wave<FLAGS>(ta, hot_tab, scode, root, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
                           gridDim.x * (SPM_TILE_BLOCK / 64));
 }
 
-// fallback rows with the fast row kernel's private buffers, straight into the row's tile slot
+// fallback rows with the fast row kernel's buffer sizes, straight into the row's tile slot. The
+// lattice and NFC buffers of each lane live in LDS (private arrays would be scratch: one HBM round
+// trip per access, serialized per lane).
+constexpr int SPM_FB_LANE_U32 = 2 * FAST_SEG + 8 * FAST_SEG + FAST_VCAP + 3 * (FAST_VCAP + 1);
+
 template <int FLAGS>
 __global__ __launch_bounds__(SPM_FB_BLOCK) void k_spm_tile_fb(TileArgs ta) {
     __shared__ uint2 fast[FAST_N];
     __shared__ uint16_t sfast[1];
+    __shared__ uint32_t lanebuf[SPM_FB_BLOCK * SPM_FB_LANE_U32];
     const uint32_t nl = *ta.fb_count;
     if (nl == 0) return;  // uniform: the common case
     stage_tables(fast, sfast, nullptr, false);
-    uint32_t seg[FAST_SEG], seg2[FAST_SEG], dec[4 * FAST_SEG], dec2[4 * FAST_SEG];
-    uint32_t vchar[FAST_VCAP];
-    float vbest[FAST_VCAP + 1];
-    int32_t vstart[FAST_VCAP + 1], vid[FAST_VCAP + 1];
+    uint32_t *b = lanebuf + threadIdx.x * SPM_FB_LANE_U32;
     Scratch sc;
-    small_scratch(sc, seg, seg2, dec, dec2, FAST_SEG);
-    sc.vchar = vchar; sc.vbest = vbest; sc.vstart = vstart; sc.vid = vid; sc.vcap = FAST_VCAP;
+    small_scratch(sc, b, b + FAST_SEG, b + 2 * FAST_SEG, b + 6 * FAST_SEG, FAST_SEG);
+    b += 10 * FAST_SEG;
+    sc.vchar = b;
+    sc.vbest = (float *)(b + FAST_VCAP);
+    sc.vstart = (int32_t *)(b + FAST_VCAP + (FAST_VCAP + 1));
+    sc.vid = (int32_t *)(b + FAST_VCAP + 2 * (FAST_VCAP + 1));
+    sc.vcap = FAST_VCAP;
     const RowArgs &a = ta.ra;
     for (uint32_t i = blockIdx.x * SPM_FB_BLOCK + threadIdx.x; i < nl; i += gridDim.x * SPM_FB_BLOCK) {
         const uint64_t r = ta.fb_list[i];
@@ -130,7 +139,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     AK_PROF(AK_PROF_SPM_TILES, true, st);
     HIP_TRY(hipGetLastError());
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    k_spm_tile_fb<3><<<(unsigned)num_cus(), SPM_FB_BLOCK, 0, st>>>(ta);
+    k_spm_tile_fb<3><<<(unsigned)num_cus() * 2, SPM_FB_BLOCK, 0, st>>>(ta);
     RowArgs ra = ta.ra;
     ra.counts = w->counts;
     ra.err = w->ctr + CTR_ERR;

@@ -11,9 +11,10 @@
 // Words run in parallel from base 0 instead of from the row's carried float score. The carried base
 // only enters a word's decisions through float rounding, so a word whose every lattice node's
 // winner beats the other candidates by more than a rounding bound tau (below) makes the same
-// decisions from any base the row can carry; a row with a closer call goes to the exact sequential
-// row kernels (ak_dev.h SpmSink), which carry the base as sentencepiece does. The result is
-// bit-identical to the reference either way (tests: golden, near-tie rows, oracle at scale).
+// decisions from any base the row can carry; a row with a closer call is redone in the tile by one
+// lane, its words in order from the carried float base, as sentencepiece's whole-row lattice (and
+// ak_dev.h SpmSink) computes it. The result is bit-identical to the reference either way (tests:
+// golden, near-tie rows, oracle at scale).
 //
 // tau: at node e every candidate's value under base b differs from its base-0 value + b by at most
 // (depth + 1) (ulp_M + ulp_0) / 2 (one rounding per stored score), and the leader is stored as a
@@ -27,7 +28,7 @@
 
 namespace ak {
 
-constexpr int S_BCAP = 512;                 // staged bytes per tile
+constexpr int S_BCAP = 480;                 // staged bytes per tile (4 blocks of 4 waves fit a CU's LDS)
 constexpr int S_E = S_BCAP + 2 * T_MAXR + 64;  // entries of V
 constexpr int S_W = S_E + T_MAXR + 16;      // entries of W (chars, "▁", row sentinels)
 constexpr int S_WORDS = 256;                // words per tile (more: the tile's rows fall back)
@@ -36,6 +37,15 @@ constexpr uint16_t W_CODED = 0x8000;  // W entry: 0x8000 | dense code (a char so
 constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: the trie walk stops there)
 constexpr uint16_t W_END = 0x7FFF;
 constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
+constexpr uint32_t SPM_ROOT_CAP = 128;  // root children of codes below this are cached in LDS (spm_root_entry)
+
+// LDS cache entry of the trie root's child for code c: {node index or -1, base, value, aux}
+__device__ __forceinline__ int4 spm_root_entry(const SpmDev &m, uint32_t c) {
+    const int t = m.root_base + (int)c;
+    if (c == 0 || (uint32_t)t >= m.n_nodes) return make_int4(-1, 0, -1, 0);
+    const int4 e = m.trie[t];
+    return e.x == 0 ? make_int4(t, e.y, e.z, e.w) : make_int4(-1, 0, -1, 0);
+}
 
 struct SpmWaveMem {
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
@@ -45,9 +55,11 @@ struct SpmWaveMem {
     uint32_t back[S_W];                      // best piece ending here: id << 8 | chars
     uint8_t wrow[S_WORDS];                   // row of each word
     uint8_t fb[T_MAXR];
+    uint8_t mfail[T_MAXR];                   // row has a lattice node within the rounding bound (pass V2)
     uint16_t rowend[T_MAXR];
     uint32_t rowslot[T_MAXR];
     uint16_t rowpos[T_MAXR + 1];             // W position of each row's W_B (+ end)
+    uint16_t wfirst[T_MAXR + 1];             // index of each row's first word (+ end)
     uint32_t rowcnt[T_MAXR];
     uint32_t rowfirst[T_MAXR];               // tile-stream position of the row's first id
     uint64_t passacc[10];
@@ -67,9 +79,92 @@ __device__ __forceinline__ uint32_t spm_wcp(const SpmDev &m, uint16_t x) {
     return (x & W_CODED) ? m.code_cp[x & 0x7FFFu] : (uint32_t)x;
 }
 
+// The unigram lattice of one word (W positions [p0, p1), "▁" at p0) from the float base `base`:
+// sentencepiece 0.2.2's arithmetic (double candidate for pieces, float for unk, first arrival wins
+// ties). The word owns best / back at (p0, p1] (p0 is the previous word's end node: the base stays
+// in a register). MARGIN: track the smallest gap between a candidate and the stored leader.
+// Inactive lanes pass p1 <= p0. `root` caches the trie's root children (code -> node) in LDS.
+template <bool MARGIN>
+__device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const int4 *root, int p0, int p1, float base,
+                                        float &minm) {
+    for (int i = p0 + 1; i <= p1; ++i) M.back[i] = BK_NONE;
+    for (int s = p0; s < p1; ++s) {
+        const float till = s == p0 ? base : M.best[s];
+        bool has_single = false;
+        int node = 0, nb = 0;
+        for (int k = s; k < p1; ++k) {
+            const uint32_t v = M.w[k];
+            if (!(v & W_CODED)) break;
+            int t;
+            int4 e;
+            if (k == s && (v & 0x7FFFu) < SPM_ROOT_CAP) {  // root child from LDS
+                e = root[v & 0x7FFFu];
+                t = e.x;  // root[] holds {node index, base, value, aux}: a miss has index -1
+                if (t < 0) break;
+            } else if (k == s) {
+                t = m.root_base + (int)(v & 0x7FFFu);
+                e = m.trie[t];
+                if (e.x != 0) break;
+                e.x = t;
+            } else {
+                t = nb + (int)(v & 0x7FFFu);
+                e = m.trie[t];
+                if (e.x != node) break;
+            }
+            node = t;
+            nb = e.y;
+            const int value = e.z;
+            if (value < 0) continue;
+            const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
+            if (kind == 2) continue;
+            const int id = value & 0xFFFFFF;
+            const double score = kind == 1 ? (double)((float)e.w * m.max_score) - 0.1 : (double)__int_as_float(e.w);
+            const double cand = score + (double)till;
+            const int ee = k + 1;
+            const uint32_t bk = M.back[ee];
+            if (bk == BK_NONE || cand > (double)M.best[ee]) {
+                if (MARGIN && bk != BK_NONE) minm = fminf(minm, (float)(cand - (double)M.best[ee]));
+                M.best[ee] = (float)cand;
+                M.back[ee] = ((uint32_t)id << 8) | (uint32_t)(ee - s);
+            } else if (MARGIN) {
+                minm = fminf(minm, (float)((double)M.best[ee] - cand));
+            }
+            if (k == s) has_single = true;  // sentencepiece: a piece of exactly the first char
+        }
+        if (!has_single) {
+            const int ee = s + 1;
+            const float cand = m.unk_score + till;
+            const uint32_t bk = M.back[ee];
+            if (bk == BK_NONE || cand > M.best[ee]) {
+                if (MARGIN && bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
+                M.best[ee] = cand;
+                M.back[ee] = ((uint32_t)m.unk_id << 8) | 1u;
+            } else if (MARGIN) {
+                minm = fminf(minm, M.best[ee] - cand);
+            }
+        }
+    }
+}
+
+// backtrack a solved word into forward links nxt[s] = chars of the piece at s; returns its id
+// count (byte fallback: one id per UTF-8 byte of an unk char)
+__device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &m, uint8_t *nxt, int p0, int p1) {
+    uint32_t cnt = 0;
+    for (int e = p1; e > p0;) {
+        const uint32_t bk = M.back[e];
+        const int d = (int)(bk & 0xFFu);
+        const int s = e - d;
+        nxt[s] = (uint8_t)d;
+        const int id = (int)(bk >> 8);
+        cnt += id == m.unk_id ? (uint32_t)utf8_len(spm_wcp(m, M.w[s])) : 1u;
+        e = s;
+    }
+    return cnt;
+}
+
 template <int FLAGS>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
-                        SpmWaveMem &M, PassClock &pc) {
+                        const int4 *root, SpmWaveMem &M, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
@@ -119,103 +214,67 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                 M.w[p + (ws ? 1 : 0)] = code;
             } else if (keep && special) {
                 M.w[p] = x == V_B ? W_B : W_END;
-                if (x == V_B) M.rowpos[row] = (uint16_t)p;
             }
             const uint64_t WM = w_ballot(ws);
             const uint32_t j = nw + w_rank(WM);
+            if (keep && x == V_B) { M.rowpos[row] = (uint16_t)p; M.wfirst[row] = (uint16_t)j; }
             if (ws && j < (uint32_t)S_WORDS) { starts[j] = (uint16_t)p; wrow[j] = (uint8_t)row; }
             nw += (uint32_t)w_popc(WM);
             wlen += tot;
             rs += (uint32_t)w_popc(RM);
             if (KM) carry = (uint16_t)w_bcast((uint32_t)x, msb64(KM));
         }
-        if (lane == 0) M.rowpos[rs] = (uint16_t)wlen;
+        if (lane == 0) { M.rowpos[rs] = (uint16_t)wlen; M.wfirst[rs] = (uint16_t)nw; }
         if (nw > (uint32_t)S_WORDS || wlen > (uint32_t)S_W) {  // never in text: the tile's rows fall back
             if (lane < nr) M.fb[lane] = 1;
             nw = 0;
         }
-        if (lane < nr) { M.rowcnt[lane] = 0; M.rowfirst[lane] = 0; }
+        if (lane < nr) { M.rowcnt[lane] = 0; M.rowfirst[lane] = 0; M.mfail[lane] = 0; }
     }
     w_sync();
     pc.mark(TP_E);
 
-    // ---------------- pass V: lane per word, Viterbi from base 0 with the running margin check,
-    // backtrack into forward links nxt[s] = chars of the piece at s; the word's id count -> wcnt.
-    // A word owns best / back at (p0, p1] (its start node p0 is the previous word's end node: the
-    // base 0 stays in a register) and nxt at [p0, p1).
+    // ---------------- pass V: lane per word, Viterbi from base 0 with the running margin check
+    // (word_dp); a row with a close call is redone exactly below (pass V2)
     uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
     for (uint32_t jb = 0; jb < nw; jb += 64) {
         const uint32_t j = jb + (uint32_t)lane;
         const bool act = j < nw;
         const int row = act ? (int)wrow[j] : 0;
         const int p0 = act ? (int)starts[j] : 0;
-        int p1 = 0;
-        if (act) p1 = (j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1;
-        for (int i = p0 + 1; i <= p1; ++i) M.back[i] = BK_NONE;
+        const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
         float minm = 3.0e38f;
-        for (int s = p0; s < p1; ++s) {
-            const float till = s == p0 ? 0.0f : M.best[s];
-            bool has_single = false;
-            int node = 0, nb = m.root_base;
-            for (int k = s; k < p1; ++k) {
-                const uint32_t v = M.w[k];
-                if (!(v & W_CODED)) break;
-                const int t = nb + (int)(v & 0x7FFFu);
-                const int4 e = m.trie[t];
-                if (e.x != node) break;
-                node = t;
-                nb = e.y;
-                const int value = e.z;
-                if (value < 0) continue;
-                const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
-                if (kind == 2) continue;
-                const int id = value & 0xFFFFFF;
-                const double score = kind == 1 ? (double)((float)e.w * m.max_score) - 0.1 : (double)__int_as_float(e.w);
-                const double cand = score + (double)till;
-                const int ee = k + 1;
-                const uint32_t bk = M.back[ee];
-                if (bk == BK_NONE || cand > (double)M.best[ee]) {
-                    if (bk != BK_NONE) minm = fminf(minm, (float)(cand - (double)M.best[ee]));
-                    M.best[ee] = (float)cand;
-                    M.back[ee] = ((uint32_t)id << 8) | (uint32_t)(ee - s);
-                } else {
-                    minm = fminf(minm, (float)((double)M.best[ee] - cand));
-                }
-                if (k == s) has_single = true;  // sentencepiece: a piece of exactly the first char
-            }
-            if (!has_single) {
-                const int ee = s + 1;
-                const float cand = m.unk_score + till;
-                const uint32_t bk = M.back[ee];
-                if (bk == BK_NONE || cand > M.best[ee]) {
-                    if (bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
-                    M.best[ee] = cand;
-                    M.back[ee] = ((uint32_t)m.unk_id << 8) | 1u;
-                } else {
-                    minm = fminf(minm, M.best[ee] - cand);
-                }
-            }
-        }
+        word_dp<true>(M, m, root, p0, p1, 0.0f, minm);
         if (act) {
             // rounding bound of this word (header comment): M = (chars from the row start to the word
             // end + 1) x the largest |score|
             const float Mb = (float)(p1 - (int)M.rowpos[row] + 1) * m.abs_score_max + 1.0f;
             const float tau = (float)(p1 - p0 + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
-            if (!(minm > tau)) M.fb[row] = 1;
-            uint32_t cnt = 0;
-            for (int e = p1; e > p0;) {
-                const uint32_t bk = M.back[e];
-                const int d = (int)(bk & 0xFFu);
-                const int s = e - d;
-                nxt[s] = (uint8_t)d;
-                const int id = (int)(bk >> 8);
-                cnt += id == m.unk_id ? (uint32_t)utf8_len(spm_wcp(m, M.w[s])) : 1u;
-                e = s;
-            }
-            wcnt[j] = (uint16_t)cnt;
+            if (!(minm > tau)) M.mfail[row] = 1;
+            wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
         }
     }
     w_sync();
+    // ---------------- pass V2 (rare): lane per row with a close call, its words in order from the
+    // carried float base, exactly as sentencepiece's whole-row lattice (ak_dev.h SpmSink)
+    {
+        const bool redo = lane < nr && M.mfail[lane] && !M.fb[lane];
+        if (w_ballot(redo)) {
+            if (redo) {
+                float base = 0.0f;
+                const int j1 = (int)M.wfirst[lane + 1];
+                for (int j = (int)M.wfirst[lane]; j < j1; ++j) {
+                    const int p0 = (int)starts[j];
+                    const int p1 = j + 1 < j1 ? (int)starts[j + 1] : (int)M.rowpos[lane + 1] - 1;
+                    float unused = 0.0f;
+                    word_dp<false>(M, m, root, p0, p1, base, unused);
+                    wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
+                    base = M.best[p1];
+                }
+            }
+            w_sync();
+        }
+    }
     pc.mark(TP_B);
 
     // ---------------- fallback rows: append to the list (rare: one atomic per tile that has any)
@@ -292,15 +351,15 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
 }
 
 template <int FLAGS>
-__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M,
-                               uint32_t wave_gid, uint32_t nwaves) {
+__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, const int4 *root,
+                               SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
     for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * (uint64_t)ta.rows;
         const uint64_t r1 = r0 + (uint64_t)ta.rows < ta.ra.n ? r0 + (uint64_t)ta.rows : ta.ra.n;
-        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r1, H, scode, M, pc);
+        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r1, H, scode, root, M, pc);
     }
     pc.flush(ta.passprof);
 }

@@ -198,7 +198,7 @@ import os as _os
 # 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (staged row kernel); AK_BPE_PATH overrides
 BPE_PATH = int(_os.environ.get("AK_BPE_PATH", "1"))
 TILE_BYTES = 560      # BPE: target bytes of text per wave-tile (the tile buffer holds 768)
-SPM_TILE_BYTES = 380  # SentencePiece: target bytes per tile (the tile buffer holds 512)
+SPM_TILE_BYTES = 360  # SentencePiece: target bytes per tile (the tile buffer holds 480)
 
 
 def tile_rows_for(n, nbytes, target=TILE_BYTES):

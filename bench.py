@@ -365,8 +365,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     prof = engine.profile_read()
-    passes = engine.profile_tile_passes(local) if not cfg5 else {}
-    fb_rows = engine.fallback_rows(local) if not cfg5 else (0, 0)
+    passes = engine.profile_tile_passes(local)
+    fb_rows = engine.fallback_rows(local)
     engine.profile_enable(False)
 
     if dist:

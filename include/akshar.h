@@ -76,8 +76,8 @@ int ak_ws_create(ak_ws **out);
 void ak_ws_free(ak_ws *ws);
 /* Kernel choice for this workspace's BPE and SentencePiece encodes with the normalize_text
  * defaults: path 1 = tile-cooperative single pass (default; tile_rows rows per wave-tile, 1..16,
- * default 8 — pick ~560 B of text per tile for BPE (768-byte tile buffer), ~380 B for
- * SentencePiece (512-byte buffer)), 0 = one lane per row (the staged row kernel). */
+ * default 8 — pick ~560 B of text per tile for BPE (768-byte tile buffer), ~360 B for
+ * SentencePiece (480-byte buffer)), 0 = one lane per row (the staged row kernel). */
 int ak_ws_set_tiling(ak_ws *ws, int bpe_path, int tile_rows);
 /* Synchronous health check after a batch: AK_ERR_HIP if the last call flagged an internal
  * overflow (a row producing more output than its staging slot bound, or overflowing the huge

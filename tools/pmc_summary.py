@@ -10,6 +10,7 @@ WRITE_SIZE in KiB -> x1024).
 """
 import collections
 import csv
+import glob
 import json
 import os
 import shutil
@@ -27,6 +28,40 @@ def counters(path, match="bpe_tiles"):
                     "lds_block": int(r.get("LDS_Block_Size") or r.get("Lds_Size") or 0),
                     "scratch": int(r.get("Scratch_Size") or 0)}
     return dict(agg), meta
+
+
+KERNEL_CLASS = {"bpe_tiles": ("tiles", "k_bpe_tiles<3>"), "spm_tiles": ("spm_tiles", "k_spm_tiles<3>")}
+
+
+def op_summary(src, tag, match, rows, nbytes):
+    """tools/pmc_op.sh output -> profiles/<tag>_<class>_pmc.json (HBM bytes per launch, SQ counters)
+    and profiles/<tag>_<class>_kernel_stats.csv (the kernel trace summary of the same op)."""
+    out = os.path.join(ROOT, "profiles")
+    cls, kname = KERNEL_CLASS[match]
+    allc, meta = {}, {}
+    for name in ("fetch", "write", "sq1", "sq2"):
+        p = os.path.join(src, name, name + "_counter_collection.csv")
+        if os.path.exists(p):
+            c, m = counters(p, match)
+            allc.update(c)
+            meta = meta or m
+    rd = allc["FETCH_SIZE"] * 1024 * 2
+    wr = allc["WRITE_SIZE"] * 1024
+    rec = {"kernel": kname, "kernel_class": cls, "rows": rows, "bytes": nbytes,
+           "command": "tools/pmc_op.sh (rocprofv3 --pmc, one run per counter group) over tools/prof_op.py, one launch "
+                      "of %d synthetic Hinglish rows (%d bytes)" % (rows, nbytes),
+           "counters": allc, **meta, "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+           "valu_per_row": round(allc.get("SQ_INSTS_VALU", 0) / rows, 1),
+           "salu_per_row": round(allc.get("SQ_INSTS_SALU", 0) / rows, 1),
+           "lds_per_row": round(allc.get("SQ_INSTS_LDS", 0) / rows, 1),
+           "wait_frac": round(allc.get("SQ_WAIT_ANY", 0) / max(allc.get("SQ_WAVE_CYCLES", 1), 1), 3),
+           "note": "read = FETCH_SIZE x 1024 x 2 (gfx950 half-count correction for 16-B/lane streaming reads), "
+                   "write = WRITE_SIZE x 1024"}
+    json.dump(rec, open(os.path.join(out, "%s_%s_pmc.json" % (tag, cls)), "w"), indent=1)
+    st = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    if st:
+        shutil.copy(st[0], os.path.join(out, "%s_%s_kernel_stats.csv" % (tag, cls)))
+    print(json.dumps(rec, indent=1))
 
 
 def main(src, tag):
@@ -55,4 +90,7 @@ def main(src, tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    if len(sys.argv) > 3:  # pmc_summary.py SRC TAG MATCH ROWS BYTES
+        op_summary(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]))
+    else:
+        main(sys.argv[1], sys.argv[2])
