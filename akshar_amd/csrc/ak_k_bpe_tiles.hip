@@ -164,7 +164,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     rc = ws_stage_reserve(w, nbytes + 2 * a0.n + 64, st);
     if (rc) return rc;
     const int R = w->tile_rows;
-    const uint64_t ntiles = (a0.n + (uint64_t)R - 1) / (uint64_t)R;
+    const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the static wave stride
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));

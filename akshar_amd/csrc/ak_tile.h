@@ -29,6 +29,7 @@ namespace ak {
 
 constexpr int T_BCAP = 768;   // staged bytes per tile (rows past it start the next sub-tile)
 constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
+constexpr uint64_t TILE_UNIT = 64;  // rows per unit of the static wave stride (tiles pack greedily inside one)
 constexpr int T_E = T_BCAP + 2 * T_MAXR + 64;
 
 constexpr uint16_t V_FB = 0xFFFC;    // sentinel of a row handed to the fallback kernels (no ids here)
@@ -616,11 +617,13 @@ __device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
                                uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
-    for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {  // static stride: tiles are near-equal
+    // static stride over units of TILE_UNIT rows (units are near-equal); inside a unit, each tile
+    // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
+    for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {
         pc.mark(TP_LOOP);
-        const uint64_t r0 = t * (uint64_t)ta.rows;
-        const uint64_t r1 = r0 + (uint64_t)ta.rows < ta.ra.n ? r0 + (uint64_t)ta.rows : ta.ra.n;
-        for (uint64_t r = r0; r < r1;) r += (uint64_t)bpe_tile<FLAGS>(ta, r, r1, H, sfast, M, pc);
+        const uint64_t r0 = t * TILE_UNIT;
+        const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;
+        for (uint64_t r = r0; r < r1;) r += (uint64_t)bpe_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, sfast, M, pc);
     }
     pc.flush(ta.passprof);
 }

@@ -355,11 +355,13 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
                                SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
+    // static stride over units of TILE_UNIT rows (units are near-equal); inside a unit, each tile
+    // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
     for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {
         pc.mark(TP_LOOP);
-        const uint64_t r0 = t * (uint64_t)ta.rows;
-        const uint64_t r1 = r0 + (uint64_t)ta.rows < ta.ra.n ? r0 + (uint64_t)ta.rows : ta.ra.n;
-        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r1, H, scode, root, M, pc);
+        const uint64_t r0 = t * TILE_UNIT;
+        const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;
+        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, root, M, pc);
     }
     pc.flush(ta.passprof);
 }

@@ -202,10 +202,11 @@ SPM_TILE_BYTES = 360  # SentencePiece: target bytes per tile (the tile buffer ho
 
 
 def tile_rows_for(n, nbytes, target=TILE_BYTES):
-    if n == 0:
-        return 8
-    avg = max(nbytes / n, 1.0)
-    return int(min(16, max(1, round(target / avg))))
+    """Rows per tile: tiles pack rows greedily up to their byte buffer (16 rows at most); AK_TILE_ROWS
+    overrides (development aid)."""
+    if _os.environ.get("AK_TILE_ROWS"):
+        return int(_os.environ["AK_TILE_ROWS"])
+    return 16
 
 
 class BPE:

@@ -180,10 +180,9 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     memset(&ta, 0, sizeof(ta));
     ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = stage.size();
     ta.ra.row_status = row_status; ta.ra.bpe = m->bdev; ta.ra.single_fast = m->bpe.fast.data();
-    const uint64_t ntiles = (n + rows - 1) / rows;
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
     ta.fb2_count = &fb2n; ta.err = &err;
-    ta.ntiles = ntiles; ta.rows = rows;
+    ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
     std::vector<uint16_t> sfast(SFAST_N);
     for (uint32_t i = 0; i < SFAST_N; ++i) sfast[i] = m->bpe.fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     TileWaveMem *M = new TileWaveMem();
@@ -258,7 +257,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     ta.ra.row_status = row_status; ta.ra.spm = m->sdev;
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
     ta.fb2_count = &fb2n; ta.err = &err;
-    ta.ntiles = (n + rows - 1) / rows; ta.rows = rows;
+    ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
     SpmWaveMem *M = new SpmWaveMem();
     EmuWave W;
     std::vector<std::thread> th;
