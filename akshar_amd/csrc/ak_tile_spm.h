@@ -88,79 +88,59 @@ template <bool MARGIN>
 __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const int4 *root, int p0, int p1, float base,
                                         float &minm) {
     for (int i = p0 + 1; i <= p1; ++i) M.back[i] = BK_NONE;
-    // One flat loop per lane: each iteration is one trie step of the walk from start s (relaxing
-    // best[k + 1] when the node holds a piece), or, once that walk ends, the unk candidate of s and
-    // the move to s + 1. Lanes advance independently (no wait for the longest walk at each start).
-    int s = p0, k = p0, node = 0, nb = 0;
-    float till = base;
-    bool has_single = false;
-    bool live = p0 < p1;
-    while (live) {
-        bool stepped = false;
-        if (k < p1) {
+    for (int s = p0; s < p1; ++s) {
+        const float till = s == p0 ? base : M.best[s];
+        bool has_single = false;
+        int node = 0, nb = 0;
+        for (int k = s; k < p1; ++k) {
             const uint32_t v = M.w[k];
-            if (v & W_CODED) {
-                const uint32_t c = v & 0x7FFFu;
-                int t;
-                int4 e;
-                bool ok;
-                if (k == s && c < SPM_ROOT_CAP) {  // root child from LDS: {node index or -1, base, value, aux}
-                    e = root[c];
-                    t = e.x;
-                    ok = t >= 0;
-                } else {
-                    t = (k == s ? m.root_base : nb) + (int)c;
-                    e = m.trie[t];
-                    ok = e.x == (k == s ? 0 : node);
-                }
-                if (ok) {
-                    stepped = true;
-                    node = t;
-                    nb = e.y;
-                    const int value = e.z;
-                    const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
-                    if (value >= 0 && kind != 2) {
-                        const int id = value & 0xFFFFFF;
-                        const double score =
-                            kind == 1 ? (double)((float)e.w * m.max_score) - 0.1 : (double)__int_as_float(e.w);
-                        const double cand = score + (double)till;
-                        const int ee = k + 1;
-                        const uint32_t bk = M.back[ee];
-                        const float cur = M.best[ee];
-                        if (bk == BK_NONE || cand > (double)cur) {
-                            if (MARGIN && bk != BK_NONE) minm = fminf(minm, (float)(cand - (double)cur));
-                            M.best[ee] = (float)cand;
-                            M.back[ee] = ((uint32_t)id << 8) | (uint32_t)(ee - s);
-                        } else if (MARGIN) {
-                            minm = fminf(minm, (float)((double)cur - cand));
-                        }
-                        if (k == s) has_single = true;  // sentencepiece: a piece of exactly the first char
-                    }
-                    ++k;
-                }
+            if (!(v & W_CODED)) break;
+            int t;
+            int4 e;
+            if (k == s && (v & 0x7FFFu) < SPM_ROOT_CAP) {  // root child from LDS
+                e = root[v & 0x7FFFu];
+                t = e.x;  // root[] holds {node index, base, value, aux}: a miss has index -1
+                if (t < 0) break;
+            } else if (k == s) {
+                t = m.root_base + (int)(v & 0x7FFFu);
+                e = m.trie[t];
+                if (e.x != 0) break;
+                e.x = t;
+            } else {
+                t = nb + (int)(v & 0x7FFFu);
+                e = m.trie[t];
+                if (e.x != node) break;
             }
+            node = t;
+            nb = e.y;
+            const int value = e.z;
+            if (value < 0) continue;
+            const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
+            if (kind == 2) continue;
+            const int id = value & 0xFFFFFF;
+            const double score = kind == 1 ? (double)((float)e.w * m.max_score) - 0.1 : (double)__int_as_float(e.w);
+            const double cand = score + (double)till;
+            const int ee = k + 1;
+            const uint32_t bk = M.back[ee];
+            if (bk == BK_NONE || cand > (double)M.best[ee]) {
+                if (MARGIN && bk != BK_NONE) minm = fminf(minm, (float)(cand - (double)M.best[ee]));
+                M.best[ee] = (float)cand;
+                M.back[ee] = ((uint32_t)id << 8) | (uint32_t)(ee - s);
+            } else if (MARGIN) {
+                minm = fminf(minm, (float)((double)M.best[ee] - cand));
+            }
+            if (k == s) has_single = true;  // sentencepiece: a piece of exactly the first char
         }
-        if (!stepped) {  // the walk from s is over: unk candidate, then the next start
-            if (!has_single) {
-                const int ee = s + 1;
-                const float cand = m.unk_score + till;
-                const uint32_t bk = M.back[ee];
-                const float cur = M.best[ee];
-                if (bk == BK_NONE || cand > cur) {
-                    if (MARGIN && bk != BK_NONE) minm = fminf(minm, cand - cur);
-                    M.best[ee] = cand;
-                    M.back[ee] = ((uint32_t)m.unk_id << 8) | 1u;
-                } else if (MARGIN) {
-                    minm = fminf(minm, cur - cand);
-                }
-            }
-            ++s;
-            live = s < p1;
-            if (live) {
-                k = s;
-                node = 0;
-                till = M.best[s];
-                has_single = false;
+        if (!has_single) {
+            const int ee = s + 1;
+            const float cand = m.unk_score + till;
+            const uint32_t bk = M.back[ee];
+            if (bk == BK_NONE || cand > M.best[ee]) {
+                if (MARGIN && bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
+                M.best[ee] = cand;
+                M.back[ee] = ((uint32_t)m.unk_id << 8) | 1u;
+            } else if (MARGIN) {
+                minm = fminf(minm, M.best[ee] - cand);
             }
         }
     }
