@@ -16,7 +16,8 @@ AK_ROW_BAD_UTF8 = 1
 AK_ROW_LIMIT = 4
 AK_TILE_PASSES = ("pre", "stage_decode_nfc_map", "elong_ws_pretok", "unused", "pretoken_starts", "merge_or_viterbi",
                   "fallback_list", "ids_to_slots", "unused2", "loop")
-AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4, "tiles": 5, "copy": 6, "spm_tiles": 7}
+AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4, "tiles": 5, "copy": 6, "spm_tiles": 7,
+           "row_tiles": 8}
 
 P = ctypes.c_void_p
 U64 = ctypes.c_uint64

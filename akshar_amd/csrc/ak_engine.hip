@@ -490,10 +490,22 @@ int ak::num_cus() {
 }
 
 static int dispatch(int op, int flags, ak_ws *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st) {
+    const bool tiles = w->bpe_path == 1 && flags == 3;
+    RowsOutFinal f;
+    memset(&f, 0, sizeof(f));
     switch (op) {
-        case OP_NORMALIZE: return launch_normalize(flags, w, a, out_offs, st);
-        case OP_SEGMENT: return launch_segment(flags, w, a, out_offs, st);
-        case OP_SWITCHES: return launch_switches(flags, w, a, out_offs, st);
+        case OP_NORMALIZE:
+            if (!tiles) return launch_normalize(flags, w, a, out_offs, st);
+            f.norm = (uint8_t *)a.out; f.norm_cap = a.cap; f.norm_offs = out_offs;
+            return launch_rows_tiles(1, w, a, 0, f, st);
+        case OP_SEGMENT:
+            if (!tiles) return launch_segment(flags, w, a, out_offs, st);
+            f.seg = (uint32_t *)a.out; f.seg_cap = a.cap; f.seg_offs = out_offs;
+            return launch_rows_tiles(2, w, a, a.matras, f, st);
+        case OP_SWITCHES:
+            if (!tiles) return launch_switches(flags, w, a, out_offs, st);
+            f.runs = (uint32_t *)a.out; f.labels = a.labels; f.run_cap = a.cap; f.run_offs = out_offs;
+            return launch_rows_tiles(4, w, a, 0, f, st);
         case OP_BPE:
             return w->bpe_path == 1 && flags == 3 ? launch_bpe_tiles(flags, w, a, out_offs, st)
                                                   : launch_bpe(flags, w, a, out_offs, st);
@@ -589,6 +601,10 @@ extern "C" int ak_analyze(ak_ws *w, int flags, int matras, const uint8_t *in, co
     if (flags < 0 || flags > 3) return fail(AK_ERR_ARG, "ak_analyze: flags must be 0..3");
     RowArgs a = make_args(in, offs, n, nullptr, 0, row_status);
     a.matras = matras;
+    if (w->bpe_path == 1 && flags == 3) {
+        RowsOutFinal f{norm, norm_cap, norm_offs, clusters, cl_cap, cl_offs, runs, labels, run_cap, run_offs};
+        return launch_rows_tiles(7, w, a, matras, f, (hipStream_t)stream);
+    }
     AnalyzeOut o{norm, norm_cap, norm_offs, clusters, cl_cap, cl_offs, runs, labels, run_cap, run_offs};
     return launch_analyze(flags, w, a, o, (hipStream_t)stream);
 }

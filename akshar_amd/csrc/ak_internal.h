@@ -56,7 +56,7 @@ struct AkWs {
     uint32_t *fb2 = nullptr;        // second fallback list (rows past the fast buffers)
     uint64_t cap_fb2 = 0;
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
-    int tile_rows = 8;
+    int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)
 };
 
@@ -283,6 +283,15 @@ struct AnalyzeOut {
     uint32_t *runs; uint8_t *labels; uint64_t run_cap; uint64_t *run_offs;
 };
 int launch_analyze(int flags, AkWs *w, const RowArgs &a, const AnalyzeOut &o, hipStream_t st);
+
+// the tile-cooperative normalize / segment / switches / analyze (ak_k_rows_tiles.hip): final
+// outputs of the selected ops (RT_NORM 1, RT_SEG 2, RT_SW 4); unused ones may be null
+struct RowsOutFinal {
+    uint8_t *norm; uint64_t norm_cap; uint64_t *norm_offs;
+    uint32_t *seg; uint64_t seg_cap; uint64_t *seg_offs;
+    uint32_t *runs; uint8_t *labels; uint64_t run_cap; uint64_t *run_offs;
+};
+int launch_rows_tiles(int ops, AkWs *w, const RowArgs &a, int matras, const RowsOutFinal &f, hipStream_t st);
 
 }  // namespace ak
 

@@ -114,10 +114,17 @@ def _run(fn_call, n, cap, make_out, dev, ws, out=None, out_offs=None):
     return outs, out_offs, total
 
 
-def normalize_batch(buf, offs, flags=3, row_status=None):
+def _tiling(ws, path):
+    """path 1 = tile-cooperative kernels for flags 3 (default), 0 = the one-lane-per-row kernels."""
+    path = BPE_PATH if path is None else path
+    check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows_for(0, 0)), "ak_ws_set_tiling")
+
+
+def normalize_batch(buf, offs, flags=3, row_status=None, path=None):
     n = _check_inputs(buf, offs)
     dev = buf.device
     ws = workspace(dev.index)
+    _tiling(ws, path)
     nbytes = int(offs[-1].item()) if n else 0
     cap = nbytes + 64 if flags & AK_NORM_CLEAN else int(_lib.lib().ak_normalize_cap(n, nbytes))
 
@@ -129,11 +136,12 @@ def normalize_batch(buf, offs, flags=3, row_status=None):
     return out[:total], oo
 
 
-def segment_batch(buf, offs, flags=3, matras=False, row_status=None):
+def segment_batch(buf, offs, flags=3, matras=False, row_status=None, path=None):
     """flags=AK_RAW (-1) segments the raw rows; else normalizes with flags first."""
     n = _check_inputs(buf, offs)
     dev = buf.device
     ws = workspace(dev.index)
+    _tiling(ws, path)
     nbytes = int(offs[-1].item()) if n else 0
     cap = int(_lib.lib().ak_segment_cap(n, nbytes))
 
@@ -145,10 +153,11 @@ def segment_batch(buf, offs, flags=3, matras=False, row_status=None):
     return out[:total], oo
 
 
-def switches_batch(buf, offs, flags=3, row_status=None):
+def switches_batch(buf, offs, flags=3, row_status=None, path=None):
     n = _check_inputs(buf, offs)
     dev = buf.device
     ws = workspace(dev.index)
+    _tiling(ws, path)
     nbytes = int(offs[-1].item()) if n else 0
     cap = int(_lib.lib().ak_segment_cap(n, nbytes))
 
@@ -164,7 +173,7 @@ def switches_batch(buf, offs, flags=3, row_status=None):
     return ends[:total], labels[:total], oo
 
 
-def analyze_batch(buf, offs, flags=3, matras=False, row_status=None):
+def analyze_batch(buf, offs, flags=3, matras=False, row_status=None, path=None):
     """explain()'s front half in one fused pass (include/akshar.h ak_analyze): returns
     (norm u8, norm_offs, cluster ends i32, cl_offs, run ends i32, run labels u8, run_offs); cluster
     and run ends index the NORMALIZED row's code points, as segment_akshars(norm) /
@@ -172,6 +181,7 @@ def analyze_batch(buf, offs, flags=3, matras=False, row_status=None):
     n = _check_inputs(buf, offs)
     dev = buf.device
     ws = workspace(dev.index)
+    _tiling(ws, path)
     nbytes = int(offs[-1].item()) if n else 0
     L = _lib.lib()
     caps = [nbytes + 64 if flags & AK_NORM_CLEAN else int(L.ak_normalize_cap(n, nbytes)),

@@ -74,10 +74,10 @@ int ak_selftest(void);
 
 int ak_ws_create(ak_ws **out);
 void ak_ws_free(ak_ws *ws);
-/* Kernel choice for this workspace's BPE and SentencePiece encodes with the normalize_text
- * defaults: path 1 = tile-cooperative single pass (default; tile_rows rows per wave-tile, 1..16,
- * default 8 — pick ~560 B of text per tile for BPE (768-byte tile buffer), ~360 B for
- * SentencePiece (480-byte buffer)), 0 = one lane per row (the staged row kernel). */
+/* Kernel choice for this workspace's calls with the normalize_text defaults (flags 3: BPE and
+ * SentencePiece encodes, normalize, segment / switches of normalized rows, analyze): path 1 =
+ * tile-cooperative single pass (default; a wave packs up to tile_rows rows, 1..16, default 16,
+ * into each tile, as many as fit its byte buffer), 0 = one lane per row (the staged row kernels). */
 int ak_ws_set_tiling(ak_ws *ws, int bpe_path, int tile_rows);
 /* Synchronous health check after a batch: AK_ERR_HIP if the last call flagged an internal
  * overflow (a row producing more output than its staging slot bound, or overflowing the huge
@@ -149,7 +149,8 @@ int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, cons
 #define AK_PROF_TILES 5      /* tile-cooperative BPE kernel (ids into per-tile staging slots) */
 #define AK_PROF_COPY 6       /* staged ids -> final positions (tile path) */
 #define AK_PROF_SPM_TILES 7  /* tile-cooperative SentencePiece kernel */
-#define AK_PROF_NKERNELS 8
+#define AK_PROF_ROW_TILES 8  /* tile-cooperative normalize / segment / switches / analyze kernel */
+#define AK_PROF_NKERNELS 9
 int ak_profile_enable(int on);
 int ak_profile_read(int kernel, double *total_ms, uint64_t *launches);
 void ak_profile_reset(void);

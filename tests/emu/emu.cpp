@@ -15,6 +15,7 @@
 #include "../../akshar_amd/csrc/ak_rows.h"
 #include "../../akshar_amd/csrc/ak_tile.h"
 #include "../../akshar_amd/csrc/ak_tile_spm.h"
+#include "../../akshar_amd/csrc/ak_tile_rows.h"
 
 #include <thread>
 
@@ -296,4 +297,91 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     for (uint64_t r = 0; r < n; ++r)
         for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = stage[2 * offs[r] + 2 * r + i];
     return (int64_t)out_offs[n];
+}
+
+// ------------------------------------------------------------------------------------------
+// tile-cooperative normalize / segment / switches / analyze: one emulated wave, fallback rows
+// through the sequential row tee (rows_fb_row) into the same slots, scan and copy
+
+template <int OPS>
+static int64_t rows_tiles_run(int matras, const uint8_t *in, const uint64_t *offs, uint64_t n, uint8_t *norm,
+                              uint64_t *norm_offs, uint32_t *seg, uint64_t *seg_offs, uint32_t *runs, uint8_t *labels,
+                              uint64_t *run_offs, uint8_t *row_status, int rows) {
+    static uint2 fast[FAST_N];
+    static uint32_t hot_tab[HOT_N];
+    static uint16_t sc_tab[HOT_N];
+    for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
+    for (uint32_t i = 0; i < HOT_N; ++i) { hot_tab[i] = hot_of(prop_global(hot_cp(i))); sc_tab[i] = seg_class_of(hot_cp(i)); }
+    const uint64_t nb = n ? offs[n] : 0;
+    std::vector<uint8_t> snorm(RT_NORM_MUL * nb + RT_NORM_ADD * n + 64), slab(nb + n + 64);
+    std::vector<uint32_t> sseg(nb + n + 64), sruns(nb + n + 64), cn(n), cs(n), cr(n), fbl(n), fb2(n);
+    uint32_t fbn = 0, fb2n = 0, err = 0;
+    TileArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.row_status = row_status;
+    ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data(); ta.fb2_count = &fb2n; ta.err = &err;
+    ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
+    RowsOut o;
+    memset(&o, 0, sizeof(o));
+    o.norm = snorm.data(); o.seg = sseg.data(); o.runs = sruns.data(); o.labels = slab.data();
+    o.norm_cap = snorm.size(); o.seg_cap = sseg.size();
+    o.cnt_norm = cn.data(); o.cnt_seg = cs.data(); o.cnt_runs = cr.data(); o.matras = matras;
+    RowsWaveMem *M = new RowsWaveMem();
+    EmuWave W;
+    std::vector<std::thread> th;
+    for (int lane = 0; lane < 64; ++lane)
+        th.emplace_back([&, lane] {
+            t_lane = lane;
+            t_wave = &W;
+            rows_tiles_wave<OPS>(ta, o, hot_tab, sc_tab, *M, 0, 1);
+        });
+    for (auto &x : th) x.join();
+    delete M;
+    if (err) return -1;
+    g_last_fb = fbn;
+    uint64_t maxlen = 0;
+    for (uint64_t r = 0; r < n; ++r) maxlen = std::max<uint64_t>(maxlen, offs[r + 1] - offs[r]);
+    const uint64_t C = std::max<uint64_t>(SLOW_CAP, 3 * maxlen + 64);
+    std::vector<uint32_t> segb(2 * C), dec(8 * C);
+    for (uint32_t i = 0; i < fbn; ++i) {
+        Scratch sc;
+        sc.seg = segb.data(); sc.dec = dec.data(); sc.seg2 = segb.data() + C; sc.dec2 = dec.data() + 4 * C;
+        sc.seg_cap = (int)C; sc.wsym = nullptr; sc.wpair = nullptr; sc.heap = nullptr; sc.link = nullptr; sc.word_cap = 0;
+        sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
+        sc.slow_status = ST_LIMIT; sc.status = 0;
+        if (!rows_fb_row<OPS>(ta.ra, o, fbl[i], fast, &sc, &err)) return -2;
+    }
+    if (err) return -3;
+    auto scan = [&](const std::vector<uint32_t> &c, uint64_t *oo) { oo[0] = 0; for (uint64_t r = 0; r < n; ++r) oo[r + 1] = oo[r] + c[r]; };
+    if (OPS & RT_NORM) {
+        scan(cn, norm_offs);
+        for (uint64_t r = 0; r < n; ++r)
+            for (uint64_t i = 0; i < cn[r]; ++i) norm[norm_offs[r] + i] = snorm[RT_NORM_MUL * offs[r] + RT_NORM_ADD * r + i];
+    }
+    if (OPS & RT_SEG) {
+        scan(cs, seg_offs);
+        for (uint64_t r = 0; r < n; ++r)
+            for (uint64_t i = 0; i < cs[r]; ++i) seg[seg_offs[r] + i] = sseg[offs[r] + r + i];
+    }
+    if (OPS & RT_SW) {
+        scan(cr, run_offs);
+        for (uint64_t r = 0; r < n; ++r)
+            for (uint64_t i = 0; i < cr[r]; ++i) {
+                runs[run_offs[r] + i] = sruns[offs[r] + r + i];
+                labels[run_offs[r] + i] = slab[offs[r] + r + i];
+            }
+    }
+    return 0;
+}
+
+extern "C" int64_t emu_rows_tiles(int ops, int matras, const uint8_t *in, const uint64_t *offs, uint64_t n, uint8_t *norm,
+                                  uint64_t *norm_offs, uint32_t *seg, uint64_t *seg_offs, uint32_t *runs, uint8_t *labels,
+                                  uint64_t *run_offs, uint8_t *row_status, int rows) {
+    switch (ops) {
+        case 1: return rows_tiles_run<1>(matras, in, offs, n, norm, norm_offs, seg, seg_offs, runs, labels, run_offs, row_status, rows);
+        case 2: return rows_tiles_run<2>(matras, in, offs, n, norm, norm_offs, seg, seg_offs, runs, labels, run_offs, row_status, rows);
+        case 4: return rows_tiles_run<4>(matras, in, offs, n, norm, norm_offs, seg, seg_offs, runs, labels, run_offs, row_status, rows);
+        case 7: return rows_tiles_run<7>(matras, in, offs, n, norm, norm_offs, seg, seg_offs, runs, labels, run_offs, row_status, rows);
+    }
+    return -1;
 }

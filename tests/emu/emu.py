@@ -16,7 +16,7 @@ def lib():
         so = os.path.join(HERE, "_emu.so")
         srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
                                                    ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h",
-                                                    "ak_tile.h", "ak_tile_spm.h", "ak_wave.h")]
+                                                    "ak_tile.h", "ak_tile_spm.h", "ak_tile_rows.h", "ak_wave.h")]
         srcs.append(os.path.join(HERE, "..", "..", "include", "akshar.h"))
         if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
             subprocess.check_call(["g++", "-O2", "-std=c++20", "-pthread", "-fPIC", "-shared", "-I",
@@ -31,6 +31,8 @@ def lib():
         L.emu_bpe_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
         L.emu_spm_tiles.restype = ctypes.c_int64
         L.emu_spm_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
+        L.emu_rows_tiles.restype = ctypes.c_int64
+        L.emu_rows_tiles.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_uint64] + [P] * 8 + [ctypes.c_int]
         L.emu_last_fallback_rows.restype = ctypes.c_uint32
         L.emu_run.restype = ctypes.c_int64
         L.emu_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_uint64, P, P,
@@ -109,6 +111,27 @@ def spm_tiles(model, buf, offs, flags=3, rows=4):
                               oo.ctypes.data, st.ctypes.data, rows)
     assert 0 <= tot <= cap, tot
     return out[:tot], oo, st[:n]
+
+
+def rows_tiles(ops, buf, offs, matras=False, rows=16):
+    """Tile-cooperative normalize (1) / segment (2) / switches (4) / analyze (7) on one emulated wave
+    -> dict of (values, offsets) per op."""
+    buf = pad(buf)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    n = len(offs) - 1
+    nb = int(offs[-1])
+    norm = np.zeros(2 * nb + n + 64, np.uint8)
+    seg = np.zeros(nb + n + 64, np.uint32)
+    runs = np.zeros(nb + n + 64, np.uint32)
+    labels = np.zeros(nb + n + 64, np.uint8)
+    no, so, ro = (np.zeros(n + 1, np.uint64) for _ in range(3))
+    st = np.zeros(max(n, 1), np.uint8)
+    rc = lib().emu_rows_tiles(ops, int(matras), buf.ctypes.data, offs.ctypes.data, n, norm.ctypes.data, no.ctypes.data,
+                              seg.ctypes.data, so.ctypes.data, runs.ctypes.data, labels.ctypes.data, ro.ctypes.data,
+                              st.ctypes.data, rows)
+    assert rc == 0, rc
+    return {"norm": (norm[:int(no[-1])], no), "seg": (seg[:int(so[-1])], so),
+            "runs": (runs[:int(ro[-1])], labels[:int(ro[-1])], ro)}
 
 
 def last_fallback_rows():

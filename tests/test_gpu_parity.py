@@ -34,22 +34,26 @@ def _bad(golden, key, got):
     return [(r["set"], r["i"], r["text"], g, r[key]) for r, g in zip(golden, got) if g != r[key]][:5]
 
 
+@pytest.mark.parametrize("path", [1, 0])
 @pytest.mark.parametrize("flags,key", NORM_KEYS)
-def test_normalize_golden(golden, gpacked, eng, flags, key):
-    out, oo = eng.normalize_batch(*gpacked, flags=flags)
+def test_normalize_golden(golden, gpacked, eng, flags, key, path):
+    """path 1: the tile-cooperative kernel for flags 3 (row kernels otherwise), 0: row kernels."""
+    out, oo = eng.normalize_batch(*gpacked, flags=flags, path=path)
     assert _bad(golden, key, rows_u8(_cpu(out), _cpu(oo))) == []
 
 
+@pytest.mark.parametrize("path", [1, 0])
 @pytest.mark.parametrize("flags,matras,key", SEG_KEYS)
-def test_segment_golden(golden, gpacked, eng, flags, matras, key):
-    ends, oo = eng.segment_batch(*gpacked, flags=flags, matras=matras)
+def test_segment_golden(golden, gpacked, eng, flags, matras, key, path):
+    ends, oo = eng.segment_batch(*gpacked, flags=flags, matras=matras, path=path)
     got = [ends_to_lens(e) for e in rows_ints(_cpu(ends), _cpu(oo))]
     assert _bad(golden, key, got) == []
 
 
+@pytest.mark.parametrize("path", [1, 0])
 @pytest.mark.parametrize("flags,key", SW_KEYS)
-def test_switches_golden(golden, gpacked, eng, flags, key):
-    ends, labels, oo = eng.switches_batch(*gpacked, flags=flags)
+def test_switches_golden(golden, gpacked, eng, flags, key, path):
+    ends, labels, oo = eng.switches_batch(*gpacked, flags=flags, path=path)
     assert _bad(golden, key, rows_runs(_cpu(ends), _cpu(labels), _cpu(oo))) == []
 
 
@@ -83,20 +87,21 @@ def test_synthetic_vs_oracle(eng, bpe_model, spm_model, kind, n, seed):
     buf, offs = _synth(kind, n, seed)
     gb, go = _to_dev(eng, buf, offs)
     ob = (buf if len(buf) else np.zeros(1, np.uint8), offs)
-    for flags in (3, 0):
-        out, oo = eng.normalize_batch(gb, go, flags=flags)
+    for flags, path in ((3, 1), (3, 0), (0, 1)):
+        out, oo = eng.normalize_batch(gb, go, flags=flags, path=path)
         ref, ro = O.normalize_batch(*ob, flags=flags)
         assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
         assert np.array_equal(_cpu(out), ref)
-    for flags, matras in ((3, False), (-1, False), (-1, True)):
-        ends, oo = eng.segment_batch(gb, go, flags=flags, matras=matras)
+    for flags, matras, path in ((3, False, 1), (3, True, 1), (3, False, 0), (-1, False, 1), (-1, True, 1)):
+        ends, oo = eng.segment_batch(gb, go, flags=flags, matras=matras, path=path)
         ref, ro = O.segment_batch(*ob, flags=flags, matras=matras)
         assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
         assert np.array_equal(_cpu(ends).astype(np.uint32), ref)
-    ends, labels, oo = eng.switches_batch(gb, go, flags=3)
-    re_, rl, ro = O.switches_batch(*ob, flags=3)
-    assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
-    assert np.array_equal(_cpu(ends).astype(np.uint32), re_) and np.array_equal(_cpu(labels), rl)
+    for path in (1, 0):
+        ends, labels, oo = eng.switches_batch(gb, go, flags=3, path=path)
+        re_, rl, ro = O.switches_batch(*ob, flags=3)
+        assert np.array_equal(_cpu(oo).astype(np.uint64), ro)
+        assert np.array_equal(_cpu(ends).astype(np.uint32), re_) and np.array_equal(_cpu(labels), rl)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(*ob)
     for path in (1, 0):
         ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, path=path)
@@ -249,11 +254,12 @@ def test_tile_path_fallback_accounting(eng, bpe_model):
     assert _cpu(st).tolist()[-1] == 1
 
 
+@pytest.mark.parametrize("path", [1, 0])
 @pytest.mark.parametrize("matras,key", [(False, "ak"), (True, "ak_m")])
-def test_analyze_fused_golden(golden, gpacked, eng, matras, key):
+def test_analyze_fused_golden(golden, gpacked, eng, matras, key, path):
     """ak_analyze (one fused pass: normalize -> segment + switches of the normalized text) against
     the golden norm / ak / sw fields (explain(): tokenizer.py:262-264)."""
-    norm, no, cl, co, runs, labels, ro = eng.analyze_batch(*gpacked, flags=3, matras=matras)
+    norm, no, cl, co, runs, labels, ro = eng.analyze_batch(*gpacked, flags=3, matras=matras, path=path)
     assert _bad(golden, "norm", rows_u8(_cpu(norm), _cpu(no))) == []
     assert _bad(golden, key, [ends_to_lens(e) for e in rows_ints(_cpu(cl), _cpu(co))]) == []
     assert _bad(golden, "sw", rows_runs(_cpu(runs), _cpu(labels), _cpu(ro))) == []
