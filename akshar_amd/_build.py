@@ -60,10 +60,12 @@ def _deps(src, seen=None):
     return seen
 
 
-# per-TU code-generation flags. ak_k_bpe_tiles.hip: without machine LICM the tile kernel keeps its
-# per-lane constants and addresses in-loop (rematerialised) and fits the 64 VGPRs of 8 waves/SIMD
-# with no scratch spills (with it: 20 VGPRs spilled to scratch in every tile's prologue).
-TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"]}
+# per-TU code-generation flags. The tile kernels: without machine LICM they keep per-lane constants
+# and addresses in-loop (rematerialised) and fit 64 VGPRs (8 waves/SIMD) with no scratch spills
+# (with it: the BPE tile kernel spilled 20 VGPRs; the row-tile kernels took 73-86 VGPRs).
+TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"],
+            "ak_k_spm_tiles.hip": ["-mllvm", "-disable-machine-licm"],
+            "ak_k_rows_tiles.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def build_hip(force=False, jobs=None):
