@@ -60,12 +60,12 @@ def _deps(src, seen=None):
     return seen
 
 
-# per-TU code-generation flags. The tile kernels: without machine LICM they keep per-lane constants
-# and addresses in-loop (rematerialised) and fit 64 VGPRs (8 waves/SIMD) with no scratch spills
-# (with it: the BPE tile kernel spilled 20 VGPRs; the row-tile kernels took 73-86 VGPRs).
-TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"],
-            "ak_k_spm_tiles.hip": ["-mllvm", "-disable-machine-licm"],
-            "ak_k_rows_tiles.hip": ["-mllvm", "-disable-machine-licm"]}
+# per-TU code-generation flags. ak_k_bpe_tiles.hip: without machine LICM the tile kernel keeps its
+# per-lane constants and addresses in-loop (rematerialised) and fits the 64 VGPRs of 8 waves/SIMD
+# with no scratch spills (with it: 20 VGPRs spilled to scratch in every tile's prologue). The SPM
+# and row-tile kernels measured faster WITH machine LICM (A/B on MI355X, tools/ab_run.sh: cfg3
+# fused analyze 66.8 vs 60.9 GB/s), so only the BPE TU takes the flag.
+TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def build_hip(force=False, jobs=None):
@@ -94,6 +94,29 @@ def build_hip(force=False, jobs=None):
     with ThreadPoolExecutor(jobs) as ex:
         for f in [ex.submit(_run, c) for c in cmds]:
             f.result()
+    _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs)
+    return out
+
+
+def build_variant(name, defines=(), tu_flags=None):
+    """Development aid: the library built with extra -D defines / per-TU flags into
+    akshar_amd/_variants/<name>.so (selected at run time by AK_LIB_VARIANT=<name>)."""
+    global TU_FLAGS
+    objdir = os.path.join(ROOT, "build", "variants", name)
+    os.makedirs(objdir, exist_ok=True)
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+    common = [hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include"),
+              "-I", CSRC, "-Wall", "-Wno-unused-function"] + ["-D" + d for d in defines]
+    flags = TU_FLAGS if tu_flags is None else tu_flags
+    from concurrent.futures import ThreadPoolExecutor
+    srcs = [os.path.join(CSRC, n) for n in sorted(os.listdir(CSRC)) if n.endswith((".hip", ".cpp"))]
+    objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
+    cmds = [common + flags.get(os.path.basename(s), []) + ["-c", "-o", o, s] for s, o in zip(srcs, objs)]
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 4)) as ex:
+        for f in [ex.submit(_run, c) for c in cmds]:
+            f.result()
+    os.makedirs(os.path.join(HERE, "_variants"), exist_ok=True)
+    out = os.path.join(HERE, "_variants", name + ".so")
     _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs)
     return out
 

@@ -7,6 +7,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_akshar_hip.so")
+if os.environ.get("AK_LIB_VARIANT"):  # development aid: A/B a prebuilt variant _variants/<name>.so
+    LIB_PATH = os.path.join(_HERE, "_variants", os.environ["AK_LIB_VARIANT"] + ".so")
 
 AK_OK = 0
 AK_NORM_LOWER = 1

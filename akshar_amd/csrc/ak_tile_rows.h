@@ -20,7 +20,10 @@
 
 namespace ak {
 
-constexpr int R_BCAP = 640;                     // staged bytes per tile (8 blocks of 4 waves fit a CU's LDS)
+#ifndef AK_R_BCAP
+#define AK_R_BCAP 768
+#endif
+constexpr int R_BCAP = AK_R_BCAP;               // staged bytes per tile
 constexpr int R_E = R_BCAP + 2 * T_MAXR + 64;  // entries of V
 
 enum { RT_NORM = 1, RT_SEG = 2, RT_SW = 4 };

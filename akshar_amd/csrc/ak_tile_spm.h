@@ -28,7 +28,10 @@
 
 namespace ak {
 
-constexpr int S_BCAP = 480;                 // staged bytes per tile (4 blocks of 4 waves fit a CU's LDS)
+#ifndef AK_S_BCAP
+#define AK_S_BCAP 480
+#endif
+constexpr int S_BCAP = AK_S_BCAP;           // staged bytes per tile (4 blocks of 4 waves fit a CU's LDS)
 constexpr int S_E = S_BCAP + 2 * T_MAXR + 64;  // entries of V
 constexpr int S_W = S_E + T_MAXR + 16;      // entries of W (chars, "▁", row sentinels)
 constexpr int S_WORDS = 256;                // words per tile (more: the tile's rows fall back)
