@@ -12,8 +12,11 @@ libraries (sentencepiece, tokenizers) are not used: models are read from their f
 import os
 from typing import List, Optional, Union
 
+import numpy as np
+
 from . import decode as _dec
 from . import engine
+from . import longrows
 from .normalize import normalize_batch
 from .segment import _split, analyze_batch, composition_from, segment_batch
 
@@ -50,7 +53,24 @@ class aksharTokenizer:
 
     # ---------------------------------------------------------------- preprocessing
     def preprocess(self, text: str) -> str:
+        pieces = self._long_pieces(text)
+        if pieces is not None:  # a long row: its exact pieces (longrows.py), normalized as a batch
+            return "".join(normalize_batch(pieces, self.normalize_roman, self.clean_hinglish))
         return normalize_batch([text], self.normalize_roman, self.clean_hinglish)[0]
+
+    @staticmethod
+    def _long_pieces(text):
+        """The exact pieces of a long text (longrows.py), or None for a text kept as one row."""
+        if len(text) * 4 <= longrows.LONG_ROW_BYTES:
+            return None
+        raw = text.encode("utf-8", "surrogatepass")
+        if len(raw) <= longrows.LONG_ROW_BYTES:
+            return None
+        cuts = longrows.cut_points(raw)
+        if len(cuts) == 0:
+            return None
+        b = [0] + [int(c) for c in cuts] + [len(raw)]
+        return [raw[b[i]:b[i + 1]].decode("utf-8", "surrogatepass") for i in range(len(b) - 1)]
 
     def preprocess_batch(self, texts: List[str]) -> List[str]:
         return normalize_batch(texts, self.normalize_roman, self.clean_hinglish)
@@ -74,6 +94,16 @@ class aksharTokenizer:
         return [[int(x) for x in ids[oo[i]:oo[i + 1]]] for i in range(len(texts))]
 
     def encode(self, text: str) -> List[int]:
+        if self.model is None:
+            raise ValueError("need model for IDs")
+        if self.model_type == "bpe":
+            raw = text.encode("utf-8", "surrogatepass")
+            if len(raw) > longrows.LONG_ROW_BYTES:  # one long row -> its exact pieces, one batch, stitched
+                buf, offs = longrows.split_rows(raw)
+                gb, go = engine.to_device(buf, offs)
+                ids, oo = self.encode_packed(gb, go, nbytes=len(raw))
+                return [int(x) for x in longrows.stitch_bpe(ids.cpu().numpy(), oo.cpu().numpy())]
+        # SentencePiece: always one row (its lattice carries a float score across the whole row)
         return self.encode_batch([text])[0]
 
     def decode(self, ids: List[int]) -> str:
@@ -113,6 +143,14 @@ class aksharTokenizer:
         return out
 
     def tokenize(self, text: str, return_metadata: bool = False) -> Union[List[str], dict]:
+        if not return_metadata:
+            if self.model is None:
+                pieces = self._long_pieces(text)
+                if pieces is not None:  # clusters of the exact pieces (longrows.py), concatenated
+                    norms = self.preprocess_batch(pieces)
+                    return [t for n, e in zip(norms, segment_batch(norms)) for t in _split(n, e)]
+            elif self.model_type == "bpe":
+                return self._tokens_for(self.encode(text))
         return self.tokenize_batch([text], return_metadata)[0]
 
     def detokenize(self, tokens: List[str]) -> str:
