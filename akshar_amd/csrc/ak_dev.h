@@ -61,6 +61,8 @@ __device__ __forceinline__ bool p_allowed(uint2 p) { return (p.x >> 26) & 1; }
 __device__ __forceinline__ bool p_lowerchg(uint2 p) { return (p.x >> 27) & 1; }
 __device__ __forceinline__ uint32_t p_normmap(uint2 p) { return p.y & 0xFFFF; }
 __device__ __forceinline__ int p_ccc_hf(uint2 p) { return p_hfccc0(p) ? 0 : p_ccc(p); }
+__device__ __forceinline__ bool p_hfkd(uint2 p) { return (p.x >> 28) & 1; }      // HF NFKD changes it
+__device__ __forceinline__ bool p_hfsecond(uint2 p) { return (p.x >> 29) & 1; }  // second of an HF composite
 
 // ------------------------------------------------------------------------------------------
 // row status bits (include/akshar.h) + internal
@@ -150,18 +152,40 @@ __device__ __forceinline__ int utf8_len(uint32_t cp) {
 constexpr uint32_t H_SBASE = 0xAC00, H_LBASE = 0x1100, H_VBASE = 0x1161, H_TBASE = 0x11A7;
 constexpr uint32_t H_LCOUNT = 19, H_VCOUNT = 21, H_TCOUNT = 28, H_NCOUNT = 588, H_SCOUNT = 11172;
 
+// NFC flavours: NF_UCD = normalize_text's NFC (unicodedata, UCD 13); NF_HF = HF NFKC over the
+// normalize_text alphabet (compat spaces already mapped: NFC with HF's ccc); NF_HFK = the
+// recomposition half of HF's full NFKC (input already HF-NFKD decomposed: no decomposition step,
+// HF's ccc, HF's primary composites).
+constexpr int NF_UCD = 0, NF_HF = 1, NF_HFK = 2;
+
+template <int NF = NF_UCD>
 __device__ __forceinline__ uint32_t compose_pair(uint32_t a, uint32_t b) {
     if (a - H_LBASE < H_LCOUNT && b - H_VBASE < H_VCOUNT)
         return H_SBASE + ((a - H_LBASE) * H_VCOUNT + (b - H_VBASE)) * H_TCOUNT;
     if (a - H_SBASE < H_SCOUNT && (a - H_SBASE) % H_TCOUNT == 0 && b > H_TBASE && b < H_TBASE + H_TCOUNT)
         return a + (b - H_TBASE);
     const uint64_t key = ((uint64_t)a << 21) | b;
-    int lo = 0, hi = AK_UT_NCOMP - 1;
+    const uint64_t *keys = NF == NF_HFK ? AK_UT_HFCOMP_KEY : AK_UT_COMP_KEY;
+    const uint32_t *vals = NF == NF_HFK ? AK_UT_HFCOMP_VAL : AK_UT_COMP_VAL;
+    int lo = 0, hi = (NF == NF_HFK ? AK_UT_NHFCOMP : AK_UT_NCOMP) - 1;
     while (lo <= hi) {
         int mid = (lo + hi) >> 1;
-        uint64_t k = AK_UT_COMP_KEY[mid];
-        if (k == key) return AK_UT_COMP_VAL[mid];
+        uint64_t k = keys[mid];
+        if (k == key) return vals[mid];
         if (k < key) lo = mid + 1; else hi = mid - 1;
+    }
+    return 0;
+}
+
+// HF's (Unicode 9) full compatibility decomposition of cp (not a Hangul syllable): offset << 5 |
+// length into AK_UT_HFKD_FLAT, 0 if HF leaves it unchanged
+__device__ __noinline__ uint32_t hf_kd_find(uint32_t cp) {
+    int lo = 0, hi = AK_UT_NHFKD - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const uint32_t k = AK_UT_HFKD_KEY[mid];
+        if (k == cp) return AK_UT_HFKD_OFF[mid];
+        if (k < cp) lo = mid + 1; else hi = mid - 1;
     }
     return 0;
 }
@@ -169,11 +193,15 @@ __device__ __forceinline__ uint32_t compose_pair(uint32_t a, uint32_t b) {
 // Full NFC of one segment (seg[0..n)) into dec[]: decompose, canonical order, compose.
 // Returns the output length, or -1 if dec[] (dcap entries) overflows. Rare path: not inlined,
 // and it receives only arrays and values so the streaming stages stay in registers.
-template <bool HF>
+template <int HF>
 __device__ __noinline__ int nfc_full(const uint32_t *seg, uint32_t *dec, int n, int dcap, const uint2 *fast) {
     auto cc = [&](uint32_t x) { const uint2 pr = prop(fast, x); return HF ? p_ccc_hf(pr) : p_ccc(pr); };
     int m = 0;
-    for (int i = 0; i < n; ++i) {
+    if constexpr (HF == NF_HFK) {  // already decomposed
+        if (n > dcap) return -1;
+        for (int i = 0; i < n; ++i) dec[i] = seg[i];
+        m = n;
+    } else for (int i = 0; i < n; ++i) {
         const uint32_t cp = seg[i];
         if (cp - H_SBASE < H_SCOUNT) {
             const uint32_t s = cp - H_SBASE;
@@ -207,7 +235,7 @@ __device__ __noinline__ int nfc_full(const uint32_t *seg, uint32_t *dec, int n, 
         const uint32_t ch = dec[i];
         const int c = cc(ch);
         if (starter >= 0) {
-            const uint32_t comp = compose_pair(st, ch);
+            const uint32_t comp = compose_pair<HF>(st, ch);
             if (comp && (lastc < c || lastc == 0)) {
                 st = comp;
                 dec[starter] = comp;
@@ -226,7 +254,7 @@ __device__ __noinline__ int nfc_full(const uint32_t *seg, uint32_t *dec, int n, 
     return w;
 }
 
-template <bool HF, class Next>
+template <int HF, class Next>
 struct NfcStage {
     Next *next;
     const uint2 *fast;
@@ -250,10 +278,11 @@ struct NfcStage {
 
     __device__ __forceinline__ void push(uint32_t cp) {
         const uint2 pr = prop(fast, cp);
-        const bool stable = HF ? (p_ccc_hf(pr) == 0 && !p_second(pr)) : p_stable(pr);
+        const bool stable = HF == NF_HFK ? (p_ccc_hf(pr) == 0 && !p_hfsecond(pr))
+                          : HF ? (p_ccc_hf(pr) == 0 && !p_second(pr)) : p_stable(pr);
         if (stable) {
             flush();
-            p0 = cp; n = 1; work = false; last = 0; p0_dec = p_decomp(pr);
+            p0 = cp; n = 1; work = false; last = 0; p0_dec = HF != NF_HFK && p_decomp(pr);
             return;
         }
         const int c = cc(pr);
@@ -261,7 +290,11 @@ struct NfcStage {
             p0 = cp; n = 1; work = true; last = c; p0_dec = false;
             return;
         }
-        if (p0_dec || p_decomp(pr) || p_second(pr) || c == 0 || c < last) work = true;
+        if constexpr (HF == NF_HFK) {
+            if (p_hfsecond(pr) || c == 0 || c < last) work = true;
+        } else {
+            if (p0_dec || p_decomp(pr) || p_second(pr) || c == 0 || c < last) work = true;
+        }
         last = c;
         if (n == 1) { p1 = cp; n = 2; return; }
         if (n >= sc->seg_cap) { sc->status |= sc->slow_status; return; }
@@ -487,7 +520,15 @@ struct BpeDev {
     const uint16_t *single_sorted_id;
     uint32_t n_single;
     uint32_t bos, eos;
+    // added tokens (HF AddedVocabulary, normalized=false): matched leftmost-longest on the text
+    // the tokenizer receives, before its normalizer (ak_bpe_set_added)
+    const uint32_t *added_cp;    // concatenated code points
+    const uint32_t *added_off;   // n_added + 1 offsets into added_cp
+    const uint32_t *added_id;
+    uint32_t n_added;
 };
+
+constexpr int AK_ADDED_MAXLEN = 16;  // longest added token (code points) the device matcher holds
 
 // two-choice cuckoo lookup (ak_model_build.h): both candidate slots are loaded at once (L2-resident
 // table, plain loads), no probe loop -> no divergence
@@ -649,23 +690,88 @@ struct BpeWordSink {  // after HF NFC: pre-tokenize and merge
     __device__ __forceinline__ void finish() { end_word(); c.put(m->eos); }
 };
 
-struct BpeSink {  // normalized stream -> HF NFKC -> BpeWordSink
+// FULL = false (clean_hinglish: the text is over the normalize_text alphabet): HF NFKC reduces to
+// compat spaces -> ' ' then NFC with HF's ccc. FULL = true (clean_hinglish=False: any text): the
+// added tokens split the text first (HF AddedVocabulary, leftmost-longest), then each piece gets
+// HF's full NFKC (its Unicode 9 NFKD per code point, Hangul algorithmic, then NF_HFK recomposition)
+// and is pre-tokenized on its own.
+template <bool FULL = false>
+struct BpeSink {
     BpeWordSink words;
-    NfcStage<true, BpeWordSink> nfc;
+    NfcStage<FULL ? NF_HFK : NF_HF, BpeWordSink> nfc;
     const uint2 *fast;
+    const BpeDev *m;
+    uint32_t abuf[FULL ? AK_ADDED_MAXLEN : 1];
+    int na;
     __device__ __forceinline__ void init(const BpeDev *md, const uint2 *f, const uint16_t *sf, Scratch *s,
                                          Cursor<uint32_t> cur) {
         fast = f;
+        m = md;
+        na = 0;
         words.c = cur;
         words.init(md, f, sf, s);
         nfc.init(&words, f, s);
         words.c.put(md->bos);
     }
-    __device__ __forceinline__ void push(uint32_t cp) {
-        if (p_hfspace(prop(fast, cp))) cp = 0x20u;
-        nfc.push(cp);
+    // one code point of a piece: HF NFKD, then the recomposition stage
+    __device__ void text(uint32_t cp) {
+        if (cp - H_SBASE < H_SCOUNT) {
+            const uint32_t q = cp - H_SBASE;
+            nfc.push(H_LBASE + q / H_NCOUNT);
+            nfc.push(H_VBASE + (q % H_NCOUNT) / H_TCOUNT);
+            if (q % H_TCOUNT) nfc.push(H_TBASE + q % H_TCOUNT);
+            return;
+        }
+        if (!p_hfkd(prop(fast, cp))) { nfc.push(cp); return; }
+        const uint32_t o = hf_kd_find(cp);
+        for (uint32_t k = 0; k < (o & 31u); ++k) nfc.push(AK_UT_HFKD_FLAT[(o >> 5) + k]);
     }
-    __device__ __forceinline__ void finish() { nfc.finish(); }
+    __device__ void special(uint32_t id) {
+        nfc.flush();
+        words.end_word();
+        words.c.put(id);
+    }
+    __device__ bool is_first(uint32_t cp) const {
+        for (uint32_t t = 0; t < m->n_added; ++t) if (m->added_cp[m->added_off[t]] == cp) return true;
+        return false;
+    }
+    // leftmost-longest: decide at abuf[0] once no added token can extend past the buffer
+    __device__ void resolve(bool final) {
+        while (na > 0) {
+            int best = -1, blen = 0;
+            bool extend = false;
+            for (uint32_t t = 0; t < m->n_added; ++t) {
+                const uint32_t o = m->added_off[t];
+                const int len = (int)(m->added_off[t + 1] - o);
+                const int k = len < na ? len : na;
+                bool eq = true;
+                for (int j = 0; j < k && eq; ++j) eq = m->added_cp[o + j] == abuf[j];
+                if (!eq) continue;
+                if (len > na) extend = true;
+                else if (len > blen) { best = (int)t; blen = len; }
+            }
+            if (extend && !final) return;
+            int drop = 1;
+            if (best >= 0) { special(m->added_id[best]); drop = blen; }
+            else text(abuf[0]);
+            for (int j = drop; j < na; ++j) abuf[j - drop] = abuf[j];
+            na -= drop;
+        }
+    }
+    __device__ __forceinline__ void push(uint32_t cp) {
+        if constexpr (FULL) {
+            if (na == 0 && (m->n_added == 0 || !is_first(cp))) { text(cp); return; }
+            abuf[na++] = cp;
+            resolve(false);
+        } else {
+            if (p_hfspace(prop(fast, cp))) cp = 0x20u;
+            nfc.push(cp);
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if constexpr (FULL) resolve(true);
+        nfc.finish();
+    }
 };
 
 // ------------------------------------------------------------------------------------------

@@ -121,6 +121,7 @@ struct ak_bpe {
     uint16_t *d_single_id = nullptr;
     bool tile_ok = false;  // every id < 0x7FFC (the tile kernel tags ids with bit 15, ak_tile.h WSTART) and
                            // new ids strictly increasing with rank (it compares merges by new id)
+    uint32_t *d_added = nullptr;  // added tokens: code points, offsets, ids (one allocation)
 };
 
 struct ak_spm {
@@ -180,7 +181,50 @@ extern "C" void ak_bpe_free(ak_bpe *m) {
     (void)hipFree(m->d_single_fast);
     (void)hipFree(m->d_single_cp);
     (void)hipFree(m->d_single_id);
+    (void)hipFree(m->d_added);
     delete m;
+}
+
+// normalize_text's allowlist (normalize.py:97-103): a char an added token needs that survives
+// clean_hinglish. \s is Python's str.isspace().
+static bool survives_clean(uint32_t c) {
+    if ((c >= 0x0900 && c <= 0x09FF) || (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'))
+        return true;
+    if (c < 0x80 && strchr(".,!?;:'\"-", (int)c) && c) return true;
+    return (c >= 0x09 && c <= 0x0D) || (c >= 0x1C && c <= 0x20) || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+           (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+}
+
+extern "C" int ak_bpe_set_added(ak_bpe *m, uint32_t n, const uint32_t *cps, const uint32_t *cp_offs,
+                                const uint32_t *ids) {
+    if (!m || (n && (!cps || !cp_offs || !ids))) return fail(AK_ERR_ARG, "ak_bpe_set_added: null argument");
+    if (n > AK_MAX_ADDED) return fail(AK_ERR_UNSUPPORTED, "ak_bpe_set_added: too many added tokens");
+    for (uint32_t t = 0; t < n; ++t) {
+        const uint32_t len = cp_offs[t + 1] - cp_offs[t];
+        if (cp_offs[t + 1] < cp_offs[t] || len == 0 || len > (uint32_t)AK_ADDED_MAXLEN)
+            return fail(AK_ERR_UNSUPPORTED, "ak_bpe_set_added: an added token must hold 1..16 code points");
+        bool all = true;
+        for (uint32_t k = cp_offs[t]; k < cp_offs[t + 1]; ++k) all = all && survives_clean(cps[k]);
+        if (all)
+            return fail(AK_ERR_UNSUPPORTED, "ak_bpe_set_added: an added token made only of allowlisted chars "
+                                            "could survive clean_hinglish (not supported)");
+    }
+    const uint32_t ncp = n ? cp_offs[n] : 0;
+    std::vector<uint32_t> h;
+    h.insert(h.end(), cps, cps + ncp);
+    const size_t off_at = h.size();
+    for (uint32_t t = 0; t <= n; ++t) h.push_back(n ? cp_offs[t] - cp_offs[0] : 0);
+    const size_t id_at = h.size();
+    h.insert(h.end(), ids, ids + n);
+    (void)hipFree(m->d_added);
+    m->d_added = nullptr;
+    HIP_TRY(hipMalloc(&m->d_added, h.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(m->d_added, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    m->dev.added_cp = m->d_added;
+    m->dev.added_off = m->d_added + off_at;
+    m->dev.added_id = m->d_added + id_at;
+    m->dev.n_added = n;
+    return AK_OK;
 }
 
 extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
@@ -570,12 +614,12 @@ extern "C" int ak_bpe_encode(const ak_bpe *m, ak_ws *w, int flags, const uint8_t
     if (!m) return fail(AK_ERR_ARG, "ak_bpe_encode: null model");
     int rc = check_common(w, in, offs, n, ids, out_offs);
     if (rc) return rc;
-    if (flags != 2 && flags != 3)
-        return fail(AK_ERR_UNSUPPORTED, "ak_bpe_encode: clean_hinglish=False is not supported (HF NFKC tables cover the normalized alphabet only)");
+    if (flags < 0 || flags > 3) return fail(AK_ERR_ARG, "ak_bpe_encode: flags must be 0..3");
     RowArgs a = make_args(in, offs, n, ids, cap, row_status);
     a.bpe = m->dev;
     a.single_fast = m->d_single_fast;
-    if (!m->tile_ok) return launch_bpe(flags, w, a, out_offs, (hipStream_t)stream);
+    // clean_hinglish=False (flags 0, 1): any text, HF's full NFKC and the added-token split: the row path
+    if (!m->tile_ok || flags < 2) return launch_bpe(flags, w, a, out_offs, (hipStream_t)stream);
     return dispatch(OP_BPE, flags, w, a, out_offs, (hipStream_t)stream);
 }
 

@@ -183,7 +183,7 @@ __device__ __forceinline__ uint64_t process_row(const RowArgs &a, uint64_t r, co
         run_input<FLAGS>(s, fast, sc, rd, b, e);
         return s.c.pos - base;
     } else if constexpr (OP == OP_BPE) {
-        BpeSink s;
+        BpeSink<(FLAGS & 2) == 0> s;
         s.init(&a.bpe, fast, sfast, sc, Cursor<uint32_t>{(uint32_t *)a.out, base, cap, EMIT});
         run_input<FLAGS>(s, fast, sc, rd, b, e);
         return s.words.c.pos - base;

@@ -233,6 +233,9 @@ class BPE:
                                            len(merges), merges.ctypes.data, m.bos, m.eos, ctypes.byref(h)),
                   "ak_bpe_create")
         self.h = h
+        cps, aoffs, aids = m.added_arrays()
+        check(_lib.lib().ak_bpe_set_added(h, len(aids), cps.ctypes.data, aoffs.ctypes.data, aids.ctypes.data),
+              "ak_bpe_set_added")
 
     def __del__(self):
         h = getattr(self, "h", None)

@@ -64,6 +64,22 @@ class BPEModel:
         self.bos_token, self.eos_token = ids[0], ids[2]
         # HF decode with no decoder configured: tokens joined by ' ' (special tokens skipped)
         self.special_ids = {int(a["id"]) for a in j.get("added_tokens", []) if a.get("special")}
+        # AddedVocabulary: split the text on these before the normalizer (ak_bpe_set_added)
+        self.added = []
+        for a in j.get("added_tokens", []):
+            for k in ("single_word", "lstrip", "rstrip", "normalized"):
+                if a.get(k, False):
+                    raise NotImplementedError("added token %r with %s=True not supported" % (a["content"], k))
+            self.added.append((a["content"], int(a["id"])))
+
+    def added_arrays(self):
+        """(u32 code points, u32 offsets[n+1], u32 ids) of the added tokens."""
+        cps, offs = [], [0]
+        for content, _ in self.added:
+            cps.extend(ord(c) for c in content)
+            offs.append(len(cps))
+        return (np.asarray(cps, dtype=np.uint32), np.asarray(offs, dtype=np.uint32),
+                np.asarray([i for _, i in self.added], dtype=np.uint32))
 
 
 # ----------------------------------------------------------------------------------------------

@@ -98,7 +98,8 @@ class aksharTokenizer:
             raise ValueError("need model for IDs")
         if self.model_type == "bpe":
             raw = text.encode("utf-8", "surrogatepass")
-            if len(raw) > longrows.LONG_ROW_BYTES:  # one long row -> its exact pieces, one batch, stitched
+            cuts_ok = not any(" " in c or "\n" in c for c, _ in self.model.model.added)  # no added token spans a cut
+            if len(raw) > longrows.LONG_ROW_BYTES and cuts_ok:  # one long row -> its exact pieces, stitched
                 buf, offs = longrows.split_rows(raw)
                 gb, go = engine.to_device(buf, offs)
                 ids, oo = self.encode_packed(gb, go, nbytes=len(raw))

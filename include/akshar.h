@@ -91,6 +91,15 @@ int ak_ws_check(ak_ws *ws);
 int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const uint32_t *single_id,
                   uint32_t n_merges, const uint32_t *merges, uint32_t bos, uint32_t eos, ak_bpe **out);
 void ak_bpe_free(ak_bpe *m);
+/* The tokenizer's added tokens (tokenizer.json "added_tokens": <pad> <unk> <s> </s> <mask> for
+ * cli.py:283-285), all normalized=false / lstrip=rstrip=single_word=false: HF's AddedVocabulary
+ * splits the text it receives on them (leftmost-longest) BEFORE the NFKC normalizer, each match
+ * becoming its id and each piece between encoded on its own. Only reachable with
+ * clean_hinglish=False (the allowlist drops '<' '>' '/'); a token made only of allowlisted chars is
+ * AK_ERR_UNSUPPORTED. n tokens <= AK_MAX_ADDED, each 1..16 code points: cps packed with
+ * cp_offs[n+1]. Host pointers; replaces any previous set. */
+#define AK_MAX_ADDED 64
+int ak_bpe_set_added(ak_bpe *m, uint32_t n, const uint32_t *cps, const uint32_t *cp_offs, const uint32_t *ids);
 
 /* Replaces SentencePieceProcessor.Load(path) (tokenizer.py:88-90) for the unigram model
  * cli.py:232-248 trains (identity normalizer, byte_fallback). pieces: n UTF-8 strings packed in
@@ -129,7 +138,10 @@ int ak_analyze(ak_ws *ws, int flags, int matras, const uint8_t *in, const uint64
                uint8_t *row_status, void *stream);
 
 /* aksharTokenizer(model, "bpe").encode(text) (tokenizer.py:167-193): normalize_text(flags) then
- * the HF pipeline; ids include <s> ... </s>. flags must include AK_NORM_CLEAN. */
+ * the HF pipeline; ids include <s> ... </s>. Any flags 0..3: with AK_NORM_CLEAN the normalized
+ * text is over the allowlist (tile path for flags 3); without it (clean_hinglish=False) any text
+ * reaches the tokenizer: added-token split, HF's full NFKC (Unicode 9 tables of tokenizers
+ * 0.22.2) and the Whitespace pre-tokenizer over every code point, one lane per row. */
 int ak_bpe_encode(const ak_bpe *m, ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
                   uint32_t *ids, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
 
@@ -169,7 +181,10 @@ int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
 #define AK_TILE_NPASS 10
 int ak_profile_tile_passes(ak_ws *ws, uint64_t *cycles, int n);
 
-/* Always-sufficient output capacities (elements) for n rows of total_bytes input bytes. */
+/* Always-sufficient output capacities (elements) for n rows of total_bytes input bytes.
+ * ak_bpe_encode_cap holds for flags 2 / 3; with clean_hinglish=False (flags 0 / 1) NFKC can
+ * expand a char (U+FDFA: 3 bytes -> 18 code points): AK_BPE_NFKC_EXPANSION * total_bytes + 2n + 16. */
+#define AK_BPE_NFKC_EXPANSION 6
 uint64_t ak_normalize_cap(uint64_t n, uint64_t total_bytes);
 uint64_t ak_segment_cap(uint64_t n, uint64_t total_bytes);
 uint64_t ak_bpe_encode_cap(uint64_t n, uint64_t total_bytes);

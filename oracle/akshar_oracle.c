@@ -352,6 +352,8 @@ typedef struct or_bpe {
     uint32_t n_merges;
     merge_t *merges;                  /* sorted by key */
     uint32_t bos, eos;
+    uint32_t n_added;                 /* added tokens (tokenizer.json added_tokens) */
+    uint32_t *added_cp, *added_off, *added_id;
 } or_bpe;
 
 static int cmp_u64pair(const void *a, const void *b) {
@@ -389,7 +391,21 @@ or_bpe *or_bpe_create(uint32_t n_single, const uint32_t *single_cp, const uint32
 
 void or_bpe_free(or_bpe *m) {
     if (!m) return;
-    free(m->single_cp); free(m->single_id); free(m->merges); free(m);
+    free(m->single_cp); free(m->single_id); free(m->merges);
+    free(m->added_cp); free(m->added_off); free(m->added_id); free(m);
+}
+
+/* tokenizers AddedVocabulary (normalized=false tokens): kept as code point strings */
+void or_bpe_set_added(or_bpe *m, uint32_t n, const uint32_t *cps, const uint32_t *cp_offs, const uint32_t *ids) {
+    free(m->added_cp); free(m->added_off); free(m->added_id);
+    m->n_added = n;
+    uint32_t ncp = n ? cp_offs[n] : 0;
+    m->added_cp = (uint32_t *)malloc(sizeof(uint32_t) * (ncp ? ncp : 1));
+    m->added_off = (uint32_t *)malloc(sizeof(uint32_t) * (n + 1));
+    m->added_id = (uint32_t *)malloc(sizeof(uint32_t) * (n ? n : 1));
+    if (ncp) memcpy(m->added_cp, cps, sizeof(uint32_t) * ncp);
+    for (uint32_t t = 0; t <= n; ++t) m->added_off[t] = n ? cp_offs[t] : 0;
+    if (n) memcpy(m->added_id, ids, sizeof(uint32_t) * n);
 }
 
 static int64_t single_lookup(const or_bpe *m, uint32_t cp) {
@@ -450,21 +466,121 @@ static void bpe_word(const or_bpe *m, const uint32_t *w, size_t n, vec_t *ids) {
 
 enum { HF_W = 0, HF_P = 1, HF_S = 2 };
 
-static void bpe_encode_cps(const or_bpe *m, vec_t *s, vec_t *ids) {
-    /* HF NFKC over the normalized alphabet: compat spaces -> U+0020, then NFC with HF's ccc */
-    for (size_t i = 0; i < s->n; ++i) if (hf_space(s->v[i])) s->v[i] = 0x20;
-    nfc_string(s, ccc_hf);
-    vpush(ids, m->bos);
-    /* Whitespace pre-tokenizer: \w+ | [^\w\s]+ */
+/* HF tokenizers' NFKC (the unicode-normalization-alignments crate, Unicode 9.0 data): full
+ * compatibility decomposition (HF's own per-code-point NFKD, Hangul algorithmic), canonical
+ * ordering by HF's ccc, canonical composition over HF's primary composites. Tables generated by
+ * tools/gen_tables.py from tokenizers 0.22.2 itself (checked there on every code point and on
+ * 300,000 random strings). Used for every flags value: over the normalize_text alphabet it
+ * reduces to "compat spaces -> U+0020, then NFC" (cli.py:276-282 normalizer = NFKC). */
+static uint32_t hf_kd_find(uint32_t cp) {
+    int lo = 0, hi = AK_UT_NHFKD - 1;
+    while (lo <= hi) {
+        int mid = (lo + hi) / 2;
+        if (AK_UT_HFKD_KEY[mid] == cp) return AK_UT_HFKD_OFF[mid];
+        if (AK_UT_HFKD_KEY[mid] < cp) lo = mid + 1; else hi = mid - 1;
+    }
+    return 0;
+}
+
+static uint32_t hf_compose_pair(uint32_t a, uint32_t b) {
+    if (a >= H_LBASE && a < H_LBASE + H_LCOUNT && b >= H_VBASE && b < H_VBASE + H_VCOUNT)
+        return H_SBASE + ((a - H_LBASE) * H_VCOUNT + (b - H_VBASE)) * H_TCOUNT;
+    if (a >= H_SBASE && a < H_SBASE + H_SCOUNT && (a - H_SBASE) % H_TCOUNT == 0 && b > H_TBASE &&
+        b < H_TBASE + H_TCOUNT)
+        return a + (b - H_TBASE);
+    uint64_t key = ((uint64_t)a << 21) | b;
+    int lo = 0, hi = AK_UT_NHFCOMP - 1;
+    while (lo <= hi) {
+        int mid = (lo + hi) / 2;
+        if (AK_UT_HFCOMP_KEY[mid] == key) return AK_UT_HFCOMP_VAL[mid];
+        if (AK_UT_HFCOMP_KEY[mid] < key) lo = mid + 1; else hi = mid - 1;
+    }
+    return 0;
+}
+
+static void hf_nfkc_string(vec_t *s) {
+    vec_t d = {0};
+    for (size_t i = 0; i < s->n; ++i) {
+        uint32_t cp = s->v[i];
+        if (cp >= H_SBASE && cp < H_SBASE + H_SCOUNT) {
+            uint32_t q = cp - H_SBASE;
+            vpush(&d, H_LBASE + q / H_NCOUNT);
+            vpush(&d, H_VBASE + (q % H_NCOUNT) / H_TCOUNT);
+            if (q % H_TCOUNT) vpush(&d, H_TBASE + q % H_TCOUNT);
+            continue;
+        }
+        uint32_t o = hf_kd_find(cp);
+        if (!o) { vpush(&d, cp); continue; }
+        for (uint32_t k = 0; k < (o & 31); ++k) vpush(&d, AK_UT_HFKD_FLAT[(o >> 5) + k]);
+    }
+    for (size_t i = 1; i < d.n; ++i) {
+        int c = ccc_hf(d.v[i]);
+        if (c == 0) continue;
+        size_t j = i;
+        uint32_t x = d.v[i];
+        while (j > 0 && ccc_hf(d.v[j - 1]) > c) { d.v[j] = d.v[j - 1]; --j; }
+        d.v[j] = x;
+    }
+    s->n = 0;
+    if (d.n) {
+        size_t starter = 0;
+        vpush(s, d.v[0]);
+        int last = ccc_hf(d.v[0]);
+        if (last != 0) last = 256;
+        for (size_t i = 1; i < d.n; ++i) {
+            uint32_t ch = d.v[i];
+            int c = ccc_hf(ch);
+            uint32_t comp = hf_compose_pair(s->v[starter], ch);
+            if (comp && (last < c || last == 0)) {
+                s->v[starter] = comp;
+                continue;
+            }
+            if (c == 0) starter = s->n;
+            last = c;
+            vpush(s, ch);
+        }
+    }
+    vfree(&d);
+}
+
+/* one piece of text between added tokens: NFKC, Whitespace pre-tokenizer (\w+ | [^\w\s]+), BPE */
+static void bpe_piece(const or_bpe *m, const uint32_t *cp, size_t n, vec_t *ids) {
+    vec_t s = {0};
+    for (size_t i = 0; i < n; ++i) vpush(&s, cp[i]);
+    hf_nfkc_string(&s);
     size_t i = 0;
-    while (i < s->n) {
-        int c = hf_class(s->v[i]);
+    while (i < s.n) {
+        int c = hf_class(s.v[i]);
         if (c == HF_S) { ++i; continue; }
         size_t j = i + 1;
-        while (j < s->n && hf_class(s->v[j]) == c) ++j;
-        bpe_word(m, s->v + i, j - i, ids);
+        while (j < s.n && hf_class(s.v[j]) == c) ++j;
+        bpe_word(m, s.v + i, j - i, ids);
         i = j;
     }
+    vfree(&s);
+}
+
+/* Tokenizer.encode: AddedVocabulary.extract_and_normalize splits the text on the added tokens
+ * (aho-corasick, leftmost-longest; normalized=false tokens match the raw text), each piece is
+ * normalized and pre-tokenized on its own, then TemplateProcessing adds <s> ... </s>. */
+static void bpe_encode_cps(const or_bpe *m, vec_t *s, vec_t *ids) {
+    vpush(ids, m->bos);
+    size_t start = 0, i = 0;
+    while (i < s->n) {
+        int best = -1;
+        uint32_t blen = 0;
+        for (uint32_t t = 0; t < m->n_added; ++t) {
+            uint32_t len = m->added_off[t + 1] - m->added_off[t];
+            if (len <= blen || i + len > s->n) continue;
+            if (memcmp(s->v + i, m->added_cp + m->added_off[t], len * sizeof(uint32_t)) == 0) { best = (int)t; blen = len; }
+        }
+        if (best < 0) { ++i; continue; }
+        bpe_piece(m, s->v + start, i - start, ids);
+        vpush(ids, m->added_id[best]);
+        i += blen;
+        start = i;
+    }
+    bpe_piece(m, s->v + start, s->n - start, ids);
     vpush(ids, m->eos);
 }
 

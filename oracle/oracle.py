@@ -27,6 +27,8 @@ def lib():
         L.or_bpe_create.restype = P
         L.or_bpe_create.argtypes = [ctypes.c_uint32, P, P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint32]
         L.or_bpe_free.argtypes = [P]
+        L.or_bpe_set_added.restype = None
+        L.or_bpe_set_added.argtypes = [P, ctypes.c_uint32, P, P, P]
         L.or_spm_create.restype = P
         L.or_spm_create.argtypes = [ctypes.c_uint32, P, P, P, P, ctypes.c_int32, P]
         L.or_spm_free.argtypes = [P]
@@ -63,6 +65,8 @@ class OracleBPE:
         self.h = lib().or_bpe_create(len(model.single_cp), _p(model.single_cp), _p(model.single_id),
                                      len(model.merges), _p(np.ascontiguousarray(model.merges)),
                                      model.bos, model.eos)
+        cps, offs, ids = model.added_arrays()
+        lib().or_bpe_set_added(self.h, len(ids), _p(cps), _p(offs), _p(ids))
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.jsonl.gz")
 GOLDEN_TIES = os.path.join(ROOT, "tests", "golden", "spm_ties.npz")
+GOLDEN_NFKC = os.path.join(ROOT, "tests", "golden", "golden_nfkc.jsonl.gz")
 BPE_PATH = os.path.join(ROOT, "models", "akshar.json")
 SPM_PATH = os.path.join(ROOT, "models", "akshar.model")
 
@@ -22,6 +23,12 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden():
     with gzip.open(GOLDEN, "rt", encoding="utf-8") as f:
+        return [json.loads(line) for line in f]
+
+
+@pytest.fixture(scope="session")
+def golden_nfkc():
+    with gzip.open(GOLDEN_NFKC, "rt", encoding="utf-8") as f:
         return [json.loads(line) for line in f]
 
 

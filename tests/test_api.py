@@ -143,8 +143,16 @@ def test_model_tokenize_and_flag_variants_on_golden(golden):
     for key, nr, ch in (("nolower", False, True), ("noclean", True, False), ("nfc", False, False)):
         tk = aksharTokenizer(model_path=SPM_PATH, model_type="sentencepiece", normalize_roman=nr, clean_hinglish=ch)
         assert tk.encode_batch(texts) == [r["spm_" + key] for r in golden], key
-    tk = aksharTokenizer(model_path=BPE_PATH, model_type="bpe", normalize_roman=False)
-    assert tk.encode_batch(texts) == [r["bpe_nolower"] for r in golden]
+    for key, nr, ch in (("nolower", False, True), ("noclean", True, False), ("nfc", False, False)):
+        tk = aksharTokenizer(model_path=BPE_PATH, model_type="bpe", normalize_roman=nr, clean_hinglish=ch)
+        assert tk.encode_batch(texts) == [r["bpe_" + key] for r in golden], key
+    # a long clean_hinglish=False row: cut at exact points (longrows.py) and stitched == the oracle's one row
+    from akshar_amd.models import BPEModel
+    from oracle import oracle as O
+    tk = aksharTokenizer(model_path=BPE_PATH, model_type="bpe", clean_hinglish=False)
+    long = " ".join(["<s>Ｈｉ", "ﬁne</s>", "ﷺ", "yaaar", "नमस्ते", "각"] * 3000)
+    ref, _ = O.OracleBPE(BPEModel(BPE_PATH)).encode_batch(*O.pack([long]), flags=1)
+    assert tk.encode(long) == [int(x) for x in ref]
 
 
 @gpu

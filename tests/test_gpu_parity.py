@@ -191,11 +191,44 @@ def test_spm_near_tie_rows(eng, spm_model):
         assert got[i] == [int(x) for x in z["ids_%d" % i]], i
 
 
-@pytest.mark.parametrize("key,flags", [("spm_nolower", 2), ("spm_noclean", 1), ("spm_nfc", 0), ("bpe_nolower", 2)])
+@pytest.mark.parametrize("key,flags", [("spm_nolower", 2), ("spm_noclean", 1), ("spm_nfc", 0), ("bpe_nolower", 2),
+                                       ("bpe_noclean", 1), ("bpe_nfc", 0)])
 def test_flag_variants_golden(golden, gpacked, eng, bpe_model, spm_model, key, flags):
     model = eng.SPM(spm_model) if key.startswith("spm") else eng.BPE(bpe_model)
     ids, oo = model.encode_batch(*gpacked, flags=flags)
     assert _bad(golden, key, rows_ints(_cpu(ids), _cpu(oo))) == []
+
+
+def test_nfkc_golden_gpu(golden_nfkc, eng, bpe_model, spm_model):
+    """clean_hinglish=False on 3,019 NFKC / pre-tokenizer / added-token strings
+    (tools/gen_golden_nfkc.py): normalize, BPE (BpeSink<true>) and SPM == the reference."""
+    texts = [r["text"] for r in golden_nfkc]
+    buf, offs = O.pack(texts)
+    gb, go = _to_dev(eng, buf, offs.astype(np.int64))
+    for key, flags in (("norm_noclean", 1), ("norm_nfc", 0)):
+        nb, no = eng.normalize_batch(gb, go, flags=flags)
+        nb, no = _cpu(nb), _cpu(no)
+        got = [bytes(nb[no[i]:no[i + 1]]).decode("utf-8") for i in range(len(texts))]
+        assert [i for i, r in enumerate(golden_nfkc) if got[i] != r[key]] == [], key
+    for key, flags in (("bpe_noclean", 1), ("bpe_nfc", 0), ("spm_noclean", 1), ("spm_nfc", 0)):
+        model = eng.BPE(bpe_model) if key.startswith("bpe") else eng.SPM(spm_model)
+        ids, oo = model.encode_batch(gb, go, flags=flags)
+        got = rows_ints(_cpu(ids), _cpu(oo))
+        assert [i for i, r in enumerate(golden_nfkc) if got[i] != r[key]] == [], key
+
+
+def test_bpe_noclean_long_rows_vs_oracle(eng, bpe_model):
+    """clean_hinglish=False rows past the fast buffers: NFKC expansion (U+FDFA: 18 code points),
+    added tokens back to back, a long mark run HF reorders, one huge pre-token -> slow / huge tiers."""
+    texts = ["\ufdfa" * 3000, "<s></s><mask>" * 2000, "a" + "\u0301\u0316" * 3000 + " x",
+             "Ａ" * 20000, "ｶﾞ" * 5000 + "<unk>" + "각" * 3000, "ﬃ" * 9000]
+    buf, offs = O.pack(texts)
+    gb, go = _to_dev(eng, buf, offs.astype(np.int64))
+    for flags in (1, 0):
+        ids, oo = eng.BPE(bpe_model).encode_batch(gb, go, flags=flags)
+        ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs, flags=flags)
+        assert np.array_equal(_cpu(oo).astype(np.uint64), ro), flags
+        assert np.array_equal(_cpu(ids).astype(np.uint32), ref), flags
 
 
 def test_spm_large_batch_vs_oracle(eng, spm_model):

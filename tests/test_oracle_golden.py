@@ -58,9 +58,27 @@ def test_spm_flag_variants(golden, packed, spm_model, key, flags):
     assert _mismatches(golden, key, rows_ints(ids, oo)) == []
 
 
-def test_bpe_nolower(golden, packed, bpe_model):
-    ids, oo = O.OracleBPE(bpe_model).encode_batch(*packed, flags=2)
-    assert _mismatches(golden, "bpe_nolower", rows_ints(ids, oo)) == []
+@pytest.mark.parametrize("key,flags", [("bpe_nolower", 2), ("bpe_noclean", 1), ("bpe_nfc", 0)])
+def test_bpe_flag_variants(golden, packed, bpe_model, key, flags):
+    """clean_hinglish=False reaches HF's full NFKC and the added-token split (oracle bpe_encode_cps)."""
+    ids, oo = O.OracleBPE(bpe_model).encode_batch(*packed, flags=flags)
+    assert _mismatches(golden, key, rows_ints(ids, oo)) == []
+
+
+def test_nfkc_golden(golden_nfkc, bpe_model, spm_model):
+    """3,019 strings over the code points HF NFKC / the pre-tokenizer / the added tokens treat
+    specially (tools/gen_golden_nfkc.py), clean_hinglish=False: normalize, BPE and SPM == reference."""
+    texts = [r["text"] for r in golden_nfkc]
+    packed = O.pack(texts)
+    for key, flags in (("norm_noclean", 1), ("norm_nfc", 0)):
+        nb, no = O.normalize_batch(*packed, flags=flags)
+        got = [bytes(nb[no[i]:no[i + 1]]).decode("utf-8") for i in range(len(texts))]
+        assert [i for i, r in enumerate(golden_nfkc) if got[i] != r[key]] == [], key
+    for key, flags in (("bpe_noclean", 1), ("bpe_nfc", 0), ("spm_noclean", 1), ("spm_nfc", 0)):
+        o = O.OracleBPE(bpe_model) if key.startswith("bpe") else O.OracleSPM(spm_model)
+        ids, oo = o.encode_batch(*packed, flags=flags)
+        got = rows_ints(ids, oo)
+        assert [i for i, r in enumerate(golden_nfkc) if got[i] != r[key]] == [], key
 
 
 def test_spm_near_tie_rows(spm_model):

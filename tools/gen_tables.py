@@ -19,6 +19,7 @@ The GPU box never runs this; it uses the committed header.
 """
 import json
 import os
+import random
 import sys
 import unicodedata
 
@@ -154,6 +155,7 @@ def main():
     # version is ccc 0 to it and never reordered (U+09FE BENGALI SANDHI MARK, Unicode 10).
     # Probe each alphabet mark against the nukta (ccc 7): HF reorders iff it knows the mark.
     hf_ccc_zero = [0] * NCP
+    alpha_set = set(alpha)
     for c in alpha:
         if ccc[c] > 7:
             got = nfkc.normalize_str("a" + chr(c) + "़")
@@ -162,6 +164,113 @@ def main():
 
     def hf_ccc(c):
         return 0 if hf_ccc_zero[c] else ccc[c]
+
+    # ---------------- HF NFKC over ALL code points (clean_hinglish=False) ----------------
+    # tokenizers 0.22.2 normalizes with Unicode 9.0 tables (U+09FE, Unicode 10, is unknown to it).
+    # Per code point: HF's full NFKD (Hangul syllables excepted: algorithmic), HF's ccc (UCD 13's
+    # for the marks HF knows, probed against U+0334 ccc 1 / U+0301 ccc 230), HF's primary
+    # composites (the UCD 13 pairs HF's NFC recomposes) and the Whitespace pre-tokenizer class of
+    # every code point. The model (decompose, reorder, compose) is checked against HF's NFKC on
+    # every code point and on random strings over the decomposing / combining / composing chars.
+    nfd_hf = normalizers.NFD()
+    nfkd_hf = normalizers.NFKD()
+    nfc_hf = normalizers.NFC()
+    surr = range(0xD800, 0xE000)
+    hf_kd = {}
+    for c in range(NCP):
+        if c in surr or 0xAC00 <= c <= 0xD7A3:
+            continue
+        k = nfkd_hf.normalize_str(chr(c))
+        if k != chr(c):
+            hf_kd[c] = [ord(x) for x in k]
+    for c in range(NCP):
+        if c in surr or ccc[c] == 0:
+            continue
+        if ccc[c] > 1:
+            s = "a" + chr(c) + "\u0334"
+            known = nfd_hf.normalize_str(s) != s
+        else:
+            s = "a\u0301" + chr(c)
+            known = nfd_hf.normalize_str(s) != s
+        hf_ccc_zero[c] = 0 if known else 1
+    hf_pairs = {ab: c for ab, c in pairs.items() if nfc_hf.normalize_str(chr(ab[0]) + chr(ab[1])) == chr(c)}
+    hf_second = set(b for _, b in hf_pairs) | hangul_vt
+    for c in range(NCP):
+        if c in surr:
+            hf_class[c] = HF_CLASS["P"]
+            continue
+        if c in alpha_set:
+            continue
+        ch = chr(c)
+        toks = ws.pre_tokenize_str(ch)
+        if not toks:
+            cls = "S"
+        else:
+            cls = "W" if len(ws.pre_tokenize_str("a" + ch)) == 1 else "P"
+        hf_class[c] = HF_CLASS[cls]
+
+    def hf_nfkc_model(text):
+        d = []
+        for ch in text:
+            c = ord(ch)
+            if 0xAC00 <= c <= 0xD7A3:
+                s_ = c - 0xAC00
+                d += [0x1100 + s_ // 588, 0x1161 + (s_ % 588) // 28] + ([0x11A7 + s_ % 28] if s_ % 28 else [])
+            else:
+                d += hf_kd.get(c, [c])
+        for i in range(1, len(d)):  # canonical ordering (stable)
+            x = d[i]
+            k = hf_ccc(x)
+            if k == 0:
+                continue
+            j = i
+            while j > 0 and hf_ccc(d[j - 1]) > k:
+                d[j] = d[j - 1]
+                j -= 1
+            d[j] = x
+        out = []
+        st = -1
+        lastc = 0
+        for i, x in enumerate(d):
+            k = hf_ccc(x)
+            if st >= 0 and (lastc < k or lastc == 0):
+                a = out[st]
+                comp = 0
+                if 0x1100 <= a < 0x1113 and 0x1161 <= x < 0x1176:
+                    comp = 0xAC00 + ((a - 0x1100) * 21 + (x - 0x1161)) * 28
+                elif 0xAC00 <= a <= 0xD7A3 and (a - 0xAC00) % 28 == 0 and 0x11A7 < x < 0x11A7 + 28:
+                    comp = a + (x - 0x11A7)
+                else:
+                    comp = hf_pairs.get((a, x), 0)
+                if comp:
+                    out[st] = comp
+                    continue
+            if i == 0 and k != 0:
+                lastc = 256
+                out.append(x)
+                continue
+            if k == 0:
+                st = len(out)
+            lastc = k
+            out.append(x)
+        return "".join(map(chr, out))
+
+    for c in range(NCP):
+        if c in surr:
+            continue
+        ch = chr(c)
+        if nfkc.normalize_str(ch) != hf_nfkc_model(ch):
+            raise SystemExit("HF NFKC model differs on U+%04X" % c)
+    pool = sorted(set(hf_kd) | set(c for c in range(NCP) if ccc[c] and c not in surr) |
+                  set(a for a, _ in hf_pairs) | hf_second | set(range(0x1100, 0x1113)) |
+                  set(range(0xAC00, 0xAC00 + 28 * 40)) | set(range(0x20, 0x7F)))
+    rng = random.Random(917)
+    nrand = 0
+    for _ in range(300000):
+        s = "".join(chr(rng.choice(pool)) for _ in range(rng.randint(1, 7)))
+        if nfkc.normalize_str(s) != hf_nfkc_model(s):
+            raise SystemExit("HF NFKC model differs on %r" % s)
+        nrand += 1
 
     # every ordered pair over the alphabet: HF NFKC == (space map, ccc_hf reorder, compose)
     npairs = 0
@@ -192,7 +301,8 @@ def main():
               | (int(c in comp_second or c in hangul_vt) << 22)
               | (int(c in comp_first or c in hangul_l or (0xAC00 <= c <= 0xD7A3 and (c - 0xAC00) % 28 == 0)) << 23)
               | (int(c in decomp or 0xAC00 <= c <= 0xD7A3) << 24) | (hf_ccc_zero[c] << 25)
-              | (int(c in allowed_set) << 26) | (int(c in lower_map) << 27))
+              | (int(c in allowed_set) << 26) | (int(c in lower_map) << 27)
+              | (int(c in hf_kd) << 28) | (int(c in hf_second) << 29))
         dl = len(decomp.get(c, []))
         di = dec_index.get(c, 0)
         w1 = norm_map[c] | (dl << 16) | (di << 19)
@@ -229,7 +339,7 @@ def main():
                 % (regex.__version__, unicodedata.unidata_version, tokenizers.__version__))
         f.write(" * Record word 0: gcb:4 incb:2 extpict:1 nfc_stable:1 ccc:8 script:3 hf_class:2\n")
         f.write(" *                hf_nfkc_space:1 comp_second:1 comp_first:1 has_decomp:1 hf_ccc_zero:1\n")
-        f.write(" *                allowed:1 lower_changes:1\n")
+        f.write(" *                allowed:1 lower_changes:1 hf_nfkd_changes:1 hf_comp_second:1\n")
         f.write(" * Record word 1: norm_map:16 decomp_len:3 decomp_idx:13\n */\n")
         f.write("#pragma once\n#include <stdint.h>\n\n")
         f.write("/* AK_UT_QUAL: storage qualifier (host: static const; HIP device: __device__ static const) */\n")
@@ -251,6 +361,23 @@ def main():
         # composition pairs: key = first<<21 | second (u64), value = composite
         arr("uint64_t", "AK_UT_COMP_KEY", ["%dULL" % ((a << 21) | b) for a, b in comp_keys], per=8)
         arr("uint32_t", "AK_UT_COMP_VAL", [pairs[k] for k in comp_keys])
+        # HF (Unicode 9) NFKD of every code point it changes (Hangul syllables excepted):
+        # sorted cps, offset << 5 | length into the flat array
+        kk = sorted(hf_kd)
+        kflat, koff = [], []
+        for c in kk:
+            koff.append((len(kflat) << 5) | len(hf_kd[c]))
+            kflat.extend(hf_kd[c])
+        assert max(len(v) for v in hf_kd.values()) < 32
+        f.write("#define AK_UT_NHFKD %d\n#define AK_UT_HFKD_MAXLEN %d\n\n" % (len(kk), max(len(v) for v in hf_kd.values())))
+        arr("uint32_t", "AK_UT_HFKD_KEY", kk)
+        arr("uint32_t", "AK_UT_HFKD_OFF", koff)
+        arr("uint32_t", "AK_UT_HFKD_FLAT", kflat)
+        # HF's primary composites (the UCD 13 pairs its NFC recomposes)
+        hk = sorted(hf_pairs)
+        f.write("#define AK_UT_NHFCOMP %d\n\n" % len(hk))
+        arr("uint64_t", "AK_UT_HFCOMP_KEY", ["%dULL" % ((a << 21) | b) for a, b in hk], per=8)
+        arr("uint32_t", "AK_UT_HFCOMP_VAL", [hf_pairs[k_] for k_ in hk])
         # lower map (semantic_normalize without the filter): sorted cps, 3 output slots (0 = none)
         lk = sorted(lower_map)
         f.write("#define AK_UT_NLOWER %d\n\n" % len(lk))
@@ -264,6 +391,8 @@ def main():
         "allowlist": len(allowed), "alphabet": len(alpha), "hf_word_chars": sum(1 for c in alpha if hf_class[c] == 0),
         "hf_space_chars": [hex(c) for c in alpha if hf_space[c]], "hf_pairs_checked": npairs,
         "hf_ccc_zero": [hex(c) for c in alpha if hf_ccc_zero[c]],
+        "hf_nfkd_cps": len(hf_kd), "hf_comp_pairs": len(hf_pairs), "hf_random_strings_checked": nrand,
+        "hf_marks_unknown": sum(hf_ccc_zero), "hf_word_chars_all": sum(1 for c in range(NCP) if hf_class[c] == 0),
         "alphabet_marks": {hex(c): ccc[c] for c in alpha if ccc[c]},
         "gcb_counts": {n: gcb.count(i) for i, n in enumerate(GCB_NAMES)},
         "incb_counts": {n: incb.count(i) for i, n in enumerate(INCB_NAMES)},
