@@ -40,6 +40,9 @@ SIGNATURES = {
     "ak_bpe_create": (I32, [U32, P, P, U32, P, U32, U32, ctypes.POINTER(P)]),
     "ak_bpe_free": (None, [P]),
     "ak_bpe_set_added": (I32, [P, U32, P, P, P]),
+    "ak_bpe_set_vocab": (I32, [P, U32, P, P, P]),
+    "ak_bpe_decode": (I32, [P, P, P, P, U64, P, U64, P, P]),
+    "ak_spm_decode": (I32, [P, P, P, P, U64, P, U64, P, P]),
     "ak_spm_create": (I32, [U32, P, P, P, P, ctypes.c_int32, P, ctypes.POINTER(P)]),
     "ak_spm_free": (None, [P]),
     "ak_normalize": (I32, [P, I32, P, P, U64, P, U64, P, P, P]),

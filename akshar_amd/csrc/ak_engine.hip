@@ -122,7 +122,31 @@ struct ak_bpe {
     bool tile_ok = false;  // every id < 0x7FFC (the tile kernel tags ids with bit 15, ak_tile.h WSTART) and
                            // new ids strictly increasing with rank (it compares merges by new id)
     uint32_t *d_added = nullptr;  // added tokens: code points, offsets, ids (one allocation)
+    DecTab dec{};                 // ak_bpe_set_vocab
+    uint8_t *d_dec = nullptr;     // text, offsets, kinds (one allocation)
 };
+
+// id -> text tables in one device allocation (DecTab)
+static int upload_dec(uint8_t *&mem, DecTab &t, const std::vector<uint8_t> &text, const std::vector<uint32_t> &off,
+                      const std::vector<uint8_t> &kind, const std::vector<uint8_t> &byteval) {
+    const size_t n = kind.size();
+    const size_t o_off = (text.size() + 3) & ~(size_t)3, o_kind = o_off + 4 * (n + 1), o_bv = o_kind + n;
+    std::vector<uint8_t> h(o_bv + n + 16, 0);
+    if (!text.empty()) memcpy(h.data(), text.data(), text.size());
+    memcpy(h.data() + o_off, off.data(), 4 * (n + 1));
+    if (n) memcpy(h.data() + o_kind, kind.data(), n);
+    if (n) memcpy(h.data() + o_bv, byteval.data(), n);
+    (void)hipFree(mem);
+    mem = nullptr;
+    HIP_TRY(hipMalloc(&mem, h.size()));
+    HIP_TRY(hipMemcpy(mem, h.data(), h.size(), hipMemcpyHostToDevice));
+    t.text = mem;
+    t.off = (const uint32_t *)(mem + o_off);
+    t.kind = mem + o_kind;
+    t.byteval = mem + o_bv;
+    t.n_ids = (uint32_t)n;
+    return AK_OK;
+}
 
 struct ak_spm {
     SpmDev dev;
@@ -132,6 +156,8 @@ struct ak_spm {
     uint32_t *d_code_cp = nullptr;
     int32_t *d_byte_ids = nullptr;
     uint32_t n_nodes = 0;
+    DecTab dec{};
+    uint8_t *d_dec = nullptr;
 };
 
 extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const uint32_t *single_id,
@@ -182,7 +208,19 @@ extern "C" void ak_bpe_free(ak_bpe *m) {
     (void)hipFree(m->d_single_cp);
     (void)hipFree(m->d_single_id);
     (void)hipFree(m->d_added);
+    (void)hipFree(m->d_dec);
     delete m;
+}
+
+extern "C" int ak_bpe_set_vocab(ak_bpe *m, uint32_t n, const uint8_t *tok_bytes, const uint64_t *tok_offs,
+                                const uint8_t *special) {
+    if (!m || !tok_offs || !special || (n && !tok_bytes)) return fail(AK_ERR_ARG, "ak_bpe_set_vocab: null argument");
+    if (tok_offs[n] >= 0xFFFFFFFFull) return fail(AK_ERR_UNSUPPORTED, "ak_bpe_set_vocab: vocabulary text over 4 GB");
+    std::vector<uint8_t> text(tok_bytes, tok_bytes + tok_offs[n]), kind(n), bv(n, 0);
+    std::vector<uint32_t> off(n + 1);
+    for (uint32_t i = 0; i <= n; ++i) off[i] = (uint32_t)(tok_offs[i] - tok_offs[0]);
+    for (uint32_t i = 0; i < n; ++i) kind[i] = special[i] ? DK_SKIP : DK_TEXT;
+    return upload_dec(m->d_dec, m->dec, text, off, kind, bv);
 }
 
 // normalize_text's allowlist (normalize.py:97-103): a char an added token needs that survives
@@ -258,6 +296,36 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.max_score = t.max_score;
     m->dev.abs_score_max = t.abs_score_max;
     m->dev.ws_code = t.ws_code;
+    {   // DecodeIds tables: pieces with U+2581 -> ' ', kinds, byte values of <0xXX>
+        std::vector<uint8_t> text, kind(n), bv(n, 0);
+        std::vector<uint32_t> off(n + 1, 0);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint8_t *p = piece_bytes + piece_offs[i];
+            const uint64_t len = piece_offs[i + 1] - piece_offs[i];
+            const uint8_t ty = types[i];
+            if (ty == 3) kind[i] = DK_SKIP;                           // CONTROL
+            else if (ty == 2) kind[i] = DK_UNK;                       // UNKNOWN
+            else if (ty == 6) {                                       // BYTE: "<0xXX>"
+                kind[i] = DK_BYTE;
+                unsigned v = 0;
+                for (uint64_t k = 3; k < 5 && k < len; ++k) {
+                    const char ch = (char)p[k];
+                    v = v * 16 + (unsigned)(ch <= '9' ? ch - '0' : (ch | 0x20) - 'a' + 10);
+                }
+                bv[i] = (uint8_t)v;
+            } else {
+                const bool ws = len >= 3 && p[0] == 0xE2 && p[1] == 0x96 && p[2] == 0x81;
+                kind[i] = ws ? DK_WS : DK_TEXT;
+                for (uint64_t k = 0; k < len;) {
+                    if (k + 3 <= len && p[k] == 0xE2 && p[k + 1] == 0x96 && p[k + 2] == 0x81) { text.push_back(0x20); k += 3; }
+                    else text.push_back(p[k++]);
+                }
+            }
+            off[i + 1] = (uint32_t)text.size();
+        }
+        const int rc = upload_dec(m->d_dec, m->dec, text, off, kind, bv);
+        if (rc) { ak_spm_free(m); return rc; }
+    }
     *out = m;
     return AK_OK;
 }
@@ -269,7 +337,28 @@ extern "C" void ak_spm_free(ak_spm *m) {
     (void)hipFree(m->d_cmap);
     (void)hipFree(m->d_code_cp);
     (void)hipFree(m->d_byte_ids);
+    (void)hipFree(m->d_dec);
     delete m;
+}
+
+static int check_common(ak_ws *w, const uint8_t *in, const uint64_t *offs, uint64_t n, const void *out,
+                        uint64_t *out_offs);
+
+extern "C" int ak_bpe_decode(const ak_bpe *m, ak_ws *w, const uint32_t *ids, const uint64_t *id_offs, uint64_t n,
+                             uint8_t *out, uint64_t cap, uint64_t *out_offs, void *stream) {
+    if (!m) return fail(AK_ERR_ARG, "ak_bpe_decode: null model");
+    if (!m->d_dec) return fail(AK_ERR_ARG, "ak_bpe_decode: no vocabulary (ak_bpe_set_vocab)");
+    int rc = check_common(w, (const uint8_t *)ids, id_offs, n, out, out_offs);
+    if (rc) return rc;
+    return launch_decode(false, w, m->dec, ids, id_offs, n, out, cap, out_offs, (hipStream_t)stream);
+}
+
+extern "C" int ak_spm_decode(const ak_spm *m, ak_ws *w, const uint32_t *ids, const uint64_t *id_offs, uint64_t n,
+                             uint8_t *out, uint64_t cap, uint64_t *out_offs, void *stream) {
+    if (!m) return fail(AK_ERR_ARG, "ak_spm_decode: null model");
+    int rc = check_common(w, (const uint8_t *)ids, id_offs, n, out, out_offs);
+    if (rc) return rc;
+    return launch_decode(true, w, m->dec, ids, id_offs, n, out, cap, out_offs, (hipStream_t)stream);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -293,6 +293,20 @@ struct RowsOutFinal {
 };
 int launch_rows_tiles(int ops, AkWs *w, const RowArgs &a, int matras, const RowsOutFinal &f, hipStream_t st);
 
+// id -> text tables of a model (ak_k_decode.hip): per id its output bytes and kind
+enum : uint8_t { DK_TEXT = 0, DK_SKIP = 1, DK_UNK = 2, DK_BYTE = 3, DK_WS = 4 };  // DK_WS: text starting with the U+2581 space
+struct DecTab {
+    const uint8_t *text;    // BPE: the token string; SPM: the piece with U+2581 -> ' '
+    const uint32_t *off;    // n_ids + 1 offsets into text
+    const uint8_t *kind;    // DK_*
+    const uint8_t *byteval; // DK_BYTE: the byte
+    uint32_t n_ids;
+};
+// decode rows of ids (id_offs[n + 1]) into UTF-8 text rows; SPM selects sentencepiece DecodeIds
+// semantics, else HF BPE decode (no decoder: tokens joined by ' ', special tokens skipped)
+int launch_decode(bool spm, AkWs *w, const DecTab &t, const uint32_t *ids, const uint64_t *id_offs, uint64_t n,
+                  uint8_t *out, uint64_t cap, uint64_t *out_offs, hipStream_t st);
+
 }  // namespace ak
 
 struct ak_ws : ak::AkWs {};

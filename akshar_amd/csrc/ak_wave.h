@@ -59,6 +59,11 @@ inline uint32_t w_exscan(uint32_t v, uint32_t *total) {
     *total = tot;
     return ex;
 }
+// inclusive prefix sum over lanes
+inline uint32_t w_inscan(uint32_t v) {
+    uint32_t tot;
+    return w_exscan(v, &tot) + v;
+}
 inline uint64_t w_atomic_load64(const uint64_t *p) {
     return reinterpret_cast<const std::atomic<uint64_t> *>(p)->load(std::memory_order_relaxed);
 }

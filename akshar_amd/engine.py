@@ -88,6 +88,43 @@ def _check_inputs(buf, offs):
     return n
 
 
+def _decode(fn, h, ids, id_offs):
+    if ids.dtype != torch.int32 or id_offs.dtype != torch.int64 or not (ids.is_cuda and id_offs.is_cuda):
+        raise TypeError("id rows must be int32 device ids with int64 device offsets")
+    ids, id_offs = ids.contiguous(), id_offs.contiguous()
+    n = id_offs.numel() - 1
+    if n < 0:
+        raise ValueError("id_offs must have n+1 entries")
+    if ids.numel() == 0:
+        ids = torch.zeros(1, dtype=torch.int32, device=ids.device)
+    dev = ids.device
+    ws = workspace(dev.index)
+    cap = 8 * (int(ids.numel()) + n) + 64
+
+    def call(out, c, oo):
+        check(fn(h, ws, _ptr(ids), _ptr(id_offs), n, _ptr(out), c, _ptr(oo), _stream(dev)), fn.__name__)
+
+    out, oo, total = _run(call, n, cap, lambda c: torch.empty(max(c, 1), dtype=torch.uint8, device=dev), dev, ws)
+    return out[:total], oo
+
+
+def decode_lists(model, rows, dev=None):
+    """list[list[int]] -> list[str] through model.decode_batch on the device."""
+    n = len(rows)
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum([len(r) for r in rows], out=offs[1:])
+    flat = np.fromiter((x for r in rows for x in r), dtype=np.int64, count=int(offs[-1]))
+    if (flat < 0).any() or (flat > 0xFFFFFFFF).any():
+        raise AksharError("token id out of range")
+    d = model.dev
+    gi = torch.from_numpy(flat.astype(np.uint32).view(np.int32).copy()).to(d)
+    go = torch.from_numpy(offs).to(d)
+    out, oo = model.decode_batch(gi, go)
+    b = out.cpu().numpy().tobytes()
+    o = oo.cpu().numpy()
+    return [b[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(n)]
+
+
 def _run(fn_call, n, cap, make_out, dev, ws, out=None, out_offs=None):
     """Run a capacity-bounded op, re-running once with the exact size if needed. Every row is exact
     at any length (include/akshar.h "Row lengths"); ak_ws_check turns an internal overflow into an
@@ -236,6 +273,19 @@ class BPE:
         cps, aoffs, aids = m.added_arrays()
         check(_lib.lib().ak_bpe_set_added(h, len(aids), cps.ctypes.data, aoffs.ctypes.data, aids.ctypes.data),
               "ak_bpe_set_added")
+        toks = [m.id_to_token.get(i, "").encode("utf-8", "surrogatepass") for i in range(m.vocab_size)]
+        tb = np.frombuffer(b"".join(toks) or b"\0", dtype=np.uint8)
+        to = np.zeros(len(toks) + 1, dtype=np.uint64)
+        np.cumsum([len(t) for t in toks], out=to[1:])
+        sp = np.asarray([1 if (i in m.special_ids or i not in m.id_to_token) else 0 for i in range(m.vocab_size)],
+                        dtype=np.uint8)
+        check(_lib.lib().ak_bpe_set_vocab(h, len(toks), tb.ctypes.data, to.ctypes.data, sp.ctypes.data),
+              "ak_bpe_set_vocab")
+
+    def decode_batch(self, ids, id_offs):
+        """Device id rows (int32, int64 offsets) -> (uint8 UTF-8 text, int64 row offsets):
+        HF Tokenizer.decode per row (tokenizer.py:219), on the device."""
+        return _decode(_lib.lib().ak_bpe_decode, self.h, ids, id_offs)
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -283,6 +333,11 @@ class SPM:
         h = getattr(self, "h", None)
         if h:
             _lib.lib().ak_spm_free(h)
+
+    def decode_batch(self, ids, id_offs):
+        """Device id rows (int32, int64 offsets) -> (uint8 UTF-8 text, int64 row offsets):
+        SentencePieceProcessor.DecodeIds per row (tokenizer.py:217), on the device."""
+        return _decode(_lib.lib().ak_spm_decode, self.h, ids, id_offs)
 
     def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, out=None, out_offs=None,
                      path=None):

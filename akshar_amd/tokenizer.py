@@ -108,11 +108,13 @@ class aksharTokenizer:
         return self.encode_batch([text])[0]
 
     def decode(self, ids: List[int]) -> str:
+        """tokenizer.py:195-219, on the device (ak_bpe_decode / ak_spm_decode)."""
+        return self.decode_batch([ids])[0]
+
+    def decode_batch(self, rows: List[List[int]]) -> List[str]:
         if self.model is None:
             raise ValueError("need model to decode")
-        if self.model_type == "sentencepiece":
-            return _dec.spm_decode(self.model.model, list(ids))
-        return _dec.bpe_decode(self.model.model, list(ids))
+        return engine.decode_lists(self.model, [list(r) for r in rows])
 
     # ---------------------------------------------------------------- tokens
     def _tokens_for(self, ids):

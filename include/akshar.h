@@ -181,6 +181,22 @@ int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
 #define AK_TILE_NPASS 10
 int ak_profile_tile_passes(ak_ws *ws, uint64_t *cycles, int n);
 
+/* Decode (tokenizer.py:195-219): rows of ids (u32, id_offs[n+1]) -> UTF-8 text
+ * rows (out, out_offs[n+1]; out_offs[n] = required total even when cap is short).
+ * ak_bpe_decode = HF Tokenizer.decode with the trained tokenizer.json (no decoder): special tokens
+ * and ids outside the vocabulary are skipped, the other token strings joined by ' '. It needs the
+ * vocabulary strings: ak_bpe_set_vocab (n ids, UTF-8 strings packed with tok_offs[n+1], special[n]
+ * = 1 for special tokens; host pointers).
+ * ak_spm_decode = SentencePieceProcessor.DecodeIds: control pieces vanish, <unk> -> " \u2047 ",
+ * U+2581 -> ' ', <0xXX> byte runs reassembled as UTF-8 (invalid bytes -> U+FFFD each), leading
+ * U+2581 dropped until the first non-empty piece; an id past the vocabulary is AK_ERR_ARG.
+ * Device pointers; one wave per row. */
+int ak_bpe_set_vocab(ak_bpe *m, uint32_t n, const uint8_t *tok_bytes, const uint64_t *tok_offs, const uint8_t *special);
+int ak_bpe_decode(const ak_bpe *m, ak_ws *ws, const uint32_t *ids, const uint64_t *id_offs, uint64_t n, uint8_t *out,
+                  uint64_t cap, uint64_t *out_offs, void *stream);
+int ak_spm_decode(const ak_spm *m, ak_ws *ws, const uint32_t *ids, const uint64_t *id_offs, uint64_t n, uint8_t *out,
+                  uint64_t cap, uint64_t *out_offs, void *stream);
+
 /* Always-sufficient output capacities (elements) for n rows of total_bytes input bytes.
  * ak_bpe_encode_cap holds for flags 2 / 3; with clean_hinglish=False (flags 0 / 1) NFKC can
  * expand a char (U+FDFA: 3 bytes -> 18 code points): AK_BPE_NFKC_EXPANSION * total_bytes + 2n + 16. */

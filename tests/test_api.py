@@ -10,6 +10,7 @@ import pytest
 import akshar_amd
 from akshar_amd import AksharTokenizer, Akshar, aksharTokenizer
 from akshar_amd import decode as dec
+from oracle import decode_ref
 from tests.conftest import BPE_PATH, SPM_PATH
 
 gpu = pytest.mark.gpu
@@ -51,10 +52,11 @@ def test_identify_script_reference_cases():
     assert ids("\t") == "other" and ids("€") == "other"
 
 
-def test_host_decoders_match_golden(golden, bpe_model, spm_model):
+def test_decoder_restatement_matches_golden(golden, bpe_model, spm_model):
+    """The oracle's CPU decoders (the device decode's checker) against the reference's outputs."""
     for r in golden:
-        assert dec.bpe_decode(bpe_model, r["bpe"]) == r["bpe_dec"]
-        assert dec.spm_decode(spm_model, r["spm"]) == r["spm_dec"]
+        assert decode_ref.bpe_decode(bpe_model, r["bpe"]) == r["bpe_dec"]
+        assert decode_ref.spm_decode(spm_model, r["spm"]) == r["spm_dec"]
 
 
 def test_model_tokens_match_golden(golden, bpe_model, spm_model):

@@ -329,3 +329,33 @@ def test_analyze_synthetic_and_empty(eng):
     assert torch.equal(ro, o3) and torch.equal(runs, e3) and torch.equal(labels, l3)
     z = eng.analyze_batch(*eng.pack([]))
     assert all(int(t.numel()) == 0 for t in (z[0], z[2], z[4])) and int(z[1][-1]) == 0
+
+
+def test_device_decode_golden(golden, eng, bpe_model, spm_model):
+    """f1: ids -> text on the device (ak_bpe_decode / ak_spm_decode) == the reference's decode
+    (tokenizer.py:195-219) on every golden row, in one batch per model."""
+    for key, model in (("bpe", eng.BPE(bpe_model)), ("spm", eng.SPM(spm_model))):
+        rows = [r[key] for r in golden]
+        got = eng.decode_lists(model, rows)
+        assert [i for i, r in enumerate(golden) if got[i] != r[key + "_dec"]] == [], key
+
+
+def test_device_decode_edge_cases(eng, bpe_model, spm_model):
+    """Byte-piece runs (valid, truncated, overlong, surrogate), unk, control pieces, leading
+    spaces, empty rows, specials / unknown ids for BPE: device == the oracle's restatement."""
+    from oracle import decode_ref
+    spm = eng.SPM(spm_model)
+    m = spm_model
+    bid = [int(x) for x in m.byte_ids]
+    ws = [i for i, p in enumerate(m.pieces) if p == "\u2581".encode()][0]
+    ctl = [i for i, t in enumerate(m.types) if t == 3]
+    rows = [[], [ws], [ws, ws], ctl + [ws, 500], [bid[0xE0], bid[0xA4], bid[0x95]], [bid[0xE0], bid[0x80], bid[0x80]],
+            [bid[0xED], bid[0xA0], bid[0x80]], [bid[0xF0], bid[0x9F]], [bid[0xC3]] + [500] + [bid[0xA9]],
+            [m.unk_id, ws, m.unk_id], [bid[0xFF], bid[0x41]] * 40, [500 + (i % 300) for i in range(300)]]
+    got = eng.decode_lists(spm, rows)
+    assert got == [decode_ref.spm_decode(m, r) for r in rows]
+    with pytest.raises(Exception):
+        eng.decode_lists(spm, [[len(m.pieces) + 5]])
+    bpe = eng.BPE(bpe_model)
+    brows = [[], [2, 3], [2, 100, 3, 200, 4], [10 ** 6, 100], [100 + i for i in range(200)]]
+    assert eng.decode_lists(bpe, brows) == [decode_ref.bpe_decode(bpe_model, r) for r in brows]
