@@ -20,6 +20,9 @@ _LAZY = {
     "analyze_text_composition": ("segment", "analyze_text_composition"),
     "identify_script": ("segment", "identify_script"),
     "is_matra": ("segment", "is_matra"),
+    "word_tokenize": ("segment", "word_tokenize"),
+    "word_tokenize_hindi": ("segment", "word_tokenize_hindi"),
+    "word_tokenize_sanskrit": ("segment", "word_tokenize_sanskrit"),
 }
 
 __all__ = sorted(_LAZY)

@@ -6,7 +6,10 @@ detect_code_switches :150-201 script runs; digits/punct neutral
 analyze_text_composition :210-236  counts + ratios (float division on the host, as the reference)
 identify_script / is_matra   per-character helpers (:26-37, :128-147), host-side: they classify
                               one character and are not on the batch path.
+word_tokenize*       :239-401 danda-aware word split of the device-normalized text
 """
+import re
+
 from . import engine
 
 MATRA_RANGES = [(0x0900, 0x0902), (0x093E, 0x094C), (0x0951, 0x0954)]  # segment.py:20-24
@@ -135,3 +138,46 @@ def analyze_text_composition(text):
 
 __all__ = ["segment_akshars", "detect_code_switches", "segment_by_script", "analyze_text_composition",
            "identify_script", "is_matra", "MATRA_RANGES", "segment_batch", "switches_batch"]
+
+
+# ------------------------------------------------------------------------------------------
+# word_tokenize* (segment.py:239-401): normalize_text on the device, then the reference's word
+# rule over the normalized text: whitespace and .,!?;:()[]{}"' end a word (and vanish), a danda /
+# double danda ends a word and is a token of its own. Morfessor morphology (morph.py) is out of
+# scope: use_morphology is accepted and, as in the reference without a trained
+# morph model, the basic split runs.
+_WORD_RE = re.compile(r"[।॥]|[^\s।॥.,!?;:()\[\]{}\"']+")
+
+
+def _words(normalized):
+    return _WORD_RE.findall(normalized)
+
+
+def word_tokenize_hindi_batch(texts, use_morphology=False):
+    from .normalize import normalize_batch
+    return [_words(n) for n in normalize_batch(texts)]
+
+
+def word_tokenize_hindi(text, use_morphology=False):
+    """segment.py:239-299."""
+    return word_tokenize_hindi_batch([text], use_morphology)[0]
+
+
+def word_tokenize_sanskrit(text, use_morphology=False):
+    """segment.py:302-363 (the same rule as Hindi in the reference)."""
+    return word_tokenize_hindi_batch([text], use_morphology)[0]
+
+
+def word_tokenize(text, language="auto", use_morphology=False):
+    """segment.py:366-401: 'auto' = Hindi when the raw text has a U+0900..U+097F char, else a plain
+    whitespace split of the raw text; unknown languages split on whitespace."""
+    if language == "auto":
+        if any(0x0900 <= ord(c) <= 0x097F for c in text):
+            language = "hindi"
+        else:
+            return [w for w in text.split() if w]
+    if language.lower() in ("hindi", "hi", "hin"):
+        return word_tokenize_hindi(text, use_morphology=use_morphology)
+    if language.lower() in ("sanskrit", "sa", "san", "skr"):
+        return word_tokenize_sanskrit(text, use_morphology=use_morphology)
+    return [w for w in text.split() if w]
