@@ -398,20 +398,41 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     // "previous" always means the previous KEPT element (shuffled from its lane or carried over).
     uint32_t wlen = 0;
     {
+        // Written branch-free where the lanes disagree: unconditional LDS loads at clamped indices,
+        // table lookups with the rare code points (outside the LDS tables) behind a ballot, and
+        // the compacting store aimed at a per-lane dummy slot (the staged bytes, dead after D) for
+        // lanes that emit nothing, so the common case issues no exec-mask juggling.
+        uint16_t *dummy = (uint16_t *)M.bytes;
+        const uint32_t h_sp = H[0x20];
         uint32_t carry_h = H_ROWSTART, carry_word = 0, carry_kword = 0xFFFFFFFFu, rs = 0;
         int carry_cls = HF_S;
+        const uint32_t vlast = vlen ? vlen - 1 : 0;
         for (uint32_t base = 0; base < vlen; base += 64) {
             const uint32_t kk = base + lane;
             const bool in = kk < vlen;
-            uint16_t x = in ? M.v[kk] : V_DEAD;
-            const uint16_t pa = in && kk >= 1 ? M.v[kk - 1] : V_DEAD;
-            const uint16_t pb = in && kk >= 2 ? M.v[kk - 2] : V_DEAD;
-            const uint16_t nx = in && kk + 1 < vlen ? M.v[kk + 1] : V_DEAD;
+            const uint32_t kc = in ? kk : vlast;
+            const uint16_t x0 = M.v[kc];
+            const uint16_t pa0 = M.v[kc >= 1 ? kc - 1 : 0];
+            const uint16_t pb0 = M.v[kc >= 2 ? kc - 2 : 0];
+            const uint16_t nx0 = M.v[kc + 1 < vlen ? kc + 1 : kc];
+            uint16_t x = in ? x0 : V_DEAD;
+            const uint16_t pa = in && kk >= 1 ? pa0 : V_DEAD;
+            const uint16_t pb = in && kk >= 2 ? pb0 : V_DEAD;
+            const uint16_t nx = in && kk + 1 < vlen ? nx0 : V_DEAD;
             const bool special = x >= V_SPECIAL;
             const bool drop = in && !special && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
             const bool keep = in && !drop;
-            uint32_t h = special ? H_ROWSTART : hot(H, x);
-            if (!special && (h & H_HFSPACE)) { x = 0x20; h = hot(H, 0x20); }
+            // hot word: LDS for U+0000..017F / U+0900..09FF, the global trie for the rest (rare)
+            const uint32_t xi = x < HOT_LO ? x : ((uint32_t)x - 0x900u < 0x100u ? (uint32_t)x - 0x900u + HOT_LO : 0u);
+            uint32_t h = H[xi];
+            const bool cold = !special && xi == 0u && x != 0;
+            if (w_ballot(cold)) {
+                if (cold) h = hot_of(prop_global(x));
+            }
+            h = special ? H_ROWSTART : h;
+            const bool hsp = !special && (h & H_HFSPACE);
+            x = hsp ? (uint16_t)0x20 : x;
+            h = hsp ? h_sp : h;
             const int cls = special ? HF_S : (int)((h >> H_CLS_SHIFT) & 3u);
             const uint64_t KM = w_ballot(keep);
             const uint64_t lt = w_lanemask_lt();  // N only: the nearest kept lane below
@@ -421,15 +442,23 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             const int cls_l = w_shfl(cls, src);
             const uint32_t hprev = pk ? h_l : carry_h;
             const int cprev = pk ? cls_l : carry_cls;
-            // HF-NFC quick check -> row fallback
+            // HF-NFC quick check -> row fallback (rare: behind a ballot)
             const uint64_t RM = w_ballot(keep && (x == V_B || x == V_FB));
             const bool trig = keep && !special && !(h & H_HFST) && nfc_trig<true>(h, hprev);
-            if (trig) M.fb[rs + w_rank_incl(RM) - 1] = 1;
+            if (w_ballot(trig)) {
+                if (trig) M.fb[rs + w_rank_incl(RM) - 1] = 1;
+            }
             // pre-tokenizer + ids
             const bool wordchar = keep && !special && cls != HF_S;
             const uint64_t SM = w_ballot(wordchar && cls != cprev);
             const uint32_t word = carry_word + w_rank_incl(SM);  // inclusive
-            const uint32_t id = wordchar ? single_id_of(m, sfast, a.single_fast, x) : 0xFFFFu;
+            const uint32_t si = sfast_index(x);
+            uint32_t id = sfast[si < SFAST_N ? si : 0u];
+            const bool rare = wordchar && si >= SFAST_N;
+            if (w_ballot(rare)) {
+                if (rare) id = single_id_of(m, sfast, a.single_fast, x);
+            }
+            id = wordchar ? id : 0xFFFFu;
             const bool kept = id != 0xFFFFu;
             const uint64_t K2 = w_ballot(kept);
             const uint64_t pk2 = K2 & lt;
@@ -438,7 +467,8 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             const bool kstart = kept && word != kprev;
             const bool out = kept || (keep && special);
             const uint64_t OM = w_ballot(out);
-            if (out) M.w[wlen + w_rank(OM)] = special ? x : (uint16_t)(id | (kstart ? WSTART : 0u));
+            uint16_t *dst = out ? &M.w[wlen + w_rank(OM)] : &dummy[lane];
+            *dst = special ? x : (uint16_t)(id | (kstart ? WSTART : 0u));
             wlen += (uint32_t)w_popc(OM);
             rs += (uint32_t)w_popc(RM);
             if (KM) {
