@@ -16,14 +16,11 @@
 namespace ak {
 
 constexpr int SPM_TILE_BLOCK = 256;           // 4 waves per block
-#ifndef AK_SPM_WPE
-#define AK_SPM_WPE 4  // waves per SIMD the register budget must allow (the LDS allows 4)
-#endif
 constexpr uint32_t SPM_T_MUL = 2, SPM_T_ADD = 2;  // staging slot of row r: 2 offs[r] + 2 r
 constexpr int SPM_FB_BLOCK = 64;
 
 template <int FLAGS>
-__global__ __launch_bounds__(SPM_TILE_BLOCK, AK_SPM_WPE) void k_spm_tiles(TileArgs ta) {
+__global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
     __shared__ int4 root[SPM_ROOT_CAP];

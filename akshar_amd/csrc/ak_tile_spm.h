@@ -149,97 +149,6 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const in
     }
 }
 
-// The same lattice, pull order: for each end node e of the word, the candidates arrive from their
-// starts s = e-1-j in ascending s (j = SPM_WIN-1 .. 0), exactly the order in which word_dp's push
-// loop delivers them to e, and s = e-1 adds the unk candidate when it has no one-char piece. The
-// trie walks of the SPM_WIN most recent starts advance together, one char per step, so each step
-// issues its (independent) trie loads at once: one L2 round trip per char instead of one per
-// (start, depth). Window slot j holds the walk from s = e-1-j (node, child base) and best[s], the
-// best score of the current node stays in a register. Returns false if a walk outlives the window
-// (a piece of more than SPM_WIN chars might continue): the caller redoes the word with word_dp.
-constexpr int SPM_WIN = 8;
-
-template <bool MARGIN>
-__device__ __forceinline__ bool word_dp_win(SpmWaveMem &M, const SpmDev &m, const int4 *root, int p0, int p1,
-                                            float base, float &minm) {
-    int nodev[SPM_WIN], nbv[SPM_WIN];
-    float tl[SPM_WIN];
-#pragma unroll
-    for (int j = 0; j < SPM_WIN; ++j) { nodev[j] = -1; nbv[j] = 0; tl[j] = 0.0f; }
-    float prev = base;  // best[e-1]
-    bool ok = true;
-    for (int e = p0 + 1; e <= p1; ++e) {
-        if (nodev[SPM_WIN - 1] >= 0) ok = false;  // that walk would need slot SPM_WIN now
-#pragma unroll
-        for (int j = SPM_WIN - 1; j >= 1; --j) { nodev[j] = nodev[j - 1]; nbv[j] = nbv[j - 1]; tl[j] = tl[j - 1]; }
-        tl[0] = prev;
-        const uint32_t v = M.w[e - 1];
-        const bool coded = (v & W_CODED) != 0;
-        const int code = (int)(v & 0x7FFFu);
-        int4 ent[SPM_WIN];
-        int tix[SPM_WIN];
-        // slot 0: a new walk from s = e-1 (root child: LDS cache for small codes)
-        if (coded && code < (int)SPM_ROOT_CAP) {
-            ent[0] = root[code];
-            tix[0] = ent[0].x;
-            ent[0].x = ent[0].x >= 0 ? 0 : -1;  // root children check against node 0
-        } else if (coded) {
-            tix[0] = m.root_base + code;
-            ent[0] = m.trie[tix[0]];
-        } else {
-            tix[0] = -1;
-            ent[0] = make_int4(-1, 0, -1, 0);
-        }
-        nodev[0] = 0;
-#pragma unroll
-        for (int j = 1; j < SPM_WIN; ++j) {
-            tix[j] = nbv[j] + code;
-            ent[j] = (coded && nodev[j] >= 0) ? m.trie[tix[j]] : make_int4(-1, 0, -1, 0);
-        }
-        bool has = false;
-        float bst = 0.0f;
-        uint32_t bk = BK_NONE;
-        bool has_single = false;
-#pragma unroll
-        for (int j = SPM_WIN - 1; j >= 0; --j) {
-            const bool alive = coded && nodev[j] >= 0 && tix[j] >= 0 && ent[j].x == nodev[j];
-            nodev[j] = alive ? tix[j] : -1;
-            nbv[j] = ent[j].y;
-            const int value = ent[j].z;
-            if (!alive || value < 0) continue;
-            const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
-            if (kind == 2) continue;
-            const int id = value & 0xFFFFFF;
-            const double score = kind == 1 ? (double)((float)ent[j].w * m.max_score) - 0.1 : (double)__int_as_float(ent[j].w);
-            const double cand = score + (double)tl[j];
-            if (!has || cand > (double)bst) {
-                if (MARGIN && has) minm = fminf(minm, (float)(cand - (double)bst));
-                bst = (float)cand;
-                bk = ((uint32_t)id << 8) | (uint32_t)(j + 1);
-                has = true;
-            } else if (MARGIN) {
-                minm = fminf(minm, (float)((double)bst - cand));
-            }
-            if (j == 0) has_single = true;
-        }
-        if (!has_single) {
-            const float cand = m.unk_score + tl[0];
-            if (!has || cand > bst) {
-                if (MARGIN && has) minm = fminf(minm, cand - bst);
-                bst = cand;
-                bk = ((uint32_t)m.unk_id << 8) | 1u;
-                has = true;
-            } else if (MARGIN) {
-                minm = fminf(minm, bst - cand);
-            }
-        }
-        M.best[e] = bst;
-        M.back[e] = bk;
-        prev = bst;
-    }
-    return ok;
-}
-
 // backtrack a solved word into forward links nxt[s] = chars of the piece at s; returns its id
 // count (byte fallback: one id per UTF-8 byte of an unk char)
 __device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &m, uint8_t *nxt, int p0, int p1) {
@@ -338,12 +247,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const int p0 = act ? (int)starts[j] : 0;
         const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
         float minm = 3.0e38f;
-        const bool won = word_dp_win<true>(M, m, root, p0, p1, 0.0f, minm);
-        if (w_ballot(act && !won)) {  // a walk outlived the window: this word's lattice the push way
-            float mm = 3.0e38f;
-            word_dp<true>(M, m, root, p0, won ? p0 : p1, 0.0f, mm);
-            if (!won) minm = mm;
-        }
+        word_dp<true>(M, m, root, p0, p1, 0.0f, minm);
         if (act) {
             // rounding bound of this word (header comment): M = (chars from the row start to the word
             // end + 1) x the largest |score|
@@ -366,7 +270,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     const int p0 = (int)starts[j];
                     const int p1 = j + 1 < j1 ? (int)starts[j + 1] : (int)M.rowpos[lane + 1] - 1;
                     float unused = 0.0f;
-                    if (!word_dp_win<false>(M, m, root, p0, p1, base, unused)) word_dp<false>(M, m, root, p0, p1, base, unused);
+                    word_dp<false>(M, m, root, p0, p1, base, unused);
                     wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
                     base = M.best[p1];
                 }
