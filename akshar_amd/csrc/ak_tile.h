@@ -324,43 +324,54 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
     // normalize_text map (lower / allowlist) -> V with <s>/</s> sentinels around each row. If no
     // char of a row trips nfc_trig, NFC is the identity on it; a row that trips is marked for the
     // fallback kernels.
+    // Branch-light like pass N: clamped unconditional loads, the rare code points (outside the LDS
+    // hot table) behind a ballot, and the compacting stores aimed at per-lane dummy slots past P's
+    // end in W for the lanes that write nothing.
+    static_assert(sizeof(M.w) / 2 - 64 >= (size_t)(BCAP + T_MAXR + 1), "D2 dummy slots overlap P");
+    uint16_t *dummy = M.w + (sizeof(M.w) / 2 - 64) + lane;
     uint32_t vpos = 0;
     {
         uint32_t carry_h = H_ROWSTART, rows = 0;
+        const uint32_t plast = np ? np - 1 : 0;
         for (uint32_t c0 = 0; c0 < np; c0 += 64) {
             const uint32_t c = c0 + lane;
             const bool in = c < np;
-            const uint32_t ent = in ? P[c] : 0x8000u;
+            const uint32_t ent0 = P[in ? c : plast];
+            const uint32_t nent0 = P[c + 1 < np ? c + 1 : plast];
+            const uint32_t ent = in ? ent0 : 0x8000u;
             const bool mark = in && (ent & 0x8000u);
             const uint64_t RMK = w_ballot(mark);
             const int row = (int)(rows + w_rank_incl(RMK)) - 1;
             const bool chr = in && !mark;
-            uint32_t h = H_ROWSTART;
-            bool bad = false;
-            if (chr) {
-                const int pos = (int)(ent & 0x7FFFu);
-                const int rend = (int)M.rowend[row];
-                const uint32_t cp = decode_word(lds_word(M.bytes, pos), pos, rend);
-                // the next lead (or the row end) must sit right after this char: else stray bytes
-                const uint32_t nent = c + 1 < np ? P[c + 1] : 0x8000u;
-                const int nxt = (nent & 0x8000u) ? rend : (int)nent;
-                if (cp == 0xFFFFFFFFu || pos + utf8_len(cp) != nxt) { bad = true; h = 0; }
-                else h = hot(H, cp);
+            const int pos = (int)(ent & 0x7FFFu);
+            const int rend = (int)M.rowend[row > 0 ? row : 0];
+            const uint32_t cp = decode_word(lds_word(M.bytes, pos), pos, rend);
+            // the next lead (or the row end) must sit right after this char: else stray bytes
+            const uint32_t nent = c + 1 < np ? nent0 : 0x8000u;
+            const int nxt = (nent & 0x8000u) ? rend : (int)nent;
+            const bool bad = chr && (cp == 0xFFFFFFFFu || pos + utf8_len(cp) != nxt);
+            const uint32_t ci = cp < HOT_LO ? cp : (cp - 0x900u < 0x100u ? cp - 0x900u + HOT_LO : 0u);
+            uint32_t hw = H[ci];
+            const bool cold = chr && !bad && ci == 0u && cp != 0u;
+            if (w_ballot(cold)) {
+                if (cold) hw = hot_of(prop_global(cp));
             }
+            const uint32_t h = chr ? (bad ? 0u : hw) : H_ROWSTART;
             const uint32_t hl = w_shfl(h, lane ? lane - 1 : 0);
             const uint32_t hprev = lane ? hl : carry_h;
             const bool trig = chr && (bad || (!(h & H_STABLE) && nfc_trig<false>(h, hprev)));
-            if (trig) M.fb[row] = 1;
+            if (w_ballot(trig)) {
+                if (trig) M.fb[row] = 1;
+            }
             const uint32_t mv = chr ? (h & 0xFFFFu) : 0u;
-            const uint32_t cnt = mark ? (row > 0 ? 2u : 1u) : (mv ? 1u : 0u);
+            const bool two = mark && row > 0;
+            const uint32_t cnt = mark ? (two ? 2u : 1u) : (mv ? 1u : 0u);
             uint32_t tot;
             const uint32_t ex = w_exscan(cnt, &tot);
-            if (mark) {
-                if (row > 0) { M.v[vpos + ex] = V_E; M.v[vpos + ex + 1] = V_B; }
-                else M.v[vpos + ex] = V_B;
-            } else if (mv) {
-                M.v[vpos + ex] = (uint16_t)mv;
-            }
+            uint16_t *d0 = cnt ? &M.v[vpos + ex] : dummy;
+            uint16_t *d1 = two ? &M.v[vpos + ex + 1] : dummy;
+            *d0 = mark ? (two ? V_E : V_B) : (uint16_t)mv;
+            *d1 = V_B;
             vpos += tot;
             rows += (uint32_t)w_popc(RMK);
             carry_h = w_bcast(h, 63);

@@ -15,10 +15,18 @@ def em(bpe_model):
     return emu.Model(bpe=bpe_model)
 
 
+def emu_sample(golden):
+    """The golden rows the emulator runs (64 host threads per wave primitive: minutes per 1 k rows):
+    every hand-built, corpus and alphabet row, every 3rd synthetic row. The GPU tests run them all."""
+    keep = {"corpus", "adversarial", "alphabet", "long"}
+    return [r for i, r in enumerate(golden) if r["set"] in keep or i % 3 == 0]
+
+
 def test_golden(golden, em):
-    packed = O.pack([r["text"] for r in golden])
+    rows = emu_sample(golden)
+    packed = O.pack([r["text"] for r in rows])
     ids, oo, st = emu.bpe_tiles(em, *packed, rows=8)
-    bad = [(r["set"], r["text"]) for r, g in zip(golden, rows_ints(ids, oo)) if g != r["bpe"]]
+    bad = [(r["set"], r["text"]) for r, g in zip(rows, rows_ints(ids, oo)) if g != r["bpe"]]
     assert bad == []
     assert not st.any()
 
@@ -49,7 +57,7 @@ def test_fallback_rows_match_oracle(em, bpe_model, rows):
 @pytest.mark.parametrize("kind", [0, 1, 2])
 def test_synthetic_vs_oracle(em, bpe_model, kind):
     from akshar_amd import synth
-    buf, offs = synth.generate(kind, 1500, seed=300 + kind)
+    buf, offs = synth.generate(kind, 600, seed=300 + kind)
     ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
