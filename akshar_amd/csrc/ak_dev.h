@@ -513,9 +513,10 @@ struct SwitchSink {
 
 struct BpeDev {
     const uint64_t *merge_tab;  // two-choice cuckoo: lo32 = left << 16 | right, hi32 = rank << 16 | new
-    const uint32_t *merge_ctab; // the same slots, 4-byte entries (ak_model_build.h build_bpe; tile path)
+    const uint32_t *merge_ctab; // tile path: compact two-choice table (ak_model_build.h build_bpe)
     uint32_t tab_mask;
     uint32_t tab_shift;
+    uint32_t ctab_shift;
     const uint32_t *single_sorted_cp;  // for code points >= FAST_N
     const uint16_t *single_sorted_id;
     uint32_t n_single;
@@ -542,17 +543,23 @@ __device__ __forceinline__ uint32_t merge_lookup(const BpeDev &m, uint32_t a, ui
 }
 
 // the same lookup on the compact table: the new id (= rank order for tile_ok models), 0xFFFF if none.
-// One 4-byte load per candidate slot: half the registers in flight and half the L2 footprint.
+// One 4-byte load at the first-choice slot answers almost every lookup (load <= 1/4); the second
+// slot is read only when the first misses and carries the overflow flag (ak_model_build.h).
 __device__ __forceinline__ uint32_t merge_lookup_c(const BpeDev &m, uint32_t a, uint32_t b) {
     const uint32_t key = (a << 16) | b;
-    const uint32_t p1 = key * 0x9E3779B1u, p2 = (key ^ 0x5BD1E995u) * 0x85EBCA77u;
-    const uint32_t lowmask = (1u << m.tab_shift) - 1u;
+    const uint32_t lowmask = (1u << m.ctab_shift) - 1u;
     // 32-bit byte offsets (the table is < 4 GB): saddr + voffset loads, one VGPR per address
     const char *base = (const char *)m.merge_ctab;
-    const uint32_t e1 = *(const uint32_t *)(base + ((p1 >> m.tab_shift) << 2));
-    const uint32_t e2 = *(const uint32_t *)(base + ((p2 >> m.tab_shift) << 2));
-    const uint32_t t1 = (p1 & lowmask) << 16, t2 = ((p2 & lowmask) << 16) | 0x8000u;
-    const uint32_t v = (e1 ^ t1) < 0x8000u ? (e1 & 0x7FFFu) : (e2 ^ t2) < 0x8000u ? (e2 & 0x7FFFu) : 0x7FFFu;
+    const uint32_t p1 = key * 0x9E3779B1u;
+    const uint32_t e1 = *(const uint32_t *)(base + ((p1 >> m.ctab_shift) << 2));
+    uint32_t v = 0x7FFFu;
+    if (((e1 ^ ((p1 & lowmask) << 17)) & 0xFFFE8000u) == 0u) {
+        v = e1 & 0x7FFFu;
+    } else if (e1 & 0x10000u) {
+        const uint32_t p2 = (key ^ 0x5BD1E995u) * 0x85EBCA77u;
+        const uint32_t e2 = *(const uint32_t *)(base + ((p2 >> m.ctab_shift) << 2));
+        if (((e2 ^ (((p2 & lowmask) << 17) | 0x8000u)) & 0xFFFE8000u) == 0u) v = e2 & 0x7FFFu;
+    }
     return v == 0x7FFFu ? 0xFFFFu : v;
 }
 

@@ -190,6 +190,7 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     m->dev.merge_ctab = m->d_ctab;
     m->dev.tab_mask = t.mask;
     m->dev.tab_shift = t.shift;
+    m->dev.ctab_shift = t.cshift;
     m->dev.single_sorted_cp = m->d_single_cp;
     m->dev.single_sorted_id = m->d_single_id;
     m->dev.n_single = t.n_rest;
@@ -427,6 +428,7 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->tile_misc);
     (void)hipFree(w->tile_passprof);
     (void)hipFree(w->fb2);
+    (void)hipFree(w->unit_fb);
     (void)hipFree(w->counts);
     (void)hipFree(w->slow_list);
     (void)hipFree(w->huge_list);

@@ -46,7 +46,8 @@ struct AkWs {
     void *huge_mem = nullptr;       // huge-tier pool, grown on demand
     uint64_t huge_bytes = 0;
     // tile-cooperative BPE path
-    uint32_t *stage = nullptr;      // staged ids, slot of row r at offs[r] + 2 r
+    uint32_t *stage = nullptr;      // staged ids, slot of row r at offs[r] + 2 r (tile BPE: unit runs +
+                                    // a second half for the fallback rows' slots)
     uint64_t cap_stage = 0;
     uint8_t *stage8 = nullptr;      // staged run labels (switches), same slots as stage
     uint64_t cap_stage8 = 0;
@@ -55,6 +56,8 @@ struct AkWs {
     uint32_t *tile_misc = nullptr;  // [0] fallback-list length, [1] slot-overflow flag, [2] second list length
     uint32_t *fb2 = nullptr;        // second fallback list (rows past the fast buffers)
     uint64_t cap_fb2 = 0;
+    uint64_t *unit_fb = nullptr;    // tile BPE: per 64-row unit, the mask of its fallback rows
+    uint64_t cap_unit_fb = 0;
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)

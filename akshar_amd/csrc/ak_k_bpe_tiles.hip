@@ -6,7 +6,8 @@
 //   k_rows_tier      ... to the slow tier (per-thread pool regions) and, past those, the huge
 //                    tier sized from the longest such row (ak_internal.h)
 //   scan_counts      per-row counts -> u64 row offsets (out_offs)
-//   k_tile_copy      staged ids -> ids[out_offs[r] ...]
+//   k_unit_copy      staged unit runs (+ fallback slots) -> ids[out_offs[r] ...]
+//   k_tile_copy      per-row slots -> ids (the staged row ops and SPM)
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -107,6 +108,61 @@ __global__ __launch_bounds__(256) void k_tile_copy(const T *__restrict__ stage, 
     }
 }
 
+// tile BPE: staged unit runs -> final positions. One wave per 64-row unit. A unit without
+// fallback rows is one contiguous run in the stage (its rows' ids back to back from offs[u0] + 2 u0)
+// and one contiguous range of the output: a streaming copy, UC_B dword loads per lane in flight
+// before the stores. A unit with fallback rows (its unit_fb mask) copies row by row: non-fallback
+// rows from their place in the run (exclusive scan of their counts), fallback rows from their slot
+// offs[r] + 2 r in the second staging half.
+constexpr int UC_B = 4;
+__global__ __launch_bounds__(256) void k_unit_copy(const uint32_t *__restrict__ stage, const uint32_t *__restrict__ stage_fb,
+                                                   const uint64_t *__restrict__ offs, const uint64_t *__restrict__ out_offs,
+                                                   const uint64_t *__restrict__ unit_fb, uint64_t n,
+                                                   uint32_t *__restrict__ ids, uint64_t cap, uint64_t half) {
+    const int lane = w_lane();
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
+    for (uint64_t u = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < nunits; u += nwaves) {
+        const uint64_t u0 = u * TILE_UNIT;
+        const int nr = (int)(u0 + TILE_UNIT < n ? TILE_UNIT : n - u0);
+        const uint64_t fbm = unit_fb[u];
+        const uint64_t base = offs[u0] + 2 * u0;
+        const uint64_t o0 = out_offs[u0], o1 = out_offs[u0 + (uint64_t)nr];
+        if (fbm == 0) {
+            const uint64_t len = o1 - o0;
+            for (uint64_t k0 = 0; k0 < len; k0 += 64 * UC_B) {
+                uint32_t v[UC_B];
+#pragma unroll
+                for (int q = 0; q < UC_B; ++q) {
+                    const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+                    v[q] = k < len && base + k < half ? stage[base + k] : 0u;
+                }
+#pragma unroll
+                for (int q = 0; q < UC_B; ++q) {
+                    const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+                    if (k < len && o0 + k < cap) ids[o0 + k] = v[q];
+                }
+            }
+            continue;
+        }
+        // rare: a unit with fallback rows
+        const uint64_t r = u0 + (uint64_t)lane;
+        const bool in = lane < nr;
+        const uint64_t ro = in ? out_offs[r] : 0ull;
+        const uint64_t c = in ? out_offs[r + 1] - ro : 0ull;
+        const bool fb = in && ((fbm >> lane) & 1ull);
+        uint32_t tot;
+        const uint64_t p = w_exscan(fb ? 0u : (uint32_t)c, &tot);
+        const uint64_t src = fb ? offs[r] + 2 * r : base + p;
+        for (int j = 0; j < nr; ++j) {
+            const uint64_t cj = w_bcast(c, j), sj = w_bcast(src, j), dj = w_bcast(ro, j);
+            const uint32_t *from = ((fbm >> j) & 1ull) ? stage_fb : stage;
+            for (uint64_t k = (uint64_t)lane; k < cj; k += 64)
+                if (dj + k < cap && sj + k < half) ids[dj + k] = from[sj + k];
+        }
+    }
+}
+
 // wave-primitive self-test (ak_selftest): DPP scan, readlane broadcast, ballot on known patterns
 __global__ __launch_bounds__(64) void k_selftest(uint32_t *out) {
     const int lane = w_lane();
@@ -161,10 +217,19 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     uint64_t nbytes = 0;
     HIP_TRY(hipMemcpyAsync(&nbytes, a0.offs + a0.n, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    rc = ws_stage_reserve(w, nbytes + 2 * a0.n + 64, st);
+    // two halves: the tile kernel's unit runs, then the fallback rows' slots
+    const uint64_t half = nbytes + 2 * a0.n + 64;
+    rc = ws_stage_reserve(w, 2 * half, st);
     if (rc) return rc;
     const int R = w->tile_rows;
     const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the static wave stride
+    if (w->cap_unit_fb < ntiles) {
+        (void)hipFree(w->unit_fb);
+        w->unit_fb = nullptr;
+        w->cap_unit_fb = 0;
+        HIP_TRY(hipMalloc(&w->unit_fb, ntiles * 8));
+        w->cap_unit_fb = ntiles;
+    }
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
@@ -182,7 +247,8 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     memset(&ta, 0, sizeof(ta));
     ta.ra = a0;
     ta.ra.out = w->stage;
-    ta.ra.cap = w->cap_stage;
+    ta.ra.cap = half;
+    ta.unit_fb = w->unit_fb;
     ta.ra.out_offs = nullptr;
     ta.counts = w->counts;
     ta.fb_list = w->slow_list;              // n entries (ws_reserve)
@@ -215,8 +281,11 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     // fallback rows: the full row pipeline (exact NFC, HF-NFC, any UTF-8) into the same slots, then
     // the slow and huge tiers for rows past its buffers
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    k_tile_fb<3><<<(unsigned)num_cus(), FB_BLOCK, 0, st>>>(ta);
-    RowArgs ra = ta.ra;
+    TileArgs tfb = ta;
+    tfb.ra.out = w->stage + half;
+    tfb.ra.cap = half;
+    k_tile_fb<3><<<(unsigned)num_cus(), FB_BLOCK, 0, st>>>(tfb);
+    RowArgs ra = tfb.ra;
     ra.counts = w->counts;
     ra.err = w->ctr + CTR_ERR;
     k_rows_tier<OP_BPE, 3><<<SLOW_THREADS / 64, 64, 0, st>>>(ra, BPE_MUL, BPE_ADD, slow_tier(w, w->fb2, ta.fb2_count));
@@ -230,7 +299,14 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     rc = scan_counts(w, a0.n, out_offs, st);
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
-    return launch_stage_copy(w, a0.offs, out_offs, a0.n, (uint32_t *)a0.out, a0.cap, 1, 2, st);
+    const uint64_t nunits = ntiles;
+    const unsigned cgrid = (unsigned)std::min<uint64_t>((nunits + 3) / 4, (uint64_t)num_cus() * 8);
+    AK_PROF(AK_PROF_COPY, false, st);
+    k_unit_copy<<<cgrid, 256, 0, st>>>(w->stage, w->stage + half, a0.offs, out_offs, w->unit_fb, a0.n,
+                                       (uint32_t *)a0.out, a0.cap, half);
+    AK_PROF(AK_PROF_COPY, true, st);
+    HIP_TRY(hipGetLastError());
+    return AK_OK;
 }
 
 int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st) {

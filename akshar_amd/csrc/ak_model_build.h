@@ -26,7 +26,8 @@ inline uint32_t cuckoo_h2(uint32_t key, uint32_t shift) { return ((key ^ 0x5BD1E
 
 struct BpeTables {
     std::vector<uint64_t> tab;
-    std::vector<uint32_t> ctab;  // the same slots, 4-byte entries (tile path; see build_compact)
+    std::vector<uint32_t> ctab;  // tile path: its own two-choice table, 4-byte entries (below)
+    uint32_t cshift = 0;         // ... slot = product >> cshift
     uint32_t mask = 0;
     uint32_t shift = 0;  // slot = (key * 0x9E3779B1) >> shift: the product's HIGH bits
     std::vector<uint16_t> fast;     // FAST_N entries, 0xFFFF = not in vocab
@@ -72,20 +73,59 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
         size <<= 1;  // a cycle: grow and rebuild (never needed at load <= 0.5 in practice)
         if (size > (1u << 24)) return "cuckoo table build failed";
     }
-    // compact entries for the tile path: slot = product >> shift, so (slot, product's low `shift`
-    // bits, which hash) identifies the key exactly (both products are bijections of the key):
-    // entry = low bits << 16 | which << 15 | new id (< 0x7FFC); 0x00007FFF = empty (reads as "no
-    // merge" whatever it matches). The tile path compares new ids as ranks (monotone, checked at load).
-    t.ctab.assign(size, 0x00007FFFu);
-    for (uint32_t h = 0; h < size; ++h) {
-        const uint32_t key = (uint32_t)t.tab[h];
-        if (key == 0xFFFFFFFFu) continue;
-        const uint32_t nw = (uint32_t)(t.tab[h] >> 32) & 0xFFFFu;
-        if (nw >= 0x7FFFu) continue;  // such a model is not tile_ok: the entry is never read
-        const bool first = cuckoo_h1(key, t.shift) == h;
-        const uint32_t prod = first ? key * 0x9E3779B1u : (key ^ 0x5BD1E995u) * 0x85EBCA77u;
-        const uint32_t low = prod & ((1u << t.shift) - 1u);
-        t.ctab[h] = (low << 16) | (first ? 0u : 0x8000u) | nw;
+    // The tile path's compact table: its own two-choice cuckoo at load <= 1/4 (>= 2^17 slots), so
+    // almost every key sits in its first-choice slot and one 4-byte load answers almost every
+    // lookup. slot = product >> cshift, and (slot, the product's low cshift bits, which hash)
+    // identifies the key exactly (both products are bijections of the key). Entry:
+    //   bits 0-14 new id (< 0x7FFC; 0x7FFF none), bit 15 which (0: stored at h1, 1: at h2),
+    //   bit 16 "some key whose FIRST choice is this slot is stored at its second choice",
+    //   bits 17-31 the low product bits (cshift <= 15).
+    // Empty = 0x0000FFFF (which = 1: it never matches a first-choice probe; a second-choice probe
+    // that lands on it reads "no merge"). A lookup probes h2 only when h1 misses and carries the
+    // flag, so an absent pair costs one load unless its h1 slot is flagged. The tile path compares
+    // new ids as ranks (monotone, checked at load).
+    {
+        uint32_t csize = 1u << 17;
+        while (csize < 4u * n_merges) csize <<= 1;
+        for (;;) {
+            uint32_t cs = 32;
+            for (uint32_t q = csize; q > 1; q >>= 1) --cs;
+            std::vector<uint64_t> ct(csize, 0xFFFFFFFFull);  // {key, new id} during the build
+            bool ok = true;
+            for (uint32_t r = 0; r < n_merges && ok; ++r) {
+                const uint32_t key = (merges[3 * r] << 16) | merges[3 * r + 1];
+                const uint32_t a = cuckoo_h1(key, cs), b = cuckoo_h2(key, cs);
+                if ((uint32_t)ct[a] == key || (uint32_t)ct[b] == key) continue;  // the lowest rank wins
+                uint64_t e = (uint64_t)key | ((uint64_t)merges[3 * r + 2] << 32);
+                uint32_t h = a;
+                int kicks = 0;
+                for (;;) {
+                    std::swap(e, ct[h]);
+                    if ((uint32_t)e == 0xFFFFFFFFu) break;
+                    const uint32_t k2 = (uint32_t)e;
+                    h = cuckoo_h1(k2, cs) == h ? cuckoo_h2(k2, cs) : cuckoo_h1(k2, cs);
+                    if (++kicks > 4096) { ok = false; break; }
+                }
+            }
+            if (!ok) {
+                csize <<= 1;
+                if (csize > (1u << 24)) return "compact cuckoo table build failed";
+                continue;
+            }
+            t.ctab.assign(csize, 0x0000FFFFu);
+            t.cshift = cs;
+            for (uint32_t h = 0; h < csize; ++h) {
+                const uint32_t key = (uint32_t)ct[h];
+                if (key == 0xFFFFFFFFu) continue;
+                const uint32_t nw = (uint32_t)(ct[h] >> 32) & 0xFFFFu;
+                const bool first = cuckoo_h1(key, cs) == h;
+                const uint32_t prod = first ? key * 0x9E3779B1u : (key ^ 0x5BD1E995u) * 0x85EBCA77u;
+                const uint32_t low = prod & ((1u << cs) - 1u);
+                t.ctab[h] = (t.ctab[h] & 0x10000u) | (low << 17) | (first ? 0u : 0x8000u) | (nw < 0x7FFFu ? nw : 0x7FFFu);
+                if (!first) t.ctab[cuckoo_h1(key, cs)] |= 0x10000u;
+            }
+            break;
+        }
     }
     t.fast.assign(FAST_N, 0xFFFFu);
     std::vector<std::pair<uint32_t, uint16_t>> rest;

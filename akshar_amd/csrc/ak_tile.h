@@ -9,16 +9,18 @@
 //   P  Whitespace pre-tokenizer + single-char ids, compacted in place; pre-token starts -> V
 //   B  lane per pre-token: merge_all (lowest rank, leftmost on ties), in registers up to WREG-1
 //      symbols, in LDS beyond
-//   F  ids (B -> <s>, E -> </s>) into each row's staging slot, per-row token counts
+//   F  ids (B -> <s>, E -> </s>) into the unit's staging run, per-row token counts
 // Only the common case runs here (rows past the 768-byte tile buffer start the next sub-tile). A row
 // whose NFC / HF-NFC quick check trips, with invalid UTF-8, or alone over the tile buffer is
-// appended to a fallback list and encoded by the row kernels of
-// ak_k_bpe_tiles.hip (ak_rows.h process_row), which write into the same per-row slot: the tile
-// kernel has no calls, no private arrays and no scratch.
-// Row r's slot is stage[offs[r] + 2 r ...] (its ids never exceed its bytes + 2), so rows and tiles
-// never wait on each other; the launcher scans the counts into row offsets and a copy kernel
-// moves the ids to their final place. No look-back, no ticket: on MI355X every inter-tile hop
-// would be a cross-XCD L2 round trip.
+// appended to a fallback list and encoded by the row kernels of ak_k_bpe_tiles.hip (ak_rows.h
+// process_row): the tile kernel has no calls and no private arrays.
+// The wave encodes the tiles of a 64-row unit in order, so the ids of the unit's rows go back to
+// back into the unit's staging run, which starts at stage[offs[u0] + 2 u0] (row r's ids never
+// exceed its bytes + 2, so the run never leaves the unit's region); fallback rows write their own
+// slot offs[r] + 2 r of a second staging area, and the unit's fallback-row mask tells the copy
+// kernel which rows those are. Units never wait on each other; the launcher scans the counts into
+// row offsets and one streaming copy per unit moves the ids to their final place. No look-back,
+// no ticket: on MI355X every inter-unit hop would be a cross-XCD L2 round trip.
 // Reference semantics: normalize.py:117-148, tokenizer.py:167-193, cli.py:276-299.
 #pragma once
 #include "ak_dev.h"
@@ -53,6 +55,8 @@ struct TileWaveMem {
     uint32_t rowslot[T_MAXR];    // row's staging slot, relative to the tile's (S0 + 2 r0)
     uint32_t rowop[T_MAXR + 1];  // row's first position in the tile's id stream
     uint64_t passacc[10];        // PassClock accumulators (ak_profile_tile_passes)
+    uint64_t unext;              // BPE: the unit's staging run: next free position (stage index)
+    uint64_t ufbm;               // BPE: the unit's rows (bit r - u0) sent to the fallback kernels
 };
 
 struct TileArgs {
@@ -63,6 +67,7 @@ struct TileArgs {
     uint32_t *fb2_list;   // rows the fallback fast kernel could not finish (pool kernel)
     uint32_t *fb2_count;
     uint32_t *err;        // set if an id fell outside its row's slot (never: bytes + 2 bound)
+    uint64_t *unit_fb;    // BPE: per 64-row unit, the mask of its rows sent to the fallback kernels
     uint64_t *passprof;   // optional: device cycles per pass, summed over waves (T_NPASS entries)
     uint64_t ntiles;
     int rows;             // R
@@ -199,6 +204,18 @@ __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
 #else
     typedef unsigned short us2 __attribute__((ext_vector_type(2)));
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
+#endif
+}
+
+// per-half a * b + c of packed u16 pairs (v_pk_mad_u16)
+__device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef AK_HOST_EMU
+    const uint32_t lo = ((a & 0xFFFFu) * (b & 0xFFFFu) + (c & 0xFFFFu)) & 0xFFFFu;
+    const uint32_t hi = ((a >> 16) * (b >> 16) + (c >> 16)) & 0xFFFFu;
+    return lo | (hi << 16);
+#else
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(us2, a) * __builtin_bit_cast(us2, b) + __builtin_bit_cast(us2, c));
 #endif
 }
 
@@ -395,7 +412,6 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     pc.mark(TP_STAGE);
     const TileRows tr = tile_front<T_BCAP>(a, r0, rend, H, M, 1u, 2u);
     const int nr = tr.nr;
-    const uint64_t S0 = tr.S0;
     const uint32_t vlen = tr.vlen;
 
     pc.mark(TP_D);
@@ -546,33 +562,43 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                 d[k] = lo | (hi << 16);
             }
             w_sync();  // every lane has read V and its window before rank rows overwrite bytes / V
-            if (reg) {
+            {  // every lane writes its rank row (all 0xFFFF unless reg): the merge rounds read it unmasked
                 uint4 *r4 = (uint4 *)rk16;
                 r4[0] = make_uint4(d[0], d[1], d[2], d[3]);
                 r4[1] = make_uint4(d[4], d[5], d[6], d[7]);
-                M.w[st] = (uint16_t)(sy[0] & 0x7FFFu);
             }
+            if (reg) M.w[st] = (uint16_t)(sy[0] & 0x7FFFu);
             uint32_t alive = reg ? (1u << n) - 1u : 0u;
             for (;;) {
                 uint32_t e[WREG / 2];
-                if (reg) {
+                {
                     const uint4 *r4 = (const uint4 *)rk16;
                     const uint4 x0 = r4[0], x1 = r4[1];
                     e[0] = x0.x; e[1] = x0.y; e[2] = x0.z; e[3] = x0.w; e[4] = x1.x; e[5] = x1.y; e[6] = x1.z; e[7] = x1.w;
-                } else {
-#pragma unroll
-                    for (int k = 0; k < WREG / 2; ++k) e[k] = 0xFFFFFFFFu;
                 }
-                uint32_t mv = e[0];
-#pragma unroll
-                for (int k = 1; k < WREG / 2; ++k) mv = pk_min_u16(mv, e[k]);
+                // packed-u16 min as a tree (no dependent VOP3P chain)
+                const uint32_t m01 = pk_min_u16(e[0], e[1]), m23 = pk_min_u16(e[2], e[3]);
+                const uint32_t m45 = pk_min_u16(e[4], e[5]), m67 = pk_min_u16(e[6], e[7]);
+                const uint32_t mv = pk_min_u16(pk_min_u16(m01, m23), pk_min_u16(m45, m67));
                 const uint32_t minv = (mv & 0xFFFFu) < (mv >> 16) ? (mv & 0xFFFFu) : (mv >> 16);
                 const bool mg = minv != 0xFFFFu;
                 if (!w_ballot(mg)) break;
                 if (mg) {
-                    int bi = 0;
+                    // leftmost position of minv, in packed u16 arithmetic (no per-position
+                    // compare-to-mask / select): key = (value != minv) * 16 + position, min over all
+                    const uint32_t mm = minv * 0x10001u;
+                    uint32_t one = 0x00010001u;  // opaque: else the compiler folds min(x, 1) * 16 back into selects
+#ifndef AK_HOST_EMU
+                    asm volatile("" : "+v"(one));
+#endif
+                    uint32_t kk[WREG / 2];
 #pragma unroll
-                    for (int i = WREG - 2; i >= 0; --i) bi = ((e[i >> 1] >> ((i & 1) * 16)) & 0xFFFFu) == minv ? i : bi;
+                    for (int k = 0; k < WREG / 2; ++k)
+                        kk[k] = pk_mad_u16(pk_min_u16(e[k] ^ mm, one), 0x00100010u, (uint32_t)(2 * k) | ((uint32_t)(2 * k + 1) << 16));
+                    const uint32_t k01 = pk_min_u16(kk[0], kk[1]), k23 = pk_min_u16(kk[2], kk[3]);
+                    const uint32_t k45 = pk_min_u16(kk[4], kk[5]), k67 = pk_min_u16(kk[6], kk[7]);
+                    const uint32_t kmin = pk_min_u16(pk_min_u16(k01, k23), pk_min_u16(k45, k67));
+                    const int bi = (int)(((kmin & 0xFFFFu) < (kmin >> 16) ? kmin : (kmin >> 16)) & 15u);
                     const uint32_t after = alive >> (bi + 1);
                     const int jn = bi + 1 + __builtin_ctz(after);  // the right symbol of the pair
                     const uint32_t below = alive & ((1u << bi) - 1u);
@@ -604,6 +630,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     {
         const bool isfb = lane < nr && M.fb[lane];
         const uint64_t FM = w_ballot(isfb);
+        if (lane == 0) M.ufbm |= FM << (r0 % TILE_UNIT);  // tiles never straddle a unit
         if (FM) {
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(ta.fb_count, (uint32_t)w_popc(FM));
@@ -613,8 +640,9 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     }
 
     pc.mark(TP_FBC);
-    // ---------------- pass F: ids -> each row's staging slot; row start positions
-    const uint64_t sbase = S0 + 2 * r0;
+    // ---------------- pass F: ids -> the unit's staging run (back to back after the unit's earlier
+    // tiles); row start positions -> per-row counts
+    const uint64_t sbase = M.unext;
     uint32_t *stage = (uint32_t *)a.out + sbase;
     const uint64_t scap = a.cap > sbase ? a.cap - sbase : 0;
     uint32_t pos = 0;
@@ -633,7 +661,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         if (isrow) M.rowop[rs + w_rank(RM)] = op;
         w_sync();
         if (emit) {
-            const uint64_t d = (uint64_t)M.rowslot[row] + (op - M.rowop[row]);
+            const uint64_t d = op;
             const uint32_t val = x == V_B ? m.bos : x == V_E ? m.eos : (uint32_t)(x & 0x7FFFu);
             if (d < scap) stage[d] = val;
             else over = true;
@@ -642,6 +670,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         rs += (uint32_t)w_popc(RM);
     }
     if (lane == 0) M.rowop[rs] = pos;
+    if (lane == 0) M.unext = sbase + pos;
     if (w_ballot(over) && lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     w_sync();
     if (lane < nr && !M.fb[lane]) {
@@ -664,7 +693,14 @@ __device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;
-        for (uint64_t r = r0; r < r1;) r += (uint64_t)bpe_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, sfast, M, pc);
+        if (w_lane() == 0) {  // the unit's staging run starts at its rows' slot base offs[r0] + 2 r0
+            M.unext = ta.ra.offs[r0] + 2 * r0;
+            M.ufbm = 0;
+        }
+        w_sync();
+        for (uint64_t r = r0; r < r1;)
+            r += (uint64_t)bpe_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, sfast, M, pc);
+        if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
     }
     pc.flush(ta.passprof);
 }

@@ -38,6 +38,7 @@ extern "C" void *emu_bpe_create(uint32_t n_single, const uint32_t *cp, const uin
     m->bdev.merge_ctab = m->bpe.ctab.data();
     m->bdev.tab_mask = m->bpe.mask;
     m->bdev.tab_shift = m->bpe.shift;
+    m->bdev.ctab_shift = m->bpe.cshift;
     m->bdev.single_sorted_cp = m->bpe.rest_cp.data();
     m->bdev.single_sorted_id = m->bpe.rest_id.data();
     m->bdev.n_single = m->bpe.n_rest;
@@ -175,11 +176,15 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
     for (uint32_t i = 0; i < HOT_N; ++i) hot_tab[i] = hot_of(prop_global(hot_cp(i)));
     if (n == 0) { out_offs[0] = 0; return 0; }
-    std::vector<uint32_t> stage(offs[n] + 2 * n + 64), counts(n), fbl(n), fb2(n);
+    const uint64_t half = offs[n] + 2 * n + 64;
+    const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
+    std::vector<uint32_t> stage(2 * half), counts(n), fbl(n), fb2(n);
+    std::vector<uint64_t> unit_fb(nunits);
     uint32_t fbn = 0, fb2n = 0, err = 0;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
-    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = stage.size();
+    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = half;
+    ta.unit_fb = unit_fb.data();
     ta.ra.row_status = row_status; ta.ra.bpe = m->bdev; ta.ra.single_fast = m->bpe.fast.data();
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
     ta.fb2_count = &fb2n; ta.err = &err;
@@ -216,16 +221,27 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
         sc.heap = heap.data(); sc.link = link.data();
         sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
         sc.slow_status = ST_LIMIT; sc.status = 0;
-        const uint64_t cnt = process_row<OP_BPE, 3, true>(ta.ra, r, fast, m->bpe.fast.data(), &sc, offs[r] + 2 * r);
+        RowArgs fa = ta.ra;  // fallback rows: their own slot in the second staging half
+        fa.out = stage.data() + half;
+        const uint64_t cnt = process_row<OP_BPE, 3, true>(fa, r, fast, m->bpe.fast.data(), &sc, offs[r] + 2 * r);
         const bool lim = (sc.status & ST_LIMIT) != 0;
         counts[r] = lim ? 0 : (uint32_t)cnt;
         if (row_status) row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0));
     }
-    // scan + per-row copy, as the launcher's scan_counts and k_tile_copy
+    // scan + copy, as the launcher's scan_counts and k_unit_copy: each unit's non-fallback rows
+    // back to back from its run base offs[u0] + 2 u0, fallback rows from their slot in the second half
     out_offs[0] = 0;
     for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
-    for (uint64_t r = 0; r < n; ++r)
-        for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = stage[offs[r] + 2 * r + i];
+    for (uint64_t u = 0; u < nunits; ++u) {
+        const uint64_t u0 = u * TILE_UNIT;
+        uint64_t p = offs[u0] + 2 * u0;
+        for (uint64_t r = u0; r < n && r < u0 + TILE_UNIT; ++r) {
+            const bool fb = (unit_fb[u] >> (r - u0)) & 1ull;
+            const uint32_t *src = fb ? stage.data() + half + offs[r] + 2 * r : stage.data() + p;
+            for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = src[i];
+            if (!fb) p += counts[r];
+        }
+    }
     return (int64_t)out_offs[n];
 }
 
