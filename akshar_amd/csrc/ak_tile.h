@@ -168,28 +168,36 @@ __device__ __forceinline__ bool nfc_trig(uint32_t m, uint32_t p) {
            ((p & H_DECOMP) && (p & H_STABLE) && cm < (p >> H_CCC_SHIFT));
 }
 
-// bytes p .. p+3 of an LDS byte array as one little-endian word (two aligned dword reads)
+// bytes p .. p+3 of an LDS byte array as one little-endian word (two aligned dword reads and one
+// funnel shift: v_alignbit takes the shift mod 32, so an aligned p needs no branch)
 __device__ __forceinline__ uint32_t lds_word(const uint8_t *B, int p) {
     const uint32_t *w = (const uint32_t *)(B + (p & ~3));
     const uint32_t lo = w[0], hi = w[1];
     const uint32_t sh = (uint32_t)(p & 3) * 8u;
+#ifdef AK_HOST_EMU
     return sh ? (lo >> sh) | (hi << (32u - sh)) : lo;
+#else
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#endif
 }
 
 // branch-free UTF-8 decode of the char starting at p (< e) from its 4-byte window x; same
-// acceptance as lds_decode (0xFFFFFFFF = invalid)
+// acceptance as lds_decode (0xFFFFFFFF = invalid). Arithmetic only: the sequence length from the
+// lead's leading ones, the payload as if 4 bytes long then shifted down, and the checks folded
+// into one predicate (lanes of a Hinglish tile mix ASCII and Devanagari, so any branch here runs
+// both ways).
 __device__ __forceinline__ uint32_t decode_word(uint32_t x, int p, int e) {
-    const uint32_t b0 = x & 0xFFu, b1 = (x >> 8) & 0xFFu, b2 = (x >> 16) & 0xFFu, b3 = x >> 24;
-    if (b0 < 0x80u) return b0;
-    const int l = b0 >= 0xF0u ? 4 : b0 >= 0xE0u ? 3 : b0 >= 0xC0u ? 2 : 0;
-    const bool c1 = (b1 & 0xC0u) == 0x80u, c2 = (b2 & 0xC0u) == 0x80u, c3 = (b3 & 0xC0u) == 0x80u;
-    const uint32_t cp2 = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
-    const uint32_t cp3 = ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu);
-    const uint32_t cp4 = ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
-    const uint32_t cp = l == 2 ? cp2 : l == 3 ? cp3 : cp4;
-    const bool conts = l == 2 ? c1 : l == 3 ? (c1 && c2) : (c1 && c2 && c3);
-    const uint32_t mn = l == 2 ? 0x80u : l == 3 ? 0x800u : 0x10000u;
-    const bool ok = l != 0 && b0 <= 0xF4u && p + l <= e && conts && cp >= mn && cp <= 0x10FFFFu;
+    const uint32_t b0 = x & 0xFFu;
+    const uint32_t l = (uint32_t)__builtin_clz(~(b0 << 24));  // 0 ASCII, 1 stray continuation, 2..8 lead
+    const uint32_t n = l > 1u ? l : 1u;                        // bytes of the sequence
+    const uint32_t y = __builtin_bswap32(x);                   // lead byte on top
+    const uint32_t full = (((y >> 24) & (0x7Fu >> l)) << 18) | (((y >> 16) & 0x3Fu) << 12) |
+                          (((y >> 8) & 0x3Fu) << 6) | (y & 0x3Fu);
+    const uint32_t cp = full >> ((24u - 6u * n) & 31u);
+    // bytes 1 .. n-1 must be continuation bytes (10xxxxxx)
+    const uint32_t cm = ((y & 0x00C0C0C0u) ^ 0x00808080u) >> ((32u - 8u * n) & 31u);
+    const uint32_t mn = (1u << ((0x100B0700u >> (8u * (n - 1u) & 31u)) & 0xFFu)) & ~1u;  // 0, 0x80, 0x800, 0x10000
+    const bool ok = l != 1u && b0 <= 0xF4u && p + (int)n <= e && (n == 1u || cm == 0u) && cp >= mn && cp <= 0x10FFFFu;
     return ok ? cp : 0xFFFFFFFFu;
 }
 
