@@ -79,6 +79,11 @@ template <class T>
 int copy_staged(const T *stage, uint64_t stage_cap, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, T *out,
                 uint64_t cap, uint32_t mul, uint32_t add, hipStream_t st);
 int num_cus();
+// unit-run staging (tile BPE, row tiles): per-unit fallback masks, and the streaming unit copy
+int ws_unit_fb_reserve(AkWs *w, uint64_t nunits);
+template <class T>
+int copy_units(const T *stage, const T *stage_fb, uint64_t half, const uint64_t *offs, const uint64_t *out_offs,
+               const uint64_t *unit_fb, uint64_t n, T *out, uint64_t cap, uint32_t mul, uint32_t add, hipStream_t st);
 
 __device__ __forceinline__ void stage_tables(uint2 *fast, uint16_t *sfast, const uint16_t *g_single, bool bpe) {
     for (uint32_t i = threadIdx.x; i < FAST_N; i += blockDim.x) {

@@ -108,17 +108,75 @@ __global__ __launch_bounds__(256) void k_tile_copy(const T *__restrict__ stage, 
     }
 }
 
-// tile BPE: staged unit runs -> final positions. One wave per 64-row unit. A unit without
-// fallback rows is one contiguous run in the stage (its rows' ids back to back from offs[u0] + 2 u0)
-// and one contiguous range of the output: a streaming copy, UC_B dword loads per lane in flight
-// before the stores. A unit with fallback rows (its unit_fb mask) copies row by row: non-fallback
-// rows from their place in the run (exclusive scan of their counts), fallback rows from their slot
-// offs[r] + 2 r in the second staging half.
+// Staged unit runs -> final positions (tile BPE and the row tiles). One wave per 64-row unit. A
+// unit without fallback rows is one contiguous run in the stage (its rows' outputs back to back
+// from mul * offs[u0] + add * u0) and one contiguous range of the output: a streaming copy, UC_B
+// loads per lane in flight before the stores (u8: dwords funnel-shifted from two aligned loads,
+// bytes only at the two ends, so no dword straddles another unit's output). A unit with fallback
+// rows (its unit_fb mask) copies row by row: non-fallback rows from their place in the run
+// (exclusive scan of their counts), fallback rows from their slot mul * offs[r] + add * r in the
+// second staging half.
 constexpr int UC_B = 4;
-__global__ __launch_bounds__(256) void k_unit_copy(const uint32_t *__restrict__ stage, const uint32_t *__restrict__ stage_fb,
+
+template <class T>
+__device__ __forceinline__ void copy_run(const T *__restrict__ src, uint64_t src_cap, T *__restrict__ dst,
+                                         uint64_t dst_cap, uint64_t s0, uint64_t d0, uint64_t len, int lane) {
+    if constexpr (sizeof(T) == 4) {
+        for (uint64_t k0 = 0; k0 < len; k0 += 64 * UC_B) {
+            T v[UC_B];
+#pragma unroll
+            for (int q = 0; q < UC_B; ++q) {
+                const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+                v[q] = k < len && s0 + k < src_cap ? src[s0 + k] : (T)0;
+            }
+#pragma unroll
+            for (int q = 0; q < UC_B; ++q) {
+                const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+                if (k < len && d0 + k < dst_cap) dst[d0 + k] = v[q];
+            }
+        }
+    } else {
+        const uint64_t d1 = d0 + len;
+        const uint64_t a = (d0 + 3) & ~3ull, b = d1 & ~3ull;  // whole dwords of the output: [a, b)
+        if (a >= b) {  // short: bytes
+            for (uint64_t k = (uint64_t)lane; k < len; k += 64)
+                if (d0 + k < dst_cap && s0 + k < src_cap) dst[d0 + k] = src[s0 + k];
+            return;
+        }
+        const uint64_t head = a - d0, tail = d1 - b;
+        if ((uint64_t)lane < head && d0 + lane < dst_cap && s0 + lane < src_cap) dst[d0 + lane] = src[s0 + lane];
+        if ((uint64_t)lane < tail && b + lane < dst_cap && s0 + (b - d0) + lane < src_cap)
+            dst[b + lane] = src[s0 + (b - d0) + lane];
+        const uint32_t *s32 = (const uint32_t *)src;
+        uint32_t *d32 = (uint32_t *)dst;
+        const uint64_t nw = (b - a) / 4;
+        const uint64_t sa = s0 + head;                 // source byte of output byte a
+        const uint32_t sh = (uint32_t)(sa & 3) * 8u;
+        const uint64_t sw = sa >> 2;                   // its dword
+        const uint64_t src_words = src_cap / 4;        // whole dwords readable (the stage is padded)
+        for (uint64_t k0 = 0; k0 < nw; k0 += 64 * UC_B) {
+            uint32_t v[UC_B];
+#pragma unroll
+            for (int q = 0; q < UC_B; ++q) {
+                const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+                const uint32_t lo = k < nw && sw + k < src_words ? s32[sw + k] : 0u;
+                const uint32_t hi = k < nw && sw + k + 1 < src_words ? s32[sw + k + 1] : 0u;
+                v[q] = __builtin_amdgcn_alignbit(hi, lo, sh);
+            }
+#pragma unroll
+            for (int q = 0; q < UC_B; ++q) {
+                const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+                if (k < nw && a + 4 * k + 4 <= dst_cap) d32[a / 4 + k] = v[q];
+            }
+        }
+    }
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_unit_copy(const T *__restrict__ stage, const T *__restrict__ stage_fb,
                                                    const uint64_t *__restrict__ offs, const uint64_t *__restrict__ out_offs,
-                                                   const uint64_t *__restrict__ unit_fb, uint64_t n,
-                                                   uint32_t *__restrict__ ids, uint64_t cap, uint64_t half) {
+                                                   const uint64_t *__restrict__ unit_fb, uint64_t n, T *__restrict__ out,
+                                                   uint64_t cap, uint64_t half, uint32_t mul, uint32_t add) {
     const int lane = w_lane();
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
@@ -126,23 +184,10 @@ __global__ __launch_bounds__(256) void k_unit_copy(const uint32_t *__restrict__ 
         const uint64_t u0 = u * TILE_UNIT;
         const int nr = (int)(u0 + TILE_UNIT < n ? TILE_UNIT : n - u0);
         const uint64_t fbm = unit_fb[u];
-        const uint64_t base = offs[u0] + 2 * u0;
+        const uint64_t base = (uint64_t)mul * offs[u0] + (uint64_t)add * u0;
         const uint64_t o0 = out_offs[u0], o1 = out_offs[u0 + (uint64_t)nr];
         if (fbm == 0) {
-            const uint64_t len = o1 - o0;
-            for (uint64_t k0 = 0; k0 < len; k0 += 64 * UC_B) {
-                uint32_t v[UC_B];
-#pragma unroll
-                for (int q = 0; q < UC_B; ++q) {
-                    const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
-                    v[q] = k < len && base + k < half ? stage[base + k] : 0u;
-                }
-#pragma unroll
-                for (int q = 0; q < UC_B; ++q) {
-                    const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
-                    if (k < len && o0 + k < cap) ids[o0 + k] = v[q];
-                }
-            }
+            copy_run<T>(stage, half, out, cap, base, o0, o1 - o0, lane);
             continue;
         }
         // rare: a unit with fallback rows
@@ -153,14 +198,38 @@ __global__ __launch_bounds__(256) void k_unit_copy(const uint32_t *__restrict__ 
         const bool fb = in && ((fbm >> lane) & 1ull);
         uint32_t tot;
         const uint64_t p = w_exscan(fb ? 0u : (uint32_t)c, &tot);
-        const uint64_t src = fb ? offs[r] + 2 * r : base + p;
+        const uint64_t src = fb ? (uint64_t)mul * offs[r] + (uint64_t)add * r : base + p;
         for (int j = 0; j < nr; ++j) {
             const uint64_t cj = w_bcast(c, j), sj = w_bcast(src, j), dj = w_bcast(ro, j);
-            const uint32_t *from = ((fbm >> j) & 1ull) ? stage_fb : stage;
+            const T *from = ((fbm >> j) & 1ull) ? stage_fb : stage;
             for (uint64_t k = (uint64_t)lane; k < cj; k += 64)
-                if (dj + k < cap && sj + k < half) ids[dj + k] = from[sj + k];
+                if (dj + k < cap && sj + k < half) out[dj + k] = from[sj + k];
         }
     }
+}
+
+template <class T>
+int copy_units(const T *stage, const T *stage_fb, uint64_t half, const uint64_t *offs, const uint64_t *out_offs,
+               const uint64_t *unit_fb, uint64_t n, T *out, uint64_t cap, uint32_t mul, uint32_t add, hipStream_t st) {
+    const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
+    const unsigned cgrid = (unsigned)std::min<uint64_t>((nunits + 3) / 4, (uint64_t)num_cus() * 8);
+    k_unit_copy<T><<<cgrid, 256, 0, st>>>(stage, stage_fb, offs, out_offs, unit_fb, n, out, cap, half, mul, add);
+    HIP_TRY(hipGetLastError());
+    return AK_OK;
+}
+template int copy_units<uint8_t>(const uint8_t *, const uint8_t *, uint64_t, const uint64_t *, const uint64_t *,
+                                 const uint64_t *, uint64_t, uint8_t *, uint64_t, uint32_t, uint32_t, hipStream_t);
+template int copy_units<uint32_t>(const uint32_t *, const uint32_t *, uint64_t, const uint64_t *, const uint64_t *,
+                                  const uint64_t *, uint64_t, uint32_t *, uint64_t, uint32_t, uint32_t, hipStream_t);
+
+int ws_unit_fb_reserve(AkWs *w, uint64_t nunits) {
+    if (w->cap_unit_fb >= nunits) return AK_OK;
+    (void)hipFree(w->unit_fb);
+    w->unit_fb = nullptr;
+    w->cap_unit_fb = 0;
+    HIP_TRY(hipMalloc(&w->unit_fb, nunits * 8));
+    w->cap_unit_fb = nunits;
+    return AK_OK;
 }
 
 // wave-primitive self-test (ak_selftest): DPP scan, readlane broadcast, ballot on known patterns
@@ -223,13 +292,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     if (rc) return rc;
     const int R = w->tile_rows;
     const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the static wave stride
-    if (w->cap_unit_fb < ntiles) {
-        (void)hipFree(w->unit_fb);
-        w->unit_fb = nullptr;
-        w->cap_unit_fb = 0;
-        HIP_TRY(hipMalloc(&w->unit_fb, ntiles * 8));
-        w->cap_unit_fb = ntiles;
-    }
+    if ((rc = ws_unit_fb_reserve(w, ntiles))) return rc;
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
@@ -299,14 +362,11 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     rc = scan_counts(w, a0.n, out_offs, st);
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
-    const uint64_t nunits = ntiles;
-    const unsigned cgrid = (unsigned)std::min<uint64_t>((nunits + 3) / 4, (uint64_t)num_cus() * 8);
     AK_PROF(AK_PROF_COPY, false, st);
-    k_unit_copy<<<cgrid, 256, 0, st>>>(w->stage, w->stage + half, a0.offs, out_offs, w->unit_fb, a0.n,
-                                       (uint32_t *)a0.out, a0.cap, half);
+    rc = copy_units<uint32_t>(w->stage, w->stage + half, half, a0.offs, out_offs, w->unit_fb, a0.n,
+                              (uint32_t *)a0.out, a0.cap, 1, 2, st);
     AK_PROF(AK_PROF_COPY, true, st);
-    HIP_TRY(hipGetLastError());
-    return AK_OK;
+    return rc;
 }
 
 int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st) {

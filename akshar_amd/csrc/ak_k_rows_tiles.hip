@@ -1,11 +1,11 @@
 // ak_k_rows_tiles.hip — tile-cooperative normalize / segment / switches / fused analyze for the
 // normalize_text defaults (ak_tile_rows.h), and their launcher:
-//   k_rows_tiles<OPS>     every wave processes whole tiles of rows into per-row staging slots and
+//   k_rows_tiles<OPS>     every wave processes whole tiles of rows into its units' staging runs and
 //                         writes per-row counts; rare rows go to a fallback list
 //   k_rows_tile_fb<OPS>   fallback rows, one lane per row (the sequential row pipeline of ak_dev.h)
-//                         into the same slots; rows past its buffers go on
+//                         into their own slots of the second staging half; rows past its buffers go on
 //   k_rows_tile_tier<OPS> ... to the slow and huge tiers
-//   scan_counts, k_tile_copy   counts -> offsets, staged outputs -> the packed outputs
+//   scan_counts, k_unit_copy   counts -> offsets, staged unit runs -> the packed outputs
 #include <stdlib.h>
 
 #include "ak_internal.h"
@@ -85,7 +85,8 @@ __global__ __launch_bounds__(64) void k_rows_tile_tier(RowArgs a, RowsOut o, Tie
 static int g_rt_bpc[8] = {};
 
 template <int OPS>
-static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsOutFinal &f, hipStream_t st) {
+static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsOut &ofb, const RowsOutFinal &f,
+                      hipStream_t st) {
     int rc;
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
@@ -107,6 +108,7 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
         w->cap_fb2 = a0.n;
     }
     const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;
+    if ((rc = ws_unit_fb_reserve(w, ntiles))) return rc;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra = a0;
@@ -119,6 +121,7 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     ta.fb2_count = w->tile_misc + 2;
     ta.passprof = g_prof_on ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
+    ta.unit_fb = w->unit_fb;
     ta.rows = std::min(w->tile_rows, T_MAXR);
     HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
     HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
@@ -130,13 +133,13 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     AK_PROF(AK_PROF_ROW_TILES, true, st);
     HIP_TRY(hipGetLastError());
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    k_rows_tile_fb<OPS><<<(unsigned)num_cus() * 2, RT_FB_BLOCK, 0, st>>>(ta, o0, w->ctr + CTR_ERR);
+    k_rows_tile_fb<OPS><<<(unsigned)num_cus() * 2, RT_FB_BLOCK, 0, st>>>(ta, ofb, w->ctr + CTR_ERR);
     RowArgs ra = ta.ra;
     ra.err = w->ctr + CTR_ERR;
-    k_rows_tile_tier<OPS><<<SLOW_THREADS / 64, 64, 0, st>>>(ra, o0, slow_tier(w, w->fb2, ta.fb2_count));
+    k_rows_tile_tier<OPS><<<SLOW_THREADS / 64, 64, 0, st>>>(ra, ofb, slow_tier(w, w->fb2, ta.fb2_count));
     HIP_TRY(hipGetLastError());
     rc = run_huge_tier(w, a0.offs, st, [&](const Tier &t, unsigned blocks) {
-        k_rows_tile_tier<OPS><<<blocks, 64, 0, st>>>(ra, o0, t);
+        k_rows_tile_tier<OPS><<<blocks, 64, 0, st>>>(ra, ofb, t);
     });
     if (rc) return rc;
     AK_PROF(AK_PROF_EMIT_SLOW, true, st);
@@ -150,16 +153,16 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     AK_PROF(AK_PROF_SCAN, true, st);
     AK_PROF(AK_PROF_COPY, false, st);
     if constexpr ((OPS & RT_NORM) != 0)
-        if ((rc = copy_staged<uint8_t>(o0.norm, o0.norm_cap, a0.offs, f.norm_offs, a0.n, f.norm, f.norm_cap,
-                                       RT_NORM_MUL, RT_NORM_ADD, st))) return rc;
+        if ((rc = copy_units<uint8_t>(o0.norm, ofb.norm, o0.norm_cap, a0.offs, f.norm_offs, w->unit_fb, a0.n, f.norm,
+                                      f.norm_cap, RT_NORM_MUL, RT_NORM_ADD, st))) return rc;
     if constexpr ((OPS & RT_SEG) != 0)
-        if ((rc = copy_staged<uint32_t>(o0.seg, o0.seg_cap, a0.offs, f.seg_offs, a0.n, f.seg, f.seg_cap, RT_SEG_MUL,
-                                        RT_SEG_ADD, st))) return rc;
+        if ((rc = copy_units<uint32_t>(o0.seg, ofb.seg, o0.seg_cap, a0.offs, f.seg_offs, w->unit_fb, a0.n, f.seg,
+                                       f.seg_cap, RT_SEG_MUL, RT_SEG_ADD, st))) return rc;
     if constexpr ((OPS & RT_SW) != 0) {
-        if ((rc = copy_staged<uint32_t>(o0.runs, o0.seg_cap, a0.offs, f.run_offs, a0.n, f.runs, f.run_cap, RT_SEG_MUL,
-                                        RT_SEG_ADD, st))) return rc;
-        if ((rc = copy_staged<uint8_t>(o0.labels, o0.seg_cap, a0.offs, f.run_offs, a0.n, f.labels, f.run_cap,
-                                       RT_SEG_MUL, RT_SEG_ADD, st))) return rc;
+        if ((rc = copy_units<uint32_t>(o0.runs, ofb.runs, o0.seg_cap, a0.offs, f.run_offs, w->unit_fb, a0.n, f.runs,
+                                       f.run_cap, RT_SEG_MUL, RT_SEG_ADD, st))) return rc;
+        if ((rc = copy_units<uint8_t>(o0.labels, ofb.labels, o0.seg_cap, a0.offs, f.run_offs, w->unit_fb, a0.n,
+                                      f.labels, f.run_cap, RT_SEG_MUL, RT_SEG_ADD, st))) return rc;
     }
     AK_PROF(AK_PROF_COPY, true, st);
     return AK_OK;
@@ -180,8 +183,12 @@ int launch_rows_tiles(int ops, AkWs *w, const RowArgs &a0, int matras, const Row
     const uint64_t need8 = RT_NORM_MUL * nbytes + RT_NORM_ADD * a0.n + 64;   // normalized bytes
     const uint64_t need32 = RT_SEG_MUL * nbytes + RT_SEG_ADD * a0.n + 64;    // cluster / run ends, labels
     const bool sg = (ops & RT_SEG) != 0, sw = (ops & RT_SW) != 0, nm = (ops & RT_NORM) != 0;
-    if ((rc = ws_stage_reserve(w, (sg ? need32 : 0) + (sw ? need32 : 0) + 64, st))) return rc;
-    if ((rc = ws_stage8_reserve(w, (nm ? need8 : 0) + (sw ? need32 : 0) + 64, st))) return rc;
+    // every area 64-element aligned; the first half holds the tile kernel's unit runs, the second
+    // the fallback rows' slots
+    const uint64_t A8 = (need8 + 63) & ~63ull, A32 = (need32 + 63) & ~63ull;
+    const uint64_t half8 = (nm ? A8 : 0) + (sw ? A32 : 0), half32 = (sg ? A32 : 0) + (sw ? A32 : 0);
+    if ((rc = ws_stage_reserve(w, 2 * half32 + 64, st))) return rc;
+    if ((rc = ws_stage8_reserve(w, 2 * half8 + 64, st))) return rc;
     if (w->cap_acounts < 2 * a0.n) {
         HIP_TRY(hipStreamSynchronize(st));
         (void)hipFree(w->acounts);
@@ -193,20 +200,25 @@ int launch_rows_tiles(int ops, AkWs *w, const RowArgs &a0, int matras, const Row
     RowsOut o;
     memset(&o, 0, sizeof(o));
     o.norm = w->stage8;
-    o.labels = w->stage8 + (nm ? need8 : 0);
+    o.labels = w->stage8 + (nm ? A8 : 0);
     o.seg = w->stage;
-    o.runs = w->stage + (sg ? need32 : 0);
+    o.runs = w->stage + (sg ? A32 : 0);
     o.norm_cap = need8;
     o.seg_cap = need32;
     o.cnt_norm = w->counts;
     o.cnt_seg = w->acounts;
     o.cnt_runs = w->acounts + a0.n;
     o.matras = matras;
+    RowsOut ofb = o;
+    ofb.norm = o.norm + half8;
+    ofb.labels = o.labels + half8;
+    ofb.seg = o.seg + half32;
+    ofb.runs = o.runs + half32;
     switch (ops) {
-        case RT_NORM: return launch_ops<RT_NORM>(w, a0, o, f, st);
-        case RT_SEG: return launch_ops<RT_SEG>(w, a0, o, f, st);
-        case RT_SW: return launch_ops<RT_SW>(w, a0, o, f, st);
-        case RT_NORM | RT_SEG | RT_SW: return launch_ops<RT_NORM | RT_SEG | RT_SW>(w, a0, o, f, st);
+        case RT_NORM: return launch_ops<RT_NORM>(w, a0, o, ofb, f, st);
+        case RT_SEG: return launch_ops<RT_SEG>(w, a0, o, ofb, f, st);
+        case RT_SW: return launch_ops<RT_SW>(w, a0, o, ofb, f, st);
+        case RT_NORM | RT_SEG | RT_SW: return launch_ops<RT_NORM | RT_SEG | RT_SW>(w, a0, o, ofb, f, st);
         default: break;
     }
     return set_error(AK_ERR_ARG, "rows tiles: unsupported op set");

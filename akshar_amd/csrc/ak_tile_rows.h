@@ -7,7 +7,10 @@
 //   NORM  their UTF-8 bytes (the normalized text)                      normalize.py:117-148
 //   SEG   UAX #29 cluster boundaries (+ the matra split)                 segment.py:40-125
 //   SW    script-run boundaries (digits / punctuation neutral)           segment.py:128-201
-// every output compacted by a wave prefix sum straight into the row's staging slot. Boundaries
+// every output compacted by a wave prefix sum straight into the unit's staging run (the wave
+// processes the tiles of a 64-row unit in order, so the unit's rows' outputs go back to back from
+// the unit's slot base; fallback rows write their own slot in a second staging area and the
+// unit's fallback-row mask tells the copy kernel which rows those are). Boundaries
 // look back with ballots: the previous kept char (GB3-GB9b), the nearest InCB breaker and any
 // Linker since (GB9c), the previous non-neutral script (runs); state crosses 64-element steps in
 // wave-uniform carries. The normalized alphabet only holds GCB Other / CR / LF / Control / Extend
@@ -52,6 +55,8 @@ struct RowsWaveMem {
     uint32_t rowslot[T_MAXR];    // row's byte offset in the tile (tile_front with slot 1, 0)
     uint32_t base[4][T_MAXR + 1];  // per row: kept chars / norm bytes / cluster ends / runs before it
     uint64_t passacc[10];
+    uint64_t un_norm, un_seg, un_runs;  // the unit's staging runs: next free element of each output
+    uint64_t ufbm;                      // the unit's rows (bit r - u0) sent to the fallback kernels
 };
 
 // segmentation / script class of a normalized char: gcb (4) | incb (2) << 4 | extpict << 6 |
@@ -89,13 +94,22 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
     const uint64_t lt = w_lanemask_lt();
     const uint64_t le = lt | (1ull << lane);
     const bool matras = o.matras != 0;
-    uint8_t *norm = o.norm + (RT_NORM_MUL * tr.S0 + RT_NORM_ADD * r0);
-    uint32_t *seg = o.seg + (RT_SEG_MUL * tr.S0 + RT_SEG_ADD * r0);
-    uint32_t *runs = o.runs + (RT_SEG_MUL * tr.S0 + RT_SEG_ADD * r0);
-    uint8_t *labels = o.labels + (RT_SEG_MUL * tr.S0 + RT_SEG_ADD * r0);
+    // this tile's outputs continue the unit's staging runs (element k of the tile's stream of
+    // each output -> run position + k)
+    uint8_t *norm = o.norm + M.un_norm;
+    uint32_t *seg = o.seg + M.un_seg;
+    uint32_t *runs = o.runs + M.un_runs;
+    uint8_t *labels = o.labels + M.un_runs;
 
+    // Fallback rows emit nothing into the unit's runs (their outputs come from the fallback
+    // kernels), so a row the sweep itself sends to the fallback (a grapheme class the tile path does
+    // not implement: never in normalize_text's output) makes the sweep run once more with the
+    // final flags.
+    const bool fb_front = lane < nr && M.fb[lane];
+    uint32_t kc, nbt, nst, nrt, rs;
+    for (int sweep = 0;; ++sweep) {
     // tile-wide running counts (wave-uniform) and carries across 64-element steps
-    uint32_t kc = 0, nbt = 0, nst = 0, nrt = 0, rs = 0;
+    kc = 0; nbt = 0; nst = 0; nrt = 0; rs = 0;
     uint32_t c_prev = 0xFFFFu;   // previous kept element: 0xFFFF = row start, else its class
     bool c_cons = false, c_link = false;  // GB9c: the last InCB breaker was a Consonant / a Linker since
     int c_sc = -1;               // last non-neutral script of the current row (-1: none yet)
@@ -122,6 +136,7 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
         const uint32_t e_prev_l = w_shfl(e_me, pk ? msb64(pk) : 0);
         const uint32_t e_prev = pk ? e_prev_l : c_prev;
         if (ischar && !gcb_tile_ok(cls)) M.fb[row] = 1;
+        const bool live = !M.fb[row < (uint32_t)T_MAXR ? row : 0];  // the row's outputs go to the run
         // char index of this element in its row: kept chars before it minus those before the row
         const uint32_t kc_me = kc + w_rank(CM);
         const uint32_t kc_row_l = w_shfl(kc_me, vb);
@@ -129,15 +144,13 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
         const uint32_t idx = kc_me - kc_row;  // chars of the row before this element
 
         // ---- NORM: UTF-8 bytes of each char
-        uint32_t nb_me = 0, nb_row = 0;
+        uint32_t nb_me = 0;
         if constexpr ((OPS & RT_NORM) != 0) {
-            const uint32_t len = ischar ? (uint32_t)utf8_len(x) : 0u;
+            const uint32_t len = ischar && live ? (uint32_t)utf8_len(x) : 0u;
             uint32_t tot;
             nb_me = nbt + w_exscan(len, &tot);
-            const uint32_t nb_row_l = w_shfl(nb_me, vb);
-            nb_row = bl ? nb_row_l : M.base[1][row < (uint32_t)T_MAXR ? row : 0];
-            if (ischar) {
-                uint8_t *d = norm + RT_NORM_MUL * M.rowslot[row] + RT_NORM_ADD * row + (nb_me - nb_row);
+            if (len) {
+                uint8_t *d = norm + nb_me;
                 const uint32_t cp = x;
                 if (len == 1) d[0] = (uint8_t)cp;
                 else if (len == 2) { d[0] = (uint8_t)(0xC0u | (cp >> 6)); d[1] = (uint8_t)(0x80u | (cp & 63u)); }
@@ -147,7 +160,7 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
         }
 
         // ---- SEG: cluster ends (segment_akshars, matras split)
-        uint32_t ns_me = 0, ns_row = 0;
+        uint32_t ns_me = 0;
         bool gb9c_cons = false, gb9c_link = false;
         uint64_t RKM = 0;
         if constexpr ((OPS & RT_SEG) != 0) {
@@ -180,13 +193,11 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
             else e1 = brk;
             // V_E: the row's final end (non-matras: if the row has chars; matras: if the last part is a run)
             const bool fin = ise && idx > 0 && (!matras || !(e_prev & SC_MATRA));
-            const uint32_t c = (e1 ? 1u : 0u) + (e2 ? 1u : 0u) + (fin ? 1u : 0u);
+            const uint32_t c = live ? (e1 ? 1u : 0u) + (e2 ? 1u : 0u) + (fin ? 1u : 0u) : 0u;
             uint32_t tot;
             ns_me = nst + w_exscan(c, &tot);
-            const uint32_t ns_row_l = w_shfl(ns_me, vb);
-            ns_row = bl ? ns_row_l : M.base[2][row < (uint32_t)T_MAXR ? row : 0];
             if (c) {
-                uint32_t *d = seg + RT_SEG_MUL * M.rowslot[row] + RT_SEG_ADD * row + (ns_me - ns_row);
+                uint32_t *d = seg + ns_me;
                 if (fin) d[0] = idx;
                 else {
                     if (e1) *d++ = idx;
@@ -203,7 +214,7 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
         }
 
         // ---- SW: script runs (digits / punctuation neutral); V_B resets the row's last script
-        uint32_t nr_me = 0, nr_row = 0;
+        uint32_t nr_me = 0;
         if constexpr ((OPS & RT_SW) != 0) {
             const int sc = (int)((cls >> 7) & 7u);
             const bool nn = ischar && sc != SC_DIGIT && sc != SC_PUNCT;
@@ -214,13 +225,11 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
             const int prev = pn ? prev_l : c_sc;
             const bool bnd = nn && prev >= 0 && sc != prev;
             const bool fin = ise && idx > 0;
-            const uint32_t c = (bnd || fin) ? 1u : 0u;
+            const uint32_t c = live && (bnd || fin) ? 1u : 0u;
             uint32_t tot;
             nr_me = nrt + w_exscan(c, &tot);
-            const uint32_t nr_row_l = w_shfl(nr_me, vb);
-            nr_row = bl ? nr_row_l : M.base[3][row < (uint32_t)T_MAXR ? row : 0];
             if (c) {
-                const uint32_t d = RT_SEG_MUL * M.rowslot[row] + RT_SEG_ADD * row + (nr_me - nr_row);
+                const uint32_t d = nr_me;
                 runs[d] = idx;
                 labels[d] = (uint8_t)(bnd ? prev : (prev < 0 ? 255 : prev));
             }
@@ -240,10 +249,14 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
         rs += (uint32_t)w_popc(BM);
         if (KM) c_prev = w_bcast(e_me, msb64(KM));
         w_sync();
-        (void)nb_row; (void)ns_row; (void)nr_row; (void)gb9c_cons; (void)gb9c_link;
+        (void)gb9c_cons; (void)gb9c_link;
+    }
+    w_sync();
+    if (sweep > 0 || !w_ballot(lane < nr && M.fb[lane] && !fb_front)) break;
     }
     if (lane == 0) {
         M.base[0][rs] = kc; M.base[1][rs] = nbt; M.base[2][rs] = nst; M.base[3][rs] = nrt;
+        M.un_norm += nbt; M.un_seg += nst; M.un_runs += nrt;
     }
     w_sync();
     pc.mark(TP_E);
@@ -252,6 +265,7 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
     {
         const bool isfb = lane < nr && M.fb[lane];
         const uint64_t FM = w_ballot(isfb);
+        if (lane == 0) M.ufbm |= FM << (r0 % TILE_UNIT);  // tiles never straddle a unit
         if (FM) {
             uint32_t fbase = 0;
             if (lane == 0) fbase = atomicAdd(ta.fb_count, (uint32_t)w_popc(FM));
@@ -325,8 +339,16 @@ __device__ void rows_tiles_wave(const TileArgs &ta, const RowsOut &o, const uint
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;
+        if (w_lane() == 0) {  // the unit's staging runs start at its rows' slot bases
+            const uint64_t b = ta.ra.offs[r0];
+            M.un_norm = RT_NORM_MUL * b + RT_NORM_ADD * r0;
+            M.un_seg = M.un_runs = RT_SEG_MUL * b + RT_SEG_ADD * r0;
+            M.ufbm = 0;
+        }
+        w_sync();
         for (uint64_t r = r0; r < r1;)
             r += (uint64_t)rows_tile<OPS>(ta, o, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, SC, M, pc);
+        if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
     }
     pc.flush(ta.passprof);
 }

@@ -329,19 +329,25 @@ static int64_t rows_tiles_run(int matras, const uint8_t *in, const uint64_t *off
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
     for (uint32_t i = 0; i < HOT_N; ++i) { hot_tab[i] = hot_of(prop_global(hot_cp(i))); sc_tab[i] = seg_class_of(hot_cp(i)); }
     const uint64_t nb = n ? offs[n] : 0;
-    std::vector<uint8_t> snorm(RT_NORM_MUL * nb + RT_NORM_ADD * n + 64), slab(nb + n + 64);
-    std::vector<uint32_t> sseg(nb + n + 64), sruns(nb + n + 64), cn(n), cs(n), cr(n), fbl(n), fb2(n);
+    // as the launcher: first half = the tile kernel's unit runs, second half = fallback rows' slots
+    const uint64_t h8 = RT_NORM_MUL * nb + RT_NORM_ADD * n + 64, h32 = nb + n + 64;
+    const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
+    std::vector<uint8_t> snorm(2 * h8), slab(2 * h32);
+    std::vector<uint32_t> sseg(2 * h32), sruns(2 * h32), cn(n), cs(n), cr(n), fbl(n), fb2(n);
+    std::vector<uint64_t> unit_fb(nunits);
     uint32_t fbn = 0, fb2n = 0, err = 0;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.row_status = row_status;
     ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data(); ta.fb2_count = &fb2n; ta.err = &err;
-    ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
+    ta.ntiles = nunits; ta.rows = rows; ta.unit_fb = unit_fb.data();
     RowsOut o;
     memset(&o, 0, sizeof(o));
     o.norm = snorm.data(); o.seg = sseg.data(); o.runs = sruns.data(); o.labels = slab.data();
-    o.norm_cap = snorm.size(); o.seg_cap = sseg.size();
+    o.norm_cap = h8; o.seg_cap = h32;
     o.cnt_norm = cn.data(); o.cnt_seg = cs.data(); o.cnt_runs = cr.data(); o.matras = matras;
+    RowsOut ofb = o;
+    ofb.norm = o.norm + h8; ofb.seg = o.seg + h32; ofb.runs = o.runs + h32; ofb.labels = o.labels + h32;
     RowsWaveMem *M = new RowsWaveMem();
     EmuWave W;
     std::vector<std::thread> th;
@@ -365,27 +371,37 @@ static int64_t rows_tiles_run(int matras, const uint8_t *in, const uint64_t *off
         sc.seg_cap = (int)C; sc.wsym = nullptr; sc.wpair = nullptr; sc.heap = nullptr; sc.link = nullptr; sc.word_cap = 0;
         sc.vchar = nullptr; sc.vbest = nullptr; sc.vstart = nullptr; sc.vid = nullptr; sc.vcap = 0;
         sc.slow_status = ST_LIMIT; sc.status = 0;
-        if (!rows_fb_row<OPS>(ta.ra, o, fbl[i], fast, &sc, &err)) return -2;
+        if (!rows_fb_row<OPS>(ta.ra, ofb, fbl[i], fast, &sc, &err)) return -2;
     }
     if (err) return -3;
     auto scan = [&](const std::vector<uint32_t> &c, uint64_t *oo) { oo[0] = 0; for (uint64_t r = 0; r < n; ++r) oo[r + 1] = oo[r] + c[r]; };
+    // as k_unit_copy: per unit, non-fallback rows back to back from the run base, fallback rows from
+    // their slot in the second half
+    auto ucopy = [&](auto *dst, const auto *stage, uint64_t half, const std::vector<uint32_t> &c, const uint64_t *oo,
+                     uint64_t mul, uint64_t add) {
+        for (uint64_t u = 0; u < nunits; ++u) {
+            const uint64_t u0 = u * TILE_UNIT;
+            uint64_t p = mul * offs[u0] + add * u0;
+            for (uint64_t r = u0; r < n && r < u0 + TILE_UNIT; ++r) {
+                const bool fb = (unit_fb[u] >> (r - u0)) & 1ull;
+                const uint64_t src = fb ? half + mul * offs[r] + add * r : p;
+                for (uint64_t i = 0; i < c[r]; ++i) dst[oo[r] + i] = stage[src + i];
+                if (!fb) p += c[r];
+            }
+        }
+    };
     if (OPS & RT_NORM) {
         scan(cn, norm_offs);
-        for (uint64_t r = 0; r < n; ++r)
-            for (uint64_t i = 0; i < cn[r]; ++i) norm[norm_offs[r] + i] = snorm[RT_NORM_MUL * offs[r] + RT_NORM_ADD * r + i];
+        ucopy(norm, snorm.data(), h8, cn, norm_offs, RT_NORM_MUL, RT_NORM_ADD);
     }
     if (OPS & RT_SEG) {
         scan(cs, seg_offs);
-        for (uint64_t r = 0; r < n; ++r)
-            for (uint64_t i = 0; i < cs[r]; ++i) seg[seg_offs[r] + i] = sseg[offs[r] + r + i];
+        ucopy(seg, sseg.data(), h32, cs, seg_offs, RT_SEG_MUL, RT_SEG_ADD);
     }
     if (OPS & RT_SW) {
         scan(cr, run_offs);
-        for (uint64_t r = 0; r < n; ++r)
-            for (uint64_t i = 0; i < cr[r]; ++i) {
-                runs[run_offs[r] + i] = sruns[offs[r] + r + i];
-                labels[run_offs[r] + i] = slab[offs[r] + r + i];
-            }
+        ucopy(runs, sruns.data(), h32, cr, run_offs, RT_SEG_MUL, RT_SEG_ADD);
+        ucopy(labels, slab.data(), h32, cr, run_offs, RT_SEG_MUL, RT_SEG_ADD);
     }
     return 0;
 }

@@ -39,4 +39,6 @@ for kind, name in ((0, "deva"), (1, "hing")):
         engine.profile_enable(False)
         k = sum(v[0] for v in prof.values()) / 3 / 1e3
         res["%s_%s" % (name, op)] = round(mb / k, 1)
+        if os.environ.get("AB_DETAIL"):  # per kernel class: ms per call
+            res["%s_%s_ms" % (name, op)] = {c: round(v[0] / 3, 3) for c, v in prof.items() if v[1]}
 print(json.dumps(res), flush=True)
