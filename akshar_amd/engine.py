@@ -289,7 +289,7 @@ class BPE:
 
     def __del__(self):
         h = getattr(self, "h", None)
-        if h:
+        if h and _lib is not None:  # at interpreter exit the module may already be torn down
             _lib.lib().ak_bpe_free(h)
 
     def encode_batch(self, buf, offs, flags=3, row_status=None, cap=None, nbytes=None, path=None, out=None,
@@ -331,7 +331,7 @@ class SPM:
 
     def __del__(self):
         h = getattr(self, "h", None)
-        if h:
+        if h and _lib is not None:  # at interpreter exit the module may already be torn down
             _lib.lib().ak_spm_free(h)
 
     def decode_batch(self, ids, id_offs):
