@@ -89,10 +89,13 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging area
     HIP_TRY(hipMemcpyAsync(&nbytes, a0.offs + a0.n, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    rc = ws_stage_reserve(w, SPM_T_MUL * nbytes + SPM_T_ADD * a0.n + 64, st);
+    // two halves: the tile kernel's unit runs, then the fallback rows' slots
+    const uint64_t half = SPM_T_MUL * nbytes + SPM_T_ADD * a0.n + 64;
+    rc = ws_stage_reserve(w, 2 * half, st);
     if (rc) return rc;
     const int R = w->tile_rows;
     const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the static wave stride
+    if ((rc = ws_unit_fb_reserve(w, ntiles))) return rc;
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
@@ -116,7 +119,8 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     memset(&ta, 0, sizeof(ta));
     ta.ra = a0;
     ta.ra.out = w->stage;
-    ta.ra.cap = w->cap_stage;
+    ta.ra.cap = half;
+    ta.unit_fb = w->unit_fb;
     ta.ra.out_offs = nullptr;
     ta.counts = w->counts;
     ta.fb_list = w->slow_list;
@@ -139,8 +143,11 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     AK_PROF(AK_PROF_SPM_TILES, true, st);
     HIP_TRY(hipGetLastError());
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    k_spm_tile_fb<3><<<(unsigned)num_cus() * 2, SPM_FB_BLOCK, 0, st>>>(ta);
-    RowArgs ra = ta.ra;
+    TileArgs tfb = ta;
+    tfb.ra.out = w->stage + half;
+    tfb.ra.cap = half;
+    k_spm_tile_fb<3><<<(unsigned)num_cus() * 2, SPM_FB_BLOCK, 0, st>>>(tfb);
+    RowArgs ra = tfb.ra;
     ra.counts = w->counts;
     ra.err = w->ctr + CTR_ERR;
     k_rows_tier<OP_SPM, 3><<<SLOW_THREADS / 64, 64, 0, st>>>(ra, SPM_T_MUL, SPM_T_ADD, slow_tier(w, w->fb2, ta.fb2_count));
@@ -154,7 +161,11 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     rc = scan_counts(w, a0.n, out_offs, st);
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
-    return launch_stage_copy(w, a0.offs, out_offs, a0.n, (uint32_t *)a0.out, a0.cap, SPM_T_MUL, SPM_T_ADD, st);
+    AK_PROF(AK_PROF_COPY, false, st);
+    rc = copy_units<uint32_t>(w->stage, w->stage + half, half, a0.offs, out_offs, w->unit_fb, a0.n,
+                              (uint32_t *)a0.out, a0.cap, SPM_T_MUL, SPM_T_ADD, st);
+    AK_PROF(AK_PROF_COPY, true, st);
+    return rc;
 }
 
 }  // namespace ak

@@ -7,7 +7,8 @@
 //      listed with their rows
 //   V  lane per "▁word": the unigram Viterbi over the word (the code-point trie in HBM / L2,
 //      best / back per position in LDS), backtrack into forward links
-//   F  ids (pieces; byte fallback for unk chars) into each row's staging slot, per-row counts
+//   F  ids (pieces; byte fallback for unk chars) into the unit's staging run (ak_tile.h: the rows
+//      of a 64-row unit back to back, fallback rows in a second staging half), per-row counts
 // Words run in parallel from base 0 instead of from the row's carried float score. The carried base
 // only enters a word's decisions through float rounding, so a word whose every lattice node's
 // winner beats the other candidates by more than a rounding bound tau (below) makes the same
@@ -66,6 +67,8 @@ struct SpmWaveMem {
     uint32_t rowcnt[T_MAXR];
     uint32_t rowfirst[T_MAXR];               // tile-stream position of the row's first id
     uint64_t passacc[10];
+    uint64_t unext;                          // the unit's staging run: next free position
+    uint64_t ufbm;                           // the unit's rows (bit r - u0) sent to the fallback kernels
 };
 static_assert(S_WORDS * 2 <= S_BCAP + 32, "word starts live in the byte buffer");
 static_assert(S_W + 2 * S_WORDS <= 2 * S_E, "nxt + word id counts live in V");
@@ -284,6 +287,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     {
         const bool isfb = lane < nr && M.fb[lane];
         const uint64_t FM = w_ballot(isfb);
+        if (lane == 0) M.ufbm |= FM << (r0 % TILE_UNIT);  // tiles never straddle a unit
         if (FM) {
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(ta.fb_count, (uint32_t)w_popc(FM));
@@ -293,9 +297,9 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     }
     pc.mark(TP_FBC);
 
-    // ---------------- pass F: ids -> each row's staging slot (a word's ids follow its row's earlier
-    // words), per-row counts
-    const uint64_t sbase = 2 * tr.S0 + 2 * r0;
+    // ---------------- pass F: ids -> the unit's staging run (the tile's id stream continues it: a
+    // word's ids follow its row's earlier words, rows follow each other), per-row counts
+    const uint64_t sbase = M.unext;
     uint32_t *stage = (uint32_t *)a.out + sbase;
     const uint64_t scap = a.cap > sbase ? a.cap - sbase : 0;
     bool over = false;
@@ -316,7 +320,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         if (live && last_of_row) M.rowcnt[row] = P + c - M.rowfirst[row];  // a row's words are consecutive
         if (live) {
             const int p1 = !last_of_row ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1;
-            uint64_t d = (uint64_t)M.rowslot[row] + (P - M.rowfirst[row]);
+            uint64_t d = P;
             for (int s = p0; s < p1;) {
                 const int e = s + (int)nxt[s];
                 const uint32_t id = M.back[e] >> 8;
@@ -342,6 +346,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         }
         pos += tot;
     }
+    if (lane == 0) M.unext = sbase + pos;
     if (w_ballot(over) && lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     w_sync();
     if (lane < nr && !M.fb[lane]) {
@@ -364,7 +369,13 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;
+        if (w_lane() == 0) {  // the unit's staging run starts at its rows' slot base 2 offs[r0] + 2 r0
+            M.unext = 2 * ta.ra.offs[r0] + 2 * r0;
+            M.ufbm = 0;
+        }
+        w_sync();
         for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, root, M, pc);
+        if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
     }
     pc.flush(ta.passprof);
 }

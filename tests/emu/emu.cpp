@@ -266,12 +266,15 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         scode[i] = (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
     }
     if (n == 0) { out_offs[0] = 0; return 0; }
-    std::vector<uint32_t> stage(2 * offs[n] + 2 * n + 64), counts(n), fbl(n), fb2(n);
+    const uint64_t half = 2 * offs[n] + 2 * n + 64;
+    const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
+    std::vector<uint32_t> stage(2 * half), counts(n), fbl(n), fb2(n);
+    std::vector<uint64_t> unit_fb(nunits);
     uint32_t fbn = 0, fb2n = 0, err = 0;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
-    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = stage.size();
-    ta.ra.row_status = row_status; ta.ra.spm = m->sdev;
+    ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = half;
+    ta.ra.row_status = row_status; ta.ra.spm = m->sdev; ta.unit_fb = unit_fb.data();
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
     ta.fb2_count = &fb2n; ta.err = &err;
     ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
@@ -303,15 +306,25 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         sc.vchar = vchar.data(); sc.vbest = vbest.data(); sc.vstart = vstart.data(); sc.vid = vid.data(); sc.vcap = (int)C;
         sc.slow_status = ST_LIMIT; sc.status = 0;
         const uint64_t s0 = 2 * offs[r] + 2 * r, s1 = 2 * offs[r + 1] + 2 * (r + 1);
-        const uint64_t cnt = process_row<OP_SPM, 3, true>(ta.ra, r, fast, nullptr, &sc, s0, s1);
+        RowArgs fa = ta.ra;  // fallback rows: their own slot in the second staging half
+        fa.out = stage.data() + half;
+        const uint64_t cnt = process_row<OP_SPM, 3, true>(fa, r, fast, nullptr, &sc, s0, s1);
         if ((sc.status & ST_LIMIT) || cnt > s1 - s0) return -2;
         counts[r] = (uint32_t)cnt;
         if (row_status) row_status[r] = (uint8_t)(sc.status & ST_BAD_UTF8);
     }
     out_offs[0] = 0;
     for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
-    for (uint64_t r = 0; r < n; ++r)
-        for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = stage[2 * offs[r] + 2 * r + i];
+    for (uint64_t u = 0; u < nunits; ++u) {  // as k_unit_copy
+        const uint64_t u0 = u * TILE_UNIT;
+        uint64_t p = 2 * offs[u0] + 2 * u0;
+        for (uint64_t r = u0; r < n && r < u0 + TILE_UNIT; ++r) {
+            const bool fb = (unit_fb[u] >> (r - u0)) & 1ull;
+            const uint32_t *src = fb ? stage.data() + half + 2 * offs[r] + 2 * r : stage.data() + p;
+            for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = src[i];
+            if (!fb) p += counts[r];
+        }
+    }
     return (int64_t)out_offs[n];
 }
 
