@@ -158,7 +158,7 @@ int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, cons
 #define AK_PROF_SCAN 2       /* row counts -> row offsets (three small kernels) */
 #define AK_PROF_EMIT 3       /* fast emit pass */
 #define AK_PROF_EMIT_SLOW 4  /* slow-path emit pass */
-#define AK_PROF_TILES 5      /* tile-cooperative BPE kernel (ids into per-tile staging slots) */
+#define AK_PROF_TILES 5      /* tile-cooperative BPE kernel (ids into per-unit staging runs) */
 #define AK_PROF_COPY 6       /* staged ids -> final positions (tile path) */
 #define AK_PROF_SPM_TILES 7  /* tile-cooperative SentencePiece kernel */
 #define AK_PROF_ROW_TILES 8  /* tile-cooperative normalize / segment / switches / analyze kernel */
@@ -175,7 +175,7 @@ int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each
  * pass of the tile-cooperative BPE kernel since the last call, while profiling is enabled. Slots:
  * 0 byte staging, 1 decode + NFC check + map/filter, 2 fused elongation + HF NFKC + pre-tokenizer,
- * 3 (unused), 4 pre-token start list, 5 BPE merges, 6 fallback-list append, 7 ids into row slots +
+ * 3 (unused), 4 pre-token start list, 5 BPE merges, 6 fallback-list append, 7 ids into the unit run +
  * counts, 8 (unused), 9 loop overhead.
  * Returns the number of slots written (0 if the tile kernel has not run), or a negative error. */
 #define AK_TILE_NPASS 10
