@@ -635,9 +635,9 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
 
     pc.mark(TP_B);
     // ---------------- fallback rows: append to the list (rare: one atomic per tile that has any)
+    const uint64_t FM = w_ballot(lane < nr && M.fb[lane]);  // the tile's fallback rows (final)
     {
-        const bool isfb = lane < nr && M.fb[lane];
-        const uint64_t FM = w_ballot(isfb);
+        const bool isfb = (FM >> lane) & 1ull;
         if (lane == 0) M.ufbm |= FM << (r0 % TILE_UNIT);  // tiles never straddle a unit
         if (FM) {
             uint32_t base = 0;
@@ -663,11 +663,10 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const bool isrow = in && (x == V_B || x == V_FB);
         const uint64_t RM = w_ballot(isrow);
         const uint32_t row = rs + w_rank_incl(RM) - 1;
-        const bool emit = in && x != V_FB && x != V_DEAD && !M.fb[row];
+        const bool emit = in && x != V_FB && x != V_DEAD && !((FM >> (row & 63u)) & 1ull);
         const uint64_t EM = w_ballot(emit);
         const uint32_t op = pos + w_rank(EM);
-        if (isrow) M.rowop[rs + w_rank(RM)] = op;
-        w_sync();
+        if (isrow) M.rowop[rs + w_rank(RM)] = op;  // read after the loop (counts)
         if (emit) {
             const uint64_t d = op;
             const uint32_t val = x == V_B ? m.bos : x == V_E ? m.eos : (uint32_t)(x & 0x7FFFu);
