@@ -256,6 +256,38 @@ def test_large_batch_property(eng, bpe_model):
     assert np.array_equal(_cpu(ids).astype(np.uint32), ref)
 
 
+def test_bpe_bench_launch_shape(eng, bpe_model):
+    """cfg4 exactly as bench.py times it: 10 M Hinglish rows (seed 1234, 1.5 GB) in ONE launch
+    (8,192 persistent waves over 156,250 64-row units; staging indices past 2^31 in the fallback
+    half). Launch-shape property: every row gets the ids it gets in 500 k-row launches. Pinned:
+    a strided sample of 5,000 rows plus the first and last unit equal the oracle."""
+    import torch
+    n = 10_000_000
+    buf, offs = _synth(1, n, 1234)
+    m = eng.BPE(bpe_model)
+    gb, go = _to_dev(eng, buf, offs)
+    ids, oo = m.encode_batch(gb, go)
+    del gb, go
+    oo_h = _cpu(oo).astype(np.int64)
+    assert oo_h[-1] == ids.numel()
+    step = 500_000
+    for c0 in range(0, n, step):
+        c1 = min(n, c0 + step)
+        sb = buf[offs[c0]:offs[c1]]
+        so = (offs[c0:c1 + 1] - offs[c0]).astype(np.uint64)
+        cb, co = _to_dev(eng, sb, so)
+        cids, coo = m.encode_batch(cb, co)
+        assert np.array_equal(_cpu(coo).astype(np.int64), oo_h[c0:c1 + 1] - oo_h[c0]), "row offsets differ in rows %d..%d" % (c0, c1)
+        assert torch.equal(cids, ids[oo_h[c0]:oo_h[c1]]), "ids differ in rows %d..%d" % (c0, c1)
+    rows = sorted(set(range(0, n, 2000)) | set(range(64)) | set(range(n - 64, n)))
+    texts = [bytes(buf[offs[r]:offs[r + 1]]).decode("utf-8") for r in rows]
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(*O.pack(texts))
+    ids_h = _cpu(ids)
+    for j, r in enumerate(rows):
+        got = ids_h[oo_h[r]:oo_h[r + 1]].astype(np.uint32)
+        assert np.array_equal(got, ref[ro[j]:ro[j + 1]]), "row %d differs from the oracle" % r
+
+
 def test_wave_primitives_selftest(eng):
     """DPP prefix scan, readlane broadcast and ballot behave as the tile kernels assume."""
     from akshar_amd import _lib
