@@ -261,7 +261,6 @@ def test_bpe_bench_launch_shape(eng, bpe_model):
     (8,192 persistent waves over 156,250 64-row units; staging indices past 2^31 in the fallback
     half). Launch-shape property: every row gets the ids it gets in 500 k-row launches. Pinned:
     a strided sample of 5,000 rows plus the first and last unit equal the oracle."""
-    import torch
     n = 10_000_000
     buf, offs = _synth(1, n, 1234)
     m = eng.BPE(bpe_model)
@@ -286,6 +285,34 @@ def test_bpe_bench_launch_shape(eng, bpe_model):
     for j, r in enumerate(rows):
         got = ids_h[oo_h[r]:oo_h[r + 1]].astype(np.uint32)
         assert np.array_equal(got, ref[ro[j]:ro[j + 1]]), "row %d differs from the oracle" % r
+
+
+def test_spm_bench_launch_shape(eng, spm_model):
+    """cfg5's launch shape (bench.py --workload cfg5 encodes its 100 M-row batch in 25 M-row
+    launches): one 25 M-row SentencePiece launch (seed 4242, 3.7 GB) gives every row the ids it
+    gets in 1 M-row launches; a strided sample of 2,500 rows plus the first and last unit equal the
+    oracle."""
+    n = 25_000_000
+    buf, offs = _synth(1, n, 4242)
+    m = eng.SPM(spm_model)
+    gb, go = _to_dev(eng, buf, offs)
+    ids, oo = m.encode_batch(gb, go)
+    del gb, go
+    oo_h = _cpu(oo).astype(np.int64)
+    assert oo_h[-1] == ids.numel()
+    step = 1_000_000
+    for c0 in range(0, n, step):
+        c1 = min(n, c0 + step)
+        cb, co = _to_dev(eng, buf[offs[c0]:offs[c1]], (offs[c0:c1 + 1] - offs[c0]).astype(np.uint64))
+        cids, coo = m.encode_batch(cb, co)
+        assert np.array_equal(_cpu(coo).astype(np.int64), oo_h[c0:c1 + 1] - oo_h[c0]), "row offsets differ in rows %d..%d" % (c0, c1)
+        assert torch.equal(cids, ids[oo_h[c0]:oo_h[c1]]), "ids differ in rows %d..%d" % (c0, c1)
+    rows = sorted(set(range(0, n, 10000)) | set(range(64)) | set(range(n - 64, n)))
+    texts = [bytes(buf[offs[r]:offs[r + 1]]).decode("utf-8") for r in rows]
+    ref, ro = O.OracleSPM(spm_model).encode_batch(*O.pack(texts))
+    ids_h = _cpu(ids)
+    for j, r in enumerate(rows):
+        assert np.array_equal(ids_h[oo_h[r]:oo_h[r + 1]].astype(np.uint32), ref[ro[j]:ro[j + 1]]), "row %d differs from the oracle" % r
 
 
 def test_wave_primitives_selftest(eng):
