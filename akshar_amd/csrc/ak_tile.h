@@ -52,7 +52,6 @@ struct TileWaveMem {
     uint16_t w[T_E + 16];        // +16: pass B reads WREG-symbol windows past a pre-token start
     uint8_t fb[T_MAXR];          // row goes to the fallback kernels
     uint16_t rowend[T_MAXR];     // row's end in the staged bytes
-    uint32_t rowslot[T_MAXR];    // row's staging slot, relative to the tile's (S0 + 2 r0)
     uint32_t rowop[T_MAXR + 1];  // row's first position in the tile's id stream
     uint64_t passacc[10];        // PassClock accumulators (ak_profile_tile_passes)
     uint64_t unext;              // BPE: the unit's staging run: next free position (stage index)
@@ -290,11 +289,9 @@ struct TileRows {
 //   D2: the whole tile's chars, 64 per step: decode, hot word, nfc_trig, normalize_text map -> V
 //       (M.v) with V_B / V_E sentinels around each row.
 // A row whose NFC quick check trips or that holds invalid UTF-8 is marked in M.fb (the caller sends
-// it to the fallback kernels). Row r's staging slot starts at slot_mul * (offs[r] - S0) +
-// slot_add * (r - r0) relative to the tile's slot base (M.rowslot).
+// it to the fallback kernels).
 template <int BCAP, class Mem>
-__device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, uint64_t rend, const uint32_t *H, Mem &M,
-                                               uint32_t slot_mul, uint32_t slot_add) {
+__device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, uint64_t rend, const uint32_t *H, Mem &M) {
     const int lane = w_lane();
     const int nr0 = (int)(rend - r0);
     const uint64_t myoff = lane <= nr0 ? a.offs[r0 + lane] : 0ull;
@@ -315,7 +312,6 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
     if (lane < nr) {
         M.fb[lane] = lane >= k ? 1 : 0;
         M.rowend[lane] = (uint16_t)(nextoff - a0);
-        M.rowslot[lane] = slot_mul * (uint32_t)(myoff - S0) + slot_add * (uint32_t)lane;
     }
     w_sync();
 
@@ -418,7 +414,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     const RowArgs &a = ta.ra;
     const BpeDev &m = a.bpe;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<T_BCAP>(a, r0, rend, H, M, 1u, 2u);
+    const TileRows tr = tile_front<T_BCAP>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
 

@@ -52,7 +52,6 @@ struct RowsWaveMem {
     uint16_t w[R_E + 16];        // P (pass D1)
     uint8_t fb[T_MAXR];
     uint16_t rowend[T_MAXR];
-    uint32_t rowslot[T_MAXR];    // row's byte offset in the tile (tile_front with slot 1, 0)
     uint32_t base[4][T_MAXR + 1];  // per row: kept chars / norm bytes / cluster ends / runs before it
     uint64_t passacc[10];
     uint64_t un_norm, un_seg, un_runs;  // the unit's staging runs: next free element of each output
@@ -87,7 +86,7 @@ __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<R_BCAP>(a, r0, rend, H, M, 1u, 0u);
+    const TileRows tr = tile_front<R_BCAP>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
     pc.mark(TP_D);

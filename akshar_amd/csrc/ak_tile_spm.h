@@ -61,7 +61,6 @@ struct SpmWaveMem {
     uint8_t fb[T_MAXR];
     uint8_t mfail[T_MAXR];                   // row has a lattice node within the rounding bound (pass V2)
     uint16_t rowend[T_MAXR];
-    uint32_t rowslot[T_MAXR];
     uint16_t rowpos[T_MAXR + 1];             // W position of each row's W_B (+ end)
     uint16_t wfirst[T_MAXR + 1];             // index of each row's first word (+ end)
     uint32_t rowcnt[T_MAXR];
@@ -176,7 +175,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     const RowArgs &a = ta.ra;
     const SpmDev &m = a.spm;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<S_BCAP>(a, r0, rend, H, M, 2u, 2u);
+    const TileRows tr = tile_front<S_BCAP>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
     pc.mark(TP_D);
