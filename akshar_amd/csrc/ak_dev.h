@@ -787,11 +787,14 @@ struct BpeSink {
 // ends on a char boundary, so the set of (start, piece) lattice nodes is the same.)
 // Every U+2581 is a forced lattice boundary when no piece holds it past its first char
 // (checked at model load), so the Viterbi runs one "▁word" at a time with the running best
-// score carried across words — the same float/double arithmetic as the whole-row lattice.
+// score carried across words — the same float arithmetic as the whole-row lattice, including its
+// rebase (a start whose best score leaves [-1e5, 1e5] shifts every live position from it to the
+// furthest end reached by that score; no node crosses a "▁", so that range stays in the word).
+// Restated in oracle/akshar_oracle.c spm_encode_cps.
 
 struct SpmDev {
     const int4 *trie;      // code-point double array: {check, base, value, aux}; value = id | kind << 24,
-                           // aux = score bits (normal) or UTF-8 byte length (user defined)
+                           // aux = bits of the float the node adds (score, or the user-defined bonus)
     const uint16_t *cmap_page;  // cp >> 7 -> page (0: no piece holds a char of it)
     const uint16_t *cmap;       // page * 128 + (cp & 127) -> code 1..K, 0 = in no piece
     const uint32_t *code_cp;    // code -> cp
@@ -800,7 +803,6 @@ struct SpmDev {
     uint32_t n_nodes;
     int32_t unk_id;
     float unk_score;       // min_score - 10
-    float max_score;
     float abs_score_max;   // largest |score| a lattice node can add (pieces, unk): the tile path's rounding bound
     uint16_t ws_code;      // tile path W entry of U+2581 (0x8000 | code, or the code point if no piece holds it)
 };
@@ -808,6 +810,7 @@ struct SpmDev {
 // word chars are stored as 0x80000000 | code for chars some piece holds, the plain code point
 // otherwise (the walk stops there; such a char can only become an unk node)
 constexpr uint32_t SPM_CODED = 0x80000000u;
+constexpr float SPM_REBASE = 100000.0f;  // sentencepiece 0.2.2: |best| beyond this is rebased to 0
 
 __device__ __forceinline__ uint32_t spm_code(const SpmDev &m, uint32_t cp) {
     const uint32_t pg = m.cmap_page[cp >> 7];
@@ -845,8 +848,15 @@ struct SpmSink {
         const uint32_t *vc = sc->vchar;
         best[0] = base;
         for (int i = 1; i <= L; ++i) { start[i] = -1; best[i] = 0.0f; pid[i] = -1; }
+        int reach = 0;  // furthest end reached so far (the rebase range)
         for (int s = 0; s < L; ++s) {
-            const float till = best[s];
+            float till = best[s];
+            if (till < -SPM_REBASE || till > SPM_REBASE) {
+                best[s] = 0.0f;
+                for (int q = s + 1; q <= reach; ++q)
+                    if (start[q] != -1) best[q] -= till;
+                till = 0.0f;
+            }
             bool has_single = false;
             int node = 0, nb = m->root_base;
             for (int k = s; k < L; ++k) {
@@ -859,18 +869,18 @@ struct SpmSink {
                 nb = e.y;
                 const int value = e.z;
                 if (value < 0) continue;
-                const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
-                if (kind == 2) continue;
+                if (((value >> 24) & 3) == 2) continue;  // unused piece
                 const int id = value & 0xFFFFFF;
-                const double score = kind == 1 ? (double)((float)e.w * m->max_score) - 0.1 : (double)__int_as_float(e.w);
-                const double cand = score + (double)till;
+                const float cand = __int_as_float(e.w) + till;
                 const int ee = k + 1;
-                if (start[ee] == -1 || cand > (double)best[ee]) { best[ee] = (float)cand; start[ee] = s; pid[ee] = id; }
+                if (ee > reach) reach = ee;
+                if (start[ee] == -1 || cand > best[ee]) { best[ee] = cand; start[ee] = s; pid[ee] = id; }
                 if (k == s) has_single = true;  // sentencepiece: a piece of length == the first char's length
             }
             if (!has_single) {
                 const int ee = s + 1;
                 const float cand = m->unk_score + till;
+                if (ee > reach) reach = ee;
                 if (start[ee] == -1 || cand > best[ee]) { best[ee] = cand; start[ee] = s; pid[ee] = m->unk_id; }
             }
         }

@@ -294,7 +294,6 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.byte_ids = m->d_byte_ids;
     m->dev.unk_id = unk_id;
     m->dev.unk_score = t.min_score - 10.0f;
-    m->dev.max_score = t.max_score;
     m->dev.abs_score_max = t.abs_score_max;
     m->dev.ws_code = t.ws_code;
     {   // DecodeIds tables: pieces with U+2581 -> ' ', kinds, byte values of <0xXX>

@@ -148,7 +148,7 @@ struct SpmTables {
     std::vector<uint16_t> cmap_page;  // SPM_CMAP_PAGES entries: page of cp >> 7 (0 = no piece char)
     std::vector<uint16_t> cmap;       // pages of 128 codes; page 0 all zero
     std::vector<uint32_t> code_cp;    // code -> code point (code 0 unused)
-    float min_score = 0, max_score = 0;
+    float min_score = 0;
     float abs_score_max = 0;          // largest |score| one lattice node adds (normal, user defined, unk)
     uint16_t ws_code = 0;             // tile-path W entry of U+2581 (0x8000 | code, or 0x2581 if no piece holds it)
 };
@@ -176,20 +176,25 @@ inline int utf8_decode_piece(const std::string &s, std::vector<uint32_t> &cps) {
 // Double-array trie over CODE POINTS of every NORMAL / USER_DEFINED / UNUSED piece: the code
 // points that occur in some piece get dense codes 1..K (cmap), node 0 is the root, the child of
 // node s on code c is t = base[s] + c with check[t] == s. value[t] = piece id | kind << 24 (kind 0
-// normal, 1 user defined, 2 unused) or -1; aux[t] = the piece's score bits (normal) or its UTF-8
-// byte length (user defined, scored by length). One 16-byte load per code point of the walk
-// (the byte-level trie needed two loads per UTF-8 byte plus the score load).
+// normal, 1 user defined, 2 unused) or -1; aux[t] = the float bits of the score the lattice adds:
+// the piece's score (normal) or sentencepiece 0.2.2's user-defined bonus (float)((bytes - 1) x 0.1)
+// (oracle/akshar_oracle.c spm_encode_cps). One 16-byte load per code point of the walk (the
+// byte-level trie needed two loads per UTF-8 byte plus the score load).
+// sentencepiece 0.2.2 EncodeOptimized: a USER_DEFINED piece of `bytes` UTF-8 bytes adds
+// (float)((double)(bytes - 1) * 0.1) instead of a score
+inline float user_defined_score(size_t bytes) { return (float)((double)((int)bytes - 1) * 0.1); }
+
 inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
                              const uint8_t *types, SpmTables &out) {
     if (n >= (1u << 24)) return "too many pieces";
-    float min_score = 3.4e38f, max_score = -3.4e38f;
+    float min_score = 3.4e38f;
     struct P { std::vector<uint32_t> cps; int val; int aux; };
     std::vector<P> ps;
     std::vector<uint32_t> alpha;
     std::vector<uint32_t> cps;
     for (uint32_t i = 0; i < n; ++i) {
         const int ty = types[i];
-        if (ty == 1) { min_score = std::min(min_score, scores[i]); max_score = std::max(max_score, scores[i]); }
+        if (ty == 1) min_score = std::min(min_score, scores[i]);
         if (ty != 1 && ty != 4 && ty != 5) continue;
         const uint64_t a = piece_offs[i], b = piece_offs[i + 1];
         if (b <= a) continue;
@@ -199,8 +204,8 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
         if (utf8_decode_piece(s, cps)) return "piece with invalid UTF-8";
         const int kind = ty == 1 ? 0 : ty == 4 ? 1 : 2;
         int aux = 0;
-        if (kind == 0) memcpy(&aux, &scores[i], 4);
-        else if (kind == 1) aux = (int)s.size();
+        const float sc = kind == 1 ? user_defined_score(s.size()) : scores[i];
+        if (kind != 2) memcpy(&aux, &sc, 4);
         ps.push_back({cps, (int)i | (kind << 24), aux});
         alpha.insert(alpha.end(), cps.begin(), cps.end());
     }
@@ -298,14 +303,13 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
     out.n_nodes = (uint32_t)nn;
     out.root_base = base[0];
     out.min_score = min_score;
-    out.max_score = max_score;
-    // the tile path's rounding bound (ak_tile_spm.h): normal scores, user-defined scores
-    // (length x max_score - 0.1, as the lattice computes them) and the unk score (min - 10)
+    // the tile path's rounding bound (ak_tile_spm.h): normal scores, user-defined bonuses and the
+    // unk score (min - 10)
     double amax = std::fabs((double)(min_score - 10.0f));
     for (uint32_t i = 0; i < n; ++i) {
         if (types[i] == 1) amax = std::max(amax, std::fabs((double)scores[i]));
         else if (types[i] == 4)
-            amax = std::max(amax, std::fabs((double)((float)(piece_offs[i + 1] - piece_offs[i]) * max_score) - 0.1));
+            amax = std::max(amax, std::fabs((double)user_defined_score((size_t)(piece_offs[i + 1] - piece_offs[i]))));
     }
     out.abs_score_max = (float)(amax * (1.0 + 1e-6));
     const uint16_t wpg = out.cmap_page[0x2581u >> 7];

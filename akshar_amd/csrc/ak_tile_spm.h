@@ -17,11 +17,14 @@
 // ak_dev.h SpmSink) computes it. The result is bit-identical to the reference either way (tests:
 // golden, near-tie rows, oracle at scale).
 //
-// tau: at node e every candidate's value under base b differs from its base-0 value + b by at most
-// (depth + 1) (ulp_M + ulp_0) / 2 (one rounding per stored score), and the leader is stored as a
-// float (+ ulp_M / 2). With M >= every |score| the row can reach by this word's end (chars from the
-// row start x the largest |piece or unk score|), ulp_M, ulp_0 <= M 2^-23, and the running check
-// (each candidate against the leader's stored value, which is <= the true margin + ulp_0 / 2),
+// tau: a value reached from base b is a chain of float adds (one rounding each, <= ulp_M / 2), and
+// sentencepiece's rebase only shifts every live value of the word by the same float (exact: Sterbenz),
+// so each value's offset from its base differs from the exact-sum offset by <= depth x M 2^-24, from
+// base b as from base 0. A comparison of two candidates (depth <= L + 1 each) under base b therefore
+// differs from the same comparison under base 0 by <= 2 (L + 1) (M + M) 2^-24 = (L + 1) M 2^-22; the
+// running check measures it on stored floats. M bounds every |value| the row can reach: chars from
+// the row start to the word end x the largest |piece or unk score|, and never more than
+// 1e5 + that score (the rebase keeps every carried start within [-1e5, 1e5]).
 // tau = (L + 3) M 2^-22 for a word of L chars is sufficient.
 // Reference semantics: normalize.py:117-148, tokenizer.py:190-191, cli.py:232-248.
 #pragma once
@@ -85,16 +88,23 @@ __device__ __forceinline__ uint32_t spm_wcp(const SpmDev &m, uint16_t x) {
 }
 
 // The unigram lattice of one word (W positions [p0, p1), "▁" at p0) from the float base `base`:
-// sentencepiece 0.2.2's arithmetic (double candidate for pieces, float for unk, first arrival wins
-// ties). The word owns best / back at (p0, p1] (p0 is the previous word's end node: the base stays
-// in a register). MARGIN: track the smallest gap between a candidate and the stored leader.
-// Inactive lanes pass p1 <= p0. `root` caches the trie's root children (code -> node) in LDS.
+// sentencepiece 0.2.2's arithmetic (float candidates, first arrival wins ties, the rebase of a start
+// whose best leaves [-1e5, 1e5]: ak_dev.h SpmSink). The word owns best / back at (p0, p1] (p0 is the
+// previous word's end node: the base stays in a register). MARGIN: track the smallest gap between a
+// candidate and the stored leader. Inactive lanes pass p1 <= p0. `root` caches the trie's root
+// children (code -> node) in LDS.
 template <bool MARGIN>
 __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const int4 *root, int p0, int p1, float base,
                                         float &minm) {
     for (int i = p0 + 1; i <= p1; ++i) M.back[i] = BK_NONE;
+    int reach = p0;
     for (int s = p0; s < p1; ++s) {
-        const float till = s == p0 ? base : M.best[s];
+        float till = s == p0 ? base : M.best[s];
+        if (till < -SPM_REBASE || till > SPM_REBASE) {
+            for (int q = s + 1; q <= reach; ++q)
+                if (M.back[q] != BK_NONE) M.best[q] -= till;
+            till = 0.0f;
+        }
         bool has_single = false;
         int node = 0, nb = 0;
         for (int k = s; k < p1; ++k) {
@@ -120,25 +130,25 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const in
             nb = e.y;
             const int value = e.z;
             if (value < 0) continue;
-            const int kind = (value >> 24) & 3;  // 0 normal, 1 user defined, 2 unused
-            if (kind == 2) continue;
+            if (((value >> 24) & 3) == 2) continue;  // unused piece
             const int id = value & 0xFFFFFF;
-            const double score = kind == 1 ? (double)((float)e.w * m.max_score) - 0.1 : (double)__int_as_float(e.w);
-            const double cand = score + (double)till;
+            const float cand = __int_as_float(e.w) + till;
             const int ee = k + 1;
+            reach = ee > reach ? ee : reach;
             const uint32_t bk = M.back[ee];
-            if (bk == BK_NONE || cand > (double)M.best[ee]) {
-                if (MARGIN && bk != BK_NONE) minm = fminf(minm, (float)(cand - (double)M.best[ee]));
-                M.best[ee] = (float)cand;
+            if (bk == BK_NONE || cand > M.best[ee]) {
+                if (MARGIN && bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
+                M.best[ee] = cand;
                 M.back[ee] = ((uint32_t)id << 8) | (uint32_t)(ee - s);
             } else if (MARGIN) {
-                minm = fminf(minm, (float)((double)M.best[ee] - cand));
+                minm = fminf(minm, M.best[ee] - cand);
             }
             if (k == s) has_single = true;  // sentencepiece: a piece of exactly the first char
         }
         if (!has_single) {
             const int ee = s + 1;
             const float cand = m.unk_score + till;
+            reach = ee > reach ? ee : reach;
             const uint32_t bk = M.back[ee];
             if (bk == BK_NONE || cand > M.best[ee]) {
                 if (MARGIN && bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
@@ -252,8 +262,8 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         word_dp<true>(M, m, root, p0, p1, 0.0f, minm);
         if (act) {
             // rounding bound of this word (header comment): M = (chars from the row start to the word
-            // end + 1) x the largest |score|
-            const float Mb = (float)(p1 - (int)M.rowpos[row] + 1) * m.abs_score_max + 1.0f;
+            // end + 1) x the largest |score|, at most 1e5 + that score
+            const float Mb = fminf((float)(p1 - (int)M.rowpos[row] + 1) * m.abs_score_max, SPM_REBASE + m.abs_score_max) + 1.0f;
             const float tau = (float)(p1 - p0 + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
             if (!(minm > tau)) M.mfail[row] = 1;
             wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);

@@ -599,7 +599,7 @@ typedef struct or_spm {
     uint8_t *types;
     int32_t unk_id;
     int32_t byte_ids[256];
-    float min_score, max_score;
+    float min_score;
     size_t max_len;
     /* open-addressing hash of trie-visible pieces (NORMAL, USER_DEFINED, UNUSED) */
     uint32_t hcap;
@@ -627,12 +627,8 @@ or_spm *or_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t *offs, co
     m->unk_id = unk_id;
     memcpy(m->byte_ids, byte_ids, sizeof(m->byte_ids));
     m->min_score = INFINITY;
-    m->max_score = -INFINITY;
     for (uint32_t i = 0; i < n; ++i) {
-        if (types[i] == SPT_NORMAL) {
-            if (scores[i] < m->min_score) m->min_score = scores[i];
-            if (scores[i] > m->max_score) m->max_score = scores[i];
-        }
+        if (types[i] == SPT_NORMAL && scores[i] < m->min_score) m->min_score = scores[i];
     }
     m->hcap = 1;
     while (m->hcap < 4 * n + 16) m->hcap <<= 1;
@@ -693,25 +689,40 @@ static void spm_encode_cps(const or_spm *m, const vec_t *s, vec_t *ids) {
         }
     }
     while (nb >= 3 && norm[nb - 3] == 0xE2 && norm[nb - 2] == 0x96 && norm[nb - 1] == 0x81) nb -= 3;
-    /* Viterbi */
+    /* Viterbi: sentencepiece 0.2.2 Model::EncodeOptimized (unigram_model.cc) as the installed
+     * wheel computes it. Its source is not in this container; the arithmetic below was read from
+     * the wheel's machine code (_sentencepiece.cpython-310-x86_64-linux-gnu.so, objdump) and is
+     * pinned by tests/golden (cli_golden: the 1.5 MB file as one row, every id; spm_ties; the
+     * rebase vectors of tools/gen_golden_spm_rebase.py):
+     *   - every candidate is float: cand = score + till (one float add), compared `>` against
+     *     the stored float best (first arrival wins ties); the unk candidate likewise;
+     *   - a USER_DEFINED piece scores (float)((double)(length_bytes - 1) * 0.1);
+     *   - rebase: at each start position whose best score is outside [-1e5, 1e5], that score is
+     *     subtracted (float) from every position in [start, furthest end reached so far] that
+     *     holds a node, and from the start itself, so the carried magnitude stays below ~1e5. */
     bnode_t *best = (bnode_t *)malloc(sizeof(bnode_t) * (nb + 1));
     for (size_t i = 0; i <= nb; ++i) { best[i].id = -1; best[i].score = 0.0f; best[i].starts_at = -1; }
     const float unk_score = m->min_score - 10.0f;
-    size_t st = 0;
+    size_t st = 0, reach = 0;
     while (st < nb) {
-        const float till = best[st].score;
+        float till = best[st].score;
+        if (till < -100000.0f || till > 100000.0f) {
+            for (size_t q = st; q <= reach; ++q)
+                if (q == st || best[q].starts_at != -1) best[q].score = best[q].score - till;
+            till = 0.0f;
+        }
         int has_single = 0;
         size_t mblen = one_char_len(norm[st]);
         if (mblen > nb - st) mblen = nb - st;
         for (size_t e = st + 1; e <= nb && e - st <= m->max_len; ++e) {
             int32_t id = piece_lookup(m, norm + st, e - st);
             if (id < 0 || m->types[id] == SPT_UNUSED) continue;
+            if (e > reach) reach = e;
             size_t length = e - st;
-            double score = m->types[id] == SPT_USER ? (double)((float)length * m->max_score) - 0.1
-                                                   : (double)m->scores[id];
-            double cand = score + (double)till;
-            if (best[e].starts_at == -1 || cand > (double)best[e].score) {
-                best[e].score = (float)cand;
+            const float score = m->types[id] == SPT_USER ? (float)((double)(length - 1) * 0.1) : m->scores[id];
+            const float cand = score + till;
+            if (best[e].starts_at == -1 || cand > best[e].score) {
+                best[e].score = cand;
                 best[e].starts_at = (int32_t)st;
                 best[e].id = id;
             }
@@ -719,12 +730,13 @@ static void spm_encode_cps(const or_spm *m, const vec_t *s, vec_t *ids) {
         }
         if (!has_single) {
             bnode_t *t = &best[st + mblen];
-            float cand = unk_score + till;
+            const float cand = unk_score + till;
             if (t->starts_at == -1 || cand > t->score) {
                 t->score = cand;
                 t->starts_at = (int32_t)st;
                 t->id = m->unk_id;
             }
+            if (st + mblen > reach) reach = st + mblen;
         }
         st += mblen;
     }

@@ -62,7 +62,6 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->sdev.byte_ids = m->byte_ids.data();
     m->sdev.unk_id = unk_id;
     m->sdev.unk_score = m->spm.min_score - 10.0f;
-    m->sdev.max_score = m->spm.max_score;
     m->sdev.abs_score_max = m->spm.abs_score_max;
     m->sdev.ws_code = m->spm.ws_code;
     return m;

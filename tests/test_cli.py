@@ -42,13 +42,9 @@ def _case(g, inp, model_type, fmt, model=True):
     raise KeyError((inp, model_type, fmt, model))
 
 
-# SentencePiece on one whole-file row: the lattice carries the best score across the whole row.
-# The oracle (double candidate vs float stored best, unigram_model.cc EncodeOptimized as restated
-# in oracle/akshar_oracle.c) matches the six near-tie golden rows (tests/golden/spm_ties.npz, at
-# 370K-741K bytes) but NOT the sentencepiece 0.2.2 wheel on this 1.5 MB row once the carried score
-# passes ~1.8e5: first divergence at id 22404 (DESIGN.md "Parity unpinned"). Float-only,
-# double-only, lattice and mixed restatements were tried; none reproduces the wheel on this row.
-SPM_LONG_PINNED = 22400
+# SentencePiece on one whole-file row: the lattice carries the best score across the whole row,
+# and sentencepiece 0.2.2 rebases it whenever it leaves [-1e5, 1e5] (oracle/akshar_oracle.c
+# spm_encode_cps; ak_dev.h SpmSink). The whole row is pinned to the reference CLI, every id.
 
 
 # ------------------------------------------------------------------ CPU: the cuts are exact
@@ -64,9 +60,9 @@ def test_cut_points_are_whitespace_after_solid_chars(cli_golden):
 
 
 def test_oracle_whole_row_matches_reference_cli_and_cut_pieces(cli_golden, bpe_model, spm_model):
-    """The oracle on the ~1.5 MB file as one row reproduces the reference CLI's BPE ids and its
-    SentencePiece ids up to SPM_LONG_PINNED (see below), and the BPE / normalize / segment results
-    of the cut pieces, stitched, equal the one-row results."""
+    """The oracle on the ~1.5 MB file as one row reproduces the reference CLI's BPE and
+    SentencePiece ids, and the BPE / normalize / segment results of the cut pieces, stitched,
+    equal the one-row results."""
     from akshar_amd import longrows
     raw = long_text_as_read(cli_golden).encode()
     one = (np.frombuffer(raw, np.uint8).copy(), np.asarray([0, len(raw)], np.uint64))
@@ -74,8 +70,7 @@ def test_oracle_whole_row_matches_reference_cli_and_cut_pieces(cli_golden, bpe_m
     assert " ".join(map(str, ids)) == _case(cli_golden, "long", "bpe", "id")
     sids, _ = O.OracleSPM(spm_model).encode_batch(*one)
     ref = [int(x) for x in _case(cli_golden, "long", "sentencepiece", "id").split()]
-    assert list(sids[:SPM_LONG_PINNED]) == ref[:SPM_LONG_PINNED]
-    assert list(sids) != ref  # documents the unpinned tail: drop this line once it is reproduced
+    assert list(map(int, sids)) == ref
     buf, offs = longrows.split_rows(raw)
     pieces = (buf, offs.astype(np.uint64))
     pids, poo = O.OracleBPE(bpe_model).encode_batch(*pieces)
@@ -109,16 +104,6 @@ def test_cli_tokenize_matches_reference(tmp_path, cli_golden, inp):
         if c["model"]:
             argv += ["-m", BPE_PATH if c["model"].endswith(".json") else SPM_PATH]
         got = _cli(tmp_path, argv)
-        if inp == "long" and c["model"] and c["model_type"] == "sentencepiece":
-            # the whole-file SentencePiece row: equal to the oracle on the full row, and to the
-            # reference over the pinned prefix (SPM_LONG_PINNED)
-            from akshar_amd.models import SPMModel
-            raw = path.read_text(encoding="utf-8").encode()
-            sids, _ = O.OracleSPM(SPMModel(SPM_PATH)).encode_batch(
-                np.frombuffer(raw, np.uint8).copy(), np.asarray([0, len(raw)], np.uint64))
-            assert got == " ".join(map(str, sids))
-            assert got.split()[:SPM_LONG_PINNED] == c["output"].split()[:SPM_LONG_PINNED]
-            continue
         assert got == c["output"], (inp, c["model"], c["format"])
 
 

@@ -82,10 +82,12 @@ def test_nfkc_golden(golden_nfkc, bpe_model, spm_model):
 
 
 def test_spm_near_tie_rows(spm_model):
-    """rows whose lattice decision differs between the double-candidate and a
-    float-only Viterbi (tools/find_spm_ties.py). The reference computes the double candidate on
-    every one (the recorded ids end with the double variant's pieces); the oracle does the same.
-    Only the two 370 K-char rows here (the 741 K ones run in the GPU test)."""
+    """rows whose lattice decision differs between a double-candidate and a float-only
+    Viterbi WITHOUT sentencepiece's rebase (tools/find_spm_ties.py). The reference's recorded ids end
+    with the exact winner (the "double" pieces) on every one: its rebase keeps the carried score
+    within [-1e5, 1e5], so its float candidates never round the split together; the oracle
+    (float + rebase) does the same. Only the two 370 K-char rows here (the 741 K ones run on the
+    GPU)."""
     z = np.load(GOLDEN_TIES, allow_pickle=False)
     assert int(z["n"][0]) >= 6
     for i in range(2):

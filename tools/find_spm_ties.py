@@ -16,6 +16,12 @@ without any tie of its own. For every multi-char NORMAL piece P with a split int
 word "▁P" is tried at a ladder of K; the first K where D and F pick different segmentations
 yields the test row ";:" * (K/2) + " " + P. The reference (sentencepiece, run by gen_golden.py)
 then decides which variant it computes. Build container only; writes tests/golden/spm_ties.json.
+
+Outcome (round 3): the reference takes the D pieces on all six rows, but not because it computes
+D. The wheel's EncodeOptimized uses float candidates AND rebases the carried score to 0 whenever
+it leaves [-1e5, 1e5] (oracle/akshar_oracle.c spm_encode_cps), so at these magnitudes it solves
+each word near 0 and keeps the exact winner. tools/gen_golden_spm_rebase.py holds the vectors that
+separate float + rebase from both variants here.
 """
 import json
 import os
