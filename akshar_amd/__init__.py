@@ -1,8 +1,8 @@
 """akshar_amd — MI355X-native batch tokenization engine for Akshar's encode hot path.
 
 Drop-in names of the reference package (src/akshar/__init__.py:12-20,60-109) for the path:
-`aksharTokenizer` (aliases `AksharTokenizer`, `Akshar`), `normalize_text`, `segment_akshars`,
-`detect_code_switches`, `analyze_text_composition`, `identify_script`. Everything that touches
+`aksharTokenizer` (aliases `AksharTokenizer`, `Akshar`), `normalize_text`, `normalize_hinglish`,
+`segment_akshars`, `detect_code_switches`, `analyze_text_composition`, `identify_script`. Everything that touches
 text runs in HIP kernels through the C-ABI in include/akshar.h; there is no CPU fallback.
 Imports are lazy so the package (and the C-ABI library) loads on machines without a GPU.
 """
@@ -14,6 +14,7 @@ _LAZY = {
     "Akshar": ("tokenizer", "aksharTokenizer"),
     "normalize_text": ("normalize", "normalize_text"),
     "normalize_batch": ("normalize", "normalize_batch"),
+    "normalize_hinglish": ("normalize", "normalize_hinglish"),
     "segment_akshars": ("segment", "segment_akshars"),
     "detect_code_switches": ("segment", "detect_code_switches"),
     "segment_by_script": ("segment", "segment_by_script"),

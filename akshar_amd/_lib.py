@@ -14,6 +14,12 @@ AK_OK = 0
 AK_NORM_LOWER = 1
 AK_NORM_CLEAN = 2
 AK_RAW = -1
+# ak_normalize step selection (include/akshar.h): AK_NORM_STAGES | AK_ST_*
+AK_NORM_STAGES = 16
+AK_ST_NFC = 1
+AK_ST_LOWER = 2
+AK_ST_FILTER = 4
+AK_ST_ELONG = 8
 AK_ROW_BAD_UTF8 = 1
 AK_ROW_LIMIT = 4
 AK_TILE_PASSES = ("pre", "stage_decode_nfc_map", "elong_ws_pretok", "unused", "pretoken_starts", "merge_or_viterbi",

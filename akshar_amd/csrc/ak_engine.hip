@@ -489,7 +489,12 @@ int ak::huge_prepare(AkWs *w, const uint64_t *offs, hipStream_t st, Tier *t, uns
     HIP_TRY(hipMemcpyAsync(h + 1, w->ctr + CTR_N, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     // every buffer of a row's pipeline holds <= 3 code points per raw byte (NFC at most triples a
-    // char's UTF-8, each code point is >= 1 byte), + the SPM dummy prefix / BPE sentinels
+    // char's UTF-8, each code point is >= 1 byte), + the SPM dummy prefix / BPE sentinels. HF's
+    // NFKC (BPE, clean_hinglish=False) expands further, but only per char: decomposition buffers
+    // hold one NFC segment (it ends at every starter), and a BPE pre-token ends at whitespace,
+    // which every long expansion holds (U+FDFA: 3 bytes -> 18 code points incl. 3 spaces); without
+    // a space no char passes 2 code points per byte (U+3316, U+33AF: 3 bytes -> 6; measured over
+    // every code point, tests/test_gpu_parity.py test_bpe_noclean_long_rows_vs_oracle).
     const uint64_t cap = 3ull * h[1] + 64;
     if (cap > 0x7FFFFFFFull) return fail(AK_ERR_NOMEM, "huge tier: a row of more than 700 MB (split it at spaces first)");
     const uint64_t per = pool_thread_bytes(cap);
@@ -674,8 +679,17 @@ extern "C" int ak_normalize(ak_ws *w, int flags, const uint8_t *in, const uint64
                             uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream) {
     int rc = check_common(w, in, offs, n, out, out_offs);
     if (rc) return rc;
-    if (flags < 0 || flags > 3) return fail(AK_ERR_ARG, "ak_normalize: flags must be 0..3");
+    if (flags & AK_NORM_STAGES) {
+        if (flags & ~(AK_NORM_STAGES | 15)) return fail(AK_ERR_ARG, "ak_normalize: unknown stage bits");
+        const int st = flags & 15;
+        // a mask that normalize_text's flags name runs that path (the tile kernel for the defaults)
+        if ((st & AK_ST_NFC) && ((st & AK_ST_FILTER) != 0) == ((st & AK_ST_ELONG) != 0))
+            flags = ((st & AK_ST_LOWER) ? AK_NORM_LOWER : 0) | ((st & AK_ST_FILTER) ? AK_NORM_CLEAN : 0);
+    } else if (flags < 0 || flags > 3) {
+        return fail(AK_ERR_ARG, "ak_normalize: flags must be 0..3 or AK_NORM_STAGES | AK_ST_*");
+    }
     RowArgs a = make_args(in, offs, n, out, cap, row_status);
+    if (flags & AK_NORM_STAGES) return launch_normalize_stages(flags & 15, w, a, out_offs, (hipStream_t)stream);
     return dispatch(OP_NORMALIZE, flags, w, a, out_offs, (hipStream_t)stream);
 }
 

@@ -30,7 +30,9 @@ constexpr int SCAN_ITEMS = 8;
 constexpr uint64_t SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 
 // device counters of one launch (AkWs::ctr), zeroed by every launcher
-enum { CTR_SLOW = 0, CTR_HUGE = 1, CTR_ERR = 2, CTR_N = 4 };
+// CTR_ERR: an internal overflow (ak_ws_check: engine bug); CTR_DEC_ARG: an SPM decode id past the
+// vocabulary (the caller's argument error, reported by ak_spm_decode itself)
+enum { CTR_SLOW = 0, CTR_HUGE = 1, CTR_ERR = 2, CTR_DEC_ARG = 3, CTR_N = 4 };
 constexpr uint64_t HUGE_POOL_BUDGET = 4ull << 30;  // bytes the huge tier may use for parallel rows
 
 struct AkWs {
@@ -278,6 +280,7 @@ constexpr uint32_t BPE_MUL = 1, BPE_ADD = 2;
 
 // per-op launchers (one TU each)
 int launch_normalize(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
+int launch_normalize_stages(int stages, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_segment(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_switches(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);
 int launch_bpe(int flags, AkWs *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st);

@@ -328,8 +328,8 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
         w->cap_fb2 = a0.n;
     }
     ta.fb2_list = w->fb2;
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
-    HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
+    // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 3 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit

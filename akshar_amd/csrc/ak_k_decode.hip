@@ -141,7 +141,7 @@ int launch_decode(bool spm, AkWs *w, const DecTab &t, const uint32_t *ids, const
     int rc = ws_reserve(w, n);
     if (rc) return rc;
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
-    uint32_t *err = w->ctr + CTR_ERR;
+    uint32_t *err = w->ctr + CTR_DEC_ARG;  // not CTR_ERR: a bad id is an argument error, not an engine bug
     const unsigned grid = (unsigned)std::min<uint64_t>((n + DEC_BLOCK / 64 - 1) / (DEC_BLOCK / 64), (uint64_t)num_cus() * 8);
     if (spm) k_decode<true, false><<<grid, DEC_BLOCK, 0, st>>>(t, ids, id_offs, n, out, cap, nullptr, w->counts, err);
     else k_decode<false, false><<<grid, DEC_BLOCK, 0, st>>>(t, ids, id_offs, n, out, cap, nullptr, w->counts, err);

@@ -123,8 +123,8 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     ta.ntiles = ntiles;
     ta.unit_fb = w->unit_fb;
     ta.rows = std::min(w->tile_rows, T_MAXR);
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
-    HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
+    // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 3 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = RT_BLOCK / 64;
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)num_cus() * g_rt_bpc[OPS]);

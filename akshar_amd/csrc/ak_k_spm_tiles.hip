@@ -131,8 +131,8 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.passprof = g_prof_on ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.rows = R;
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4, st));
-    HIP_TRY(hipMemsetAsync(w->tile_misc + 2, 0, 4, st));
+    // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 3 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = SPM_TILE_BLOCK / 64;
     int bpc = g_spm_blocks_per_cu;

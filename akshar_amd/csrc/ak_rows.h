@@ -143,6 +143,42 @@ __device__ __forceinline__ void run_normalized(Sink &sink, const uint2 *fast, Sc
     }
 }
 
+// AK_NORM_STAGES | mask (ak_normalize only): the selected steps of normalize_text in its order —
+// [NFC] -> [lower / allowlist map] -> [elongation] -> sink
+template <int ST, class Head>
+__device__ __forceinline__ void feed_stages(Head &h, const uint2 *fast, Scratch *sc, Reader &rd, uint64_t b, uint64_t e) {
+    uint64_t p = b;
+    if constexpr ((ST & AK_ST_NFC) != 0) {
+        NfcStage<false, Head> nfc;
+        nfc.init(&h, fast, sc);
+        while (p < e) nfc.push(utf8_next(rd, p, e, sc->status));
+        nfc.finish();
+    } else {
+        while (p < e) h.push(utf8_next(rd, p, e, sc->status));
+        h.finish();
+    }
+}
+
+template <int ST, class Next>
+__device__ __forceinline__ void map_stages(Next &n, const uint2 *fast, Scratch *sc, Reader &rd, uint64_t b, uint64_t e) {
+    // MapStage's FLAGS: bit 0 lower, bit 1 allowlist (both: normalize_text's combined per-char map)
+    constexpr int MAPF = ((ST & AK_ST_LOWER) ? 1 : 0) | ((ST & AK_ST_FILTER) ? 2 : 0);
+    MapStage<MAPF, Next> mp;
+    mp.init(&n, fast);
+    feed_stages<ST>(mp, fast, sc, rd, b, e);
+}
+
+template <int ST, class Sink>
+__device__ __forceinline__ void run_stages(Sink &sink, const uint2 *fast, Scratch *sc, Reader &rd, uint64_t b, uint64_t e) {
+    if constexpr ((ST & AK_ST_ELONG) != 0) {
+        ElongStage<Sink> el;
+        el.init(&sink);
+        map_stages<ST>(el, fast, sc, rd, b, e);
+    } else {
+        map_stages<ST>(sink, fast, sc, rd, b, e);
+    }
+}
+
 template <int FLAGS, class Sink>
 __device__ __forceinline__ void run_input(Sink &sink, const uint2 *fast, Scratch *sc, Reader &rd, uint64_t b,
                                           uint64_t e) {
@@ -150,6 +186,8 @@ __device__ __forceinline__ void run_input(Sink &sink, const uint2 *fast, Scratch
         uint64_t p = b;
         while (p < e) sink.push(utf8_next(rd, p, e, sc->status));
         sink.finish();
+    } else if constexpr ((FLAGS & AK_NORM_STAGES) != 0) {
+        run_stages<FLAGS & 15>(sink, fast, sc, rd, b, e);
     } else {
         run_normalized<FLAGS>(sink, fast, sc, rd, b, e);
     }

@@ -9,12 +9,13 @@ This is the batched form of the reference's per-string API; the
 per-string classes in tokenizer.py / normalize.py / segment.py are thin wrappers over it.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
 
 from . import _lib
-from ._lib import AK_NORM_CLEAN, AK_NORM_LOWER, AK_RAW, AksharError, check
+from ._lib import AK_NORM_CLEAN, AK_NORM_LOWER, AK_NORM_STAGES, AK_RAW, AK_ST_FILTER, AksharError, check
 from .models import BPEModel, SPMModel
 
 _WS = {}
@@ -88,6 +89,19 @@ def _check_inputs(buf, offs):
     return n
 
 
+def _check_out(out, out_offs, n, dev):
+    """Caller-provided encode outputs: int32 ids and int64 offsets (n + 1), contiguous, on `dev`;
+    checked before any launch because the kernels write through them."""
+    if out is not None:
+        if out.dtype != torch.int32 or out.device != dev or not out.is_contiguous():
+            raise TypeError("out must be a contiguous int32 tensor on %s" % dev)
+    if out_offs is not None:
+        if out_offs.dtype != torch.int64 or out_offs.device != dev or not out_offs.is_contiguous():
+            raise TypeError("out_offs must be a contiguous int64 tensor on %s" % dev)
+        if out_offs.numel() != n + 1:
+            raise ValueError("out_offs must have n + 1 = %d entries, got %d" % (n + 1, out_offs.numel()))
+
+
 def _decode(fn, h, ids, id_offs):
     if ids.dtype != torch.int32 or id_offs.dtype != torch.int64 or not (ids.is_cuda and id_offs.is_cuda):
         raise TypeError("id rows must be int32 device ids with int64 device offsets")
@@ -153,17 +167,19 @@ def _run(fn_call, n, cap, make_out, dev, ws, out=None, out_offs=None):
 
 def _tiling(ws, path):
     """path 1 = tile-cooperative kernels for flags 3 (default), 0 = the one-lane-per-row kernels."""
-    path = BPE_PATH if path is None else path
-    check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows_for(0, 0)), "ak_ws_set_tiling")
+    path = TILE_PATH if path is None else path
+    check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows()), "ak_ws_set_tiling")
 
 
 def normalize_batch(buf, offs, flags=3, row_status=None, path=None):
+    """flags: normalize_text's 0..3, or AK_NORM_STAGES | AK_ST_* for a subset of its steps."""
     n = _check_inputs(buf, offs)
     dev = buf.device
     ws = workspace(dev.index)
     _tiling(ws, path)
     nbytes = int(offs[-1].item()) if n else 0
-    cap = nbytes + 64 if flags & AK_NORM_CLEAN else int(_lib.lib().ak_normalize_cap(n, nbytes))
+    filtered = flags & AK_ST_FILTER if flags & AK_NORM_STAGES else flags & AK_NORM_CLEAN
+    cap = nbytes + 64 if filtered else int(_lib.lib().ak_normalize_cap(n, nbytes))
 
     def call(out, c, oo):
         check(_lib.lib().ak_normalize(ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
@@ -240,20 +256,16 @@ def analyze_batch(buf, offs, flags=3, matras=False, row_status=None, path=None):
     return norm[:tot[0]], oo[0], cl[:tot[1]], oo[1], runs[:tot[2]], labels[:tot[2]], oo[2]
 
 
-import os as _os
-
-# 1 = tile-cooperative single-pass kernel (default), 0 = one lane per row (staged row kernel); AK_BPE_PATH overrides
-BPE_PATH = int(_os.environ.get("AK_BPE_PATH", "1"))
-TILE_BYTES = 560      # BPE: target bytes of text per wave-tile (the tile buffer holds 768)
-SPM_TILE_BYTES = 360  # SentencePiece: target bytes per tile (the tile buffer holds 480)
+# Kernel choice for every flags-3 op (BPE / SentencePiece encode, normalize, segment, switches,
+# analyze): 1 = the tile-cooperative single-pass kernels (default), 0 = one lane per row (the staged
+# row kernels). AK_TILE_PATH overrides the default (development aid).
+TILE_PATH = int(os.environ.get("AK_TILE_PATH", "1"))
 
 
-def tile_rows_for(n, nbytes, target=TILE_BYTES):
-    """Rows per tile: tiles pack rows greedily up to their byte buffer (16 rows at most); AK_TILE_ROWS
-    overrides (development aid)."""
-    if _os.environ.get("AK_TILE_ROWS"):
-        return int(_os.environ["AK_TILE_ROWS"])
-    return 16
+def tile_rows():
+    """Rows per tile: tiles pack rows greedily up to their byte buffer, 16 rows at most;
+    AK_TILE_ROWS overrides (development aid)."""
+    return int(os.environ.get("AK_TILE_ROWS", "16"))
 
 
 class BPE:
@@ -298,13 +310,14 @@ class BPE:
         int64 device tensors, the latter n + 1 long) receive the result in place."""
         n = _check_inputs(buf, offs)
         dev = buf.device
+        _check_out(out, out_offs, n, dev)
         ws = workspace(dev.index)
         if nbytes is None:
             nbytes = int(offs[-1].item()) if n else 0
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
-        path = BPE_PATH if path is None else path
-        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows_for(n, nbytes)), "ak_ws_set_tiling")
+        path = TILE_PATH if path is None else path
+        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows()), "ak_ws_set_tiling")
 
         def call(out, c, oo):
             check(_lib.lib().ak_bpe_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
@@ -345,13 +358,14 @@ class SPM:
         path 1 = tile-cooperative kernel (flags 3), 0 = the staged row kernel."""
         n = _check_inputs(buf, offs)
         dev = buf.device
+        _check_out(out, out_offs, n, dev)
         ws = workspace(dev.index)
         if nbytes is None:
             nbytes = int(offs[-1].item()) if n else 0
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
-        path = BPE_PATH if path is None else path
-        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows_for(n, nbytes, SPM_TILE_BYTES)), "ak_ws_set_tiling")
+        path = TILE_PATH if path is None else path
+        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows()), "ak_ws_set_tiling")
 
         def call(out, c, oo):
             check(_lib.lib().ak_spm_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),

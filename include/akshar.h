@@ -54,6 +54,18 @@ extern "C" {
 #define AK_NORM_DEFAULT (AK_NORM_LOWER | AK_NORM_CLEAN)
 #define AK_RAW (-1)     /* segment/switches on the raw row (the free functions on unnormalized text) */
 
+/* ak_normalize only: AK_NORM_STAGES | any AK_ST_* runs exactly the selected steps of normalize_text,
+ * in its order, each of which the reference also exports on its own (normalize.py:13-114):
+ *   normalize_unicode  AK_ST_NFC          semantic_normalize AK_ST_LOWER
+ *   filter_garbage     AK_ST_FILTER       remove_elongations AK_ST_ELONG
+ *   normalize_hinglish AK_ST_FILTER | AK_ST_ELONG   (:110-114; no NFC, no lowercasing)
+ * AK_NORM_STAGES | AK_ST_NFC | AK_ST_LOWER | AK_ST_FILTER | AK_ST_ELONG == AK_NORM_DEFAULT. */
+#define AK_NORM_STAGES 16
+#define AK_ST_NFC 1    /* unicodedata.normalize('NFC') (:13-18) */
+#define AK_ST_LOWER 2  /* 'LATIN' in name(c) -> c.lower() (:21-45) */
+#define AK_ST_FILTER 4 /* allowlist filter (:92-107) */
+#define AK_ST_ELONG 8  /* re.sub(r'(.)\1{2,}', r'\1') (:48-56) */
+
 /* per-row status bits */
 #define AK_ROW_BAD_UTF8 1u
 #define AK_ROW_LIMIT 4u
@@ -110,7 +122,8 @@ int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_
                   const uint8_t *types, int32_t unk_id, const int32_t *byte_ids, ak_spm **out);
 void ak_spm_free(ak_spm *m);
 
-/* normalize_text(text, normalize_roman, clean_hinglish) (normalize.py:117-148) per row.
+/* normalize_text(text, normalize_roman, clean_hinglish) (normalize.py:117-148) per row, flags
+ * 0..3; or AK_NORM_STAGES | AK_ST_* for any subset of its steps (above).
  * out: UTF-8 bytes; a sufficient cap is ak_normalize_cap(). */
 int ak_normalize(ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n, uint8_t *out,
                  uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);

@@ -213,23 +213,40 @@ static void lower_expand(uint32_t cp, vec_t *out) {
     vpush(out, cp);
 }
 
+/* The four steps of normalize_text, each also a reference function of its own
+ * (normalize.py:13-114): AK_ST_* select them, applied in normalize_text's order.
+ * normalize_unicode = NFC; semantic_normalize = LOWER; filter_garbage = FILTER;
+ * remove_elongations = ELONG; normalize_hinglish = FILTER | ELONG. */
+#define AK_NORM_STAGES 16
+#define AK_ST_NFC 1
+#define AK_ST_LOWER 2
+#define AK_ST_FILTER 4
+#define AK_ST_ELONG 8
+
+static int stages_of(int flags) {
+    if (flags & AK_NORM_STAGES) return flags & 15;
+    return AK_ST_NFC | ((flags & AK_NORM_LOWER) ? AK_ST_LOWER : 0) |
+           ((flags & AK_NORM_CLEAN) ? AK_ST_FILTER | AK_ST_ELONG : 0);
+}
+
 static void normalize_cps(vec_t *s, int flags) {
-    nfc_string(s, ccc_ucd);
+    const int st = stages_of(flags);
+    if (st & AK_ST_NFC) nfc_string(s, ccc_ucd);
     vec_t t = {0};
     for (size_t i = 0; i < s->n; ++i) {
         uint32_t c = s->v[i];
-        if ((flags & AK_NORM_LOWER) && (flags & AK_NORM_CLEAN)) {
+        if ((st & AK_ST_LOWER) && (st & AK_ST_FILTER)) {
             uint32_t m = norm_map(c);
             if (m) vpush(&t, m);
-        } else if (flags & AK_NORM_LOWER) {
+        } else if (st & AK_ST_LOWER) {
             if (lower_changes(c)) lower_expand(c, &t); else vpush(&t, c);
-        } else if (flags & AK_NORM_CLEAN) {
+        } else if (st & AK_ST_FILTER) {
             if (allowed(c)) vpush(&t, c);
         } else {
             vpush(&t, c);
         }
     }
-    if (flags & AK_NORM_CLEAN) {
+    if (st & AK_ST_ELONG) {
         /* remove_elongations: a run of >= 3 identical code points (not '\n') -> one */
         s->n = 0;
         size_t i = 0;

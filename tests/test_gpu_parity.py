@@ -220,9 +220,12 @@ def test_nfkc_golden_gpu(golden_nfkc, eng, bpe_model, spm_model):
 
 def test_bpe_noclean_long_rows_vs_oracle(eng, bpe_model):
     """clean_hinglish=False rows past the fast buffers: NFKC expansion (U+FDFA: 18 code points),
-    added tokens back to back, a long mark run HF reorders, one huge pre-token -> slow / huge tiers."""
+    added tokens back to back, a long mark run HF reorders, one huge pre-token -> slow / huge tiers;
+    the largest space-free NFKC expanders (U+3316, U+33AF: 3 bytes -> 6 code points) as one row
+    (the huge tier's 3-code-points-per-byte bound, ak_engine.hip huge_prepare)."""
     texts = ["\ufdfa" * 3000, "<s></s><mask>" * 2000, "a" + "\u0301\u0316" * 3000 + " x",
-             "Ａ" * 20000, "ｶﾞ" * 5000 + "<unk>" + "각" * 3000, "ﬃ" * 9000]
+             "Ａ" * 20000, "ｶﾞ" * 5000 + "<unk>" + "각" * 3000, "ﬃ" * 9000, "\u3316" * 6000,
+             "\u33af\u3316ﬃ" * 3000]
     buf, offs = O.pack(texts)
     gb, go = _to_dev(eng, buf, offs.astype(np.int64))
     for flags in (1, 0):

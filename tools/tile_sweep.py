@@ -1,6 +1,6 @@
-"""Tile-kernel sweep (development aid): k_bpe_tiles time vs resident blocks per CU and tile bytes.
+"""Tile-kernel sweep (development aid): k_bpe_tiles time vs resident blocks per CU and rows per tile.
 
-  python tools/tile_sweep.py [rows] [bpc,...] [tile_bytes,...]
+  python tools/tile_sweep.py [rows] [bpc,...] [tile_rows,...]
 """
 import os
 import sys
@@ -13,7 +13,7 @@ from akshar_amd import engine, synth  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4_000_000
 bpcs = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4,3,2,1").split(",")]
-tbs = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "560").split(",")]
+tbs = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "16").split(",")]
 buf, offs = synth.generate(1, n, seed=1234)
 pad = np.zeros(len(buf) + 16, np.uint8)
 pad[:len(buf)] = buf
@@ -22,7 +22,7 @@ nbytes = int(offs[-1])
 m = engine.BPE("models/akshar.json")
 ref = None
 for tb in tbs:
-    engine.TILE_BYTES = tb
+    os.environ["AK_TILE_ROWS"] = str(tb)
     for bpc in bpcs:
         os.environ["AK_TILE_BPC"] = str(bpc)
         m.encode_batch(gb, go, nbytes=nbytes)
@@ -37,5 +37,5 @@ for tb in tbs:
         h = int(ids.sum().item()) ^ int(oo[-1].item())
         ref = h if ref is None else ref
         tiles_ms = prof.get("tiles", (0, 0))
-        print(f"tile_bytes={tb} bpc={bpc} prof={prof} MB/s(tiles)={nbytes / 1e3 / (tiles_ms[0] / max(tiles_ms[1], 1)):.0f}"
+        print(f"tile_rows={tb} bpc={bpc} prof={prof} MB/s(tiles)={nbytes / 1e3 / (tiles_ms[0] / max(tiles_ms[1], 1)):.0f}"
               f" same={h == ref}", flush=True)
