@@ -53,6 +53,7 @@ extern "C" const char *ak_last_error(void) { return g_err.c_str(); }
 // built-in profiler
 
 bool ak::g_prof_on = false;
+bool ak::g_prof_passes = false;
 
 namespace {
 struct ProfRec { int kernel; hipEvent_t start, stop; };
@@ -89,8 +90,9 @@ static void prof_drain() {
     g_prof_pending.clear();
 }
 
-extern "C" int ak_profile_enable(int on) {
-    ak::g_prof_on = on != 0;
+extern "C" int ak_profile_enable(int level) {
+    ak::g_prof_on = level >= 1;      // HIP events around every launch
+    ak::g_prof_passes = level >= 2;  // + the tile kernels' per-pass clocks (an instrumented build of the pass loop)
     return AK_OK;
 }
 

@@ -67,6 +67,7 @@ struct AkWs {
 
 // built-in kernel timing (include/akshar.h ak_profile_*): HIP events around every launch
 extern bool g_prof_on;
+extern bool g_prof_passes;
 void prof_mark(int kernel, bool end, hipStream_t st);
 #define AK_PROF(k, end, st) \
     do { if (ak::g_prof_on) ak::prof_mark((k), (end), (st)); } while (0)

@@ -297,7 +297,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
-    if (g_prof_on && !w->tile_passprof) {
+    if (g_prof_passes && !w->tile_passprof) {
         HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
         HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
     }
@@ -318,7 +318,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     ta.fb_count = w->tile_misc;
     ta.err = w->tile_misc + 1;
     ta.fb2_count = w->tile_misc + 2;
-    ta.passprof = g_prof_on ? w->tile_passprof : nullptr;
+    ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.rows = R;
     if (w->cap_fb2 < a0.n) {

@@ -92,7 +92,7 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
-    if (g_prof_on && !w->tile_passprof) {
+    if (g_prof_passes && !w->tile_passprof) {
         HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
         HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
     }
@@ -119,7 +119,7 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     ta.err = w->tile_misc + 1;
     ta.fb2_list = w->fb2;
     ta.fb2_count = w->tile_misc + 2;
-    ta.passprof = g_prof_on ? w->tile_passprof : nullptr;
+    ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.unit_fb = w->unit_fb;
     ta.rows = std::min(w->tile_rows, T_MAXR);

@@ -100,7 +100,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
-    if (g_prof_on && !w->tile_passprof) {
+    if (g_prof_passes && !w->tile_passprof) {
         HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
         HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
     }
@@ -128,7 +128,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.err = w->tile_misc + 1;
     ta.fb2_list = w->fb2;
     ta.fb2_count = w->tile_misc + 2;
-    ta.passprof = g_prof_on ? w->tile_passprof : nullptr;
+    ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.rows = R;
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count

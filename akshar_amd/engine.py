@@ -380,8 +380,10 @@ __all__ = ["pack", "pack_host", "to_device", "normalize_batch", "segment_batch",
            "flags_of", "workspace", "AK_RAW"]
 
 
-def profile_enable(on=True):
-    _lib.lib().ak_profile_enable(1 if on else 0)
+def profile_enable(on=True, passes=False):
+    """on: HIP events around every launch (profile_read); passes: also the tile kernels' per-pass
+    clocks (profile_tile_passes), which instrument the kernels themselves — never for timing."""
+    _lib.lib().ak_profile_enable((2 if passes else 1) if on else 0)
 
 
 def profile_reset():

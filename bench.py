@@ -55,7 +55,9 @@ def parse():
     ap.add_argument("--rows", type=int, default=None, help="cfg4: rows per GPU (10 M); cfg5: rows of the batch (100 M)")
     ap.add_argument("--chunk-rows", type=int, default=25_000_000, help="cfg5: rows per encode call")
     ap.add_argument("--gather", action="store_true", help="cfg4: also all-gather the id streams (RCCL)")
-    ap.add_argument("--cpu-rows", type=int, default=400_000, help="CPU baseline sample (rows, single thread)")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="CPU baseline: seconds per leg (3 legs per model)")
+    ap.add_argument("--cfg5-rows", type=int, default=25_000_000, help="N = 1: rows of the cfg5 SentencePiece launch block")
+    ap.add_argument("--no-cfg5", action="store_true", help="N = 1: skip the cfg5 SentencePiece launch block")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-others", action="store_true", help="skip the config 2/3/5 side measurements")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host->host rates")
@@ -88,47 +90,54 @@ def cpu_info():
     return model, os.cpu_count() or 1, avail
 
 
-def cpu_threads():
-    """Host threads this process may use: the affinity set, capped by OMP_NUM_THREADS (16 on the GPU
-    box, whose nproc shows the whole machine)."""
-    _, _, avail = cpu_info()
-    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return max(1, min(avail, cap) if cap > 0 else avail)
+def cpu_leg(model, buf, offs, threads, seconds):
+    """`threads` workers encode 2,000-row chunks of the batch (a shared cursor hands out disjoint
+    chunks, wrapping around) until `seconds` have elapsed; returns (bytes, ids, elapsed s). A
+    time-bounded leg stays bounded however few cores the host's quota really grants the threads."""
+    import itertools
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(offs) - 1
+    ch = min(2000, n)
+    nchunks = max(1, n // ch)
+    cursor = itertools.count()
+    t0 = time.perf_counter()
+    stop = t0 + seconds
+
+    def worker(_):
+        nb = ni = 0
+        while time.perf_counter() < stop:
+            k = next(cursor) % nchunks
+            r0, r1 = k * ch, (k + 1) * ch
+            sub_offs = (offs[r0:r1 + 1] - offs[r0]).astype(np.uint64)
+            ids, _ = model.encode_batch(buf[int(offs[r0]):int(offs[r1])], sub_offs)  # ctypes releases the GIL
+            nb += int(offs[r1] - offs[r0])
+            ni += len(ids)
+        return nb, ni
+
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(worker, range(threads)))
+    return sum(r[0] for r in res), sum(r[1] for r in res), time.perf_counter() - t0
 
 
 def cpu_baseline(args, buf, offs, kind):
-    """The oracle (oracle/akshar_oracle.c) on bounded samples of the same batch: one thread, then
-    all host threads (row ranges on a thread pool; ctypes releases the GIL in the C calls)."""
-    from concurrent.futures import ThreadPoolExecutor
-
+    """The oracle (oracle/akshar_oracle.c) on the same batch, time-bounded legs: every CPU of this
+    process's affinity set (the node's host cores), the per-GPU share of them (affinity / 8), and
+    one thread (the single-process reference the >= 10x target is quoted against)."""
     from akshar_amd.models import BPEModel, SPMModel
     from oracle import oracle as O
     model = (O.OracleBPE(BPEModel(os.path.join(ROOT, "models", "akshar.json"))) if kind == "bpe"
              else O.OracleSPM(SPMModel(os.path.join(ROOT, "models", "akshar.model"))))
-
-    def run(r0, r1):
-        sub_offs = (offs[r0:r1 + 1] - offs[r0]).astype(np.uint64)
-        sub = buf[int(offs[r0]):int(offs[r1])]
-        ids, _ = model.encode_batch(sub, sub_offs)
-        return len(sub), len(ids)
-
-    n1 = min(args.cpu_rows, len(offs) - 1)
-    t = time.perf_counter()
-    b1, i1 = run(0, n1)
-    dt1 = time.perf_counter() - t
-    T = cpu_threads()
-    nT = min(len(offs) - 1, n1 * T // 2)
-    cuts = [nT * k // T for k in range(T + 1)]
-    t = time.perf_counter()
-    with ThreadPoolExecutor(T) as ex:
-        res = list(ex.map(lambda k: run(cuts[k], cuts[k + 1]), range(T)))
-    dtT = time.perf_counter() - t
-    bT, iT = sum(r[0] for r in res), sum(r[1] for r in res)
     cpu_model, nproc, avail = cpu_info()
-    single = {"value": round(b1 / 1e6 / dt1, 3), "unit": "MB/s", "cores": 1, "kind": "port",
-              "tokens_per_s": round(i1 / dt1, 1),
-              "sample": "first %d rows (%.1f MB) of the timed batch, oracle/akshar_oracle.c %s encode, one thread, %.1f s"
-                        % (n1, b1 / 1e6, kind, dt1)}
+    sec = args.cpu_seconds
+
+    def leg(threads):
+        nb, ni, dt = cpu_leg(model, buf, offs, threads, sec)
+        return {"value": round(nb / 1e6 / dt, 3), "unit": "MB/s", "cores": threads, "kind": "port",
+                "tokens_per_s": round(ni / dt, 1),
+                "sample": "%.1f MB (%d-row chunks of the timed batch) in %.1f s on %d thread(s), oracle/akshar_oracle.c "
+                          "%s encode" % (nb / 1e6, min(2000, len(offs) - 1), dt, threads, kind)}
+
+    single = leg(1)
     calib = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     if os.path.exists(calib):
         c = json.load(open(calib)).get(kind)
@@ -136,11 +145,12 @@ def cpu_baseline(args, buf, offs, kind):
             single["python_reference_equivalent_mb_s"] = round(single["value"] / c["oracle_over_reference"], 3)
             single["calibration"] = "profiles/cpu_calibration.json: oracle / Python reference = %.2f on the same rows " \
                                     "(build container)" % c["oracle_over_reference"]
-    return {"value": round(bT / 1e6 / dtT, 3), "unit": "MB/s", "cores": T, "kind": "port",
-            "tokens_per_s": round(iT / dtT, 1),
-            "sample": "first %d rows (%.1f MB) of the timed batch split over %d threads, oracle/akshar_oracle.c %s "
-                      "encode, %.1f s" % (nT, bT / 1e6, T, kind, dtT),
-            "cpu_model": cpu_model, "nproc": nproc, "affinity_cpus": avail, "single_thread": single}
+    share = leg(max(1, avail // 8))
+    full = leg(avail)
+    full.update({"cpu_model": cpu_model, "nproc": nproc, "affinity_cpus": avail,
+                 "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "per_gpu_share": share,
+                 "single_thread": single})
+    return full
 
 
 # ------------------------------------------------------------------------------------------ side configs
@@ -244,10 +254,101 @@ def pmc_traffic(kernel, rows, nbytes):
     return None, None
 
 
+# ------------------------------------------------------------------------------------------ roofline
+def roofline_of(prof, kern, steps, rows, nbytes, n_ids):
+    """SURVEY.md §8(d) for the dominant kernel: read bytes (raw rows + u64 offsets) per launch / its
+    average launch time from the library's HIP events on the encode stream; PMC traffic of the same
+    launch shape from profiles/."""
+    k_ms, k_n = prof[kern]
+    k_n = max(k_n, 1)
+    avg_s = k_ms / k_n / 1e3
+    launches_per_step = k_n / steps
+    rows_l = rows / launches_per_step
+    bytes_l = nbytes / launches_per_step
+    ids_l = n_ids / launches_per_step
+    read_bytes = bytes_l + 8 * (rows_l + 1)  # raw UTF-8 rows + u64 row offsets (SURVEY.md §8(d))
+    write_bytes = 4 * ids_l + 4 * rows_l     # u32 ids into the row slots + u32 count per row
+    achieved = read_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(kern, int(round(rows_l)), int(round(bytes_l)))
+    r = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": KERNEL_NAMES[kern],
+         "kernel_avg_ms": round(avg_s * 1e3, 3), "launches_per_step": launches_per_step,
+         "achieved_is": "SURVEY.md §8(d) read bytes (sum B + 8 (N + 1)) per launch / average launch time",
+         "read_bytes_per_launch": int(read_bytes),
+         "total_algorithmic_bytes_per_launch": int(read_bytes + write_bytes),
+         "total_frac": round((read_bytes + write_bytes) / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0,
+         "kernel_ms_per_step": {k: round(v[0] / max(steps, 1), 3) for k, v in prof.items() if v[1]}}
+    if traffic_src:
+        r["traffic_source"] = traffic_src
+        r["traffic_over_algorithmic"] = round(traffic / (read_bytes + write_bytes), 3)
+    return r
+
+
+def pass_split(engine, fn, dev):
+    """Per-pass wave-cycle split of the tile kernel from ONE extra, untimed launch with the pass
+    clocks on (they instrument the kernel, so the timed steps run without them)."""
+    engine.profile_enable(True, passes=True)
+    engine.profile_tile_passes(dev)  # reset the accumulators
+    fn()
+    torch.cuda.synchronize()
+    passes = engine.profile_tile_passes(dev)
+    engine.profile_enable(False)
+    return passes
+
+
+def cfg5_block(args, dev):
+    """BASELINE config 5 on this GPU: ONE launch shape of the 100 M-row cfg5 batch (its first
+    --cfg5-rows rows, 25 M by default, the per-call chunk bench --workload cfg5 encodes), 24k unigram
+    SentencePiece, inputs in HBM; --steps timed launches (HIP events), the read roofline of
+    k_spm_tiles, PMC traffic of that launch shape from profiles/, and its own CPU baseline."""
+    from akshar_amd import engine, synth
+    rows = args.cfg5_rows
+    buf, offs = synth.generate(synth.KIND_HINGLISH, rows, seed=SEED, first=0)
+    nbytes = int(offs[-1])
+    pad = np.zeros(((nbytes + 15) // 16) * 16 + 16, dtype=np.uint8)
+    pad[:nbytes] = buf
+    gb, go = engine.to_device(pad, offs.astype(np.int64), dev=dev)
+    del pad
+    spm = engine.SPM(os.path.join(ROOT, "models", "akshar.model"), dev=dev)
+    cap = nbytes // 4 + 2 * rows + 1024
+    out = torch.empty(cap, dtype=torch.int32, device=gb.device)
+    oo = torch.empty(rows + 1, dtype=torch.int64, device=gb.device)
+
+    def run():
+        return spm.encode_batch(gb, go, nbytes=nbytes, out=out, out_offs=oo)
+
+    ids, _ = run()
+    n_ids = int(ids.numel())
+    torch.cuda.synchronize()
+    engine.profile_enable(True)
+    engine.profile_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    prof = engine.profile_read()
+    engine.profile_enable(False)
+    roof = roofline_of(prof, "spm_tiles", args.steps, rows, nbytes, n_ids)
+    roof["tile_pass_cycle_frac"] = pass_split(engine, run, dev)
+    del gb, go, out, oo
+    torch.cuda.empty_cache()
+    res = {"workload": "cfg5 launch: first %d rows of the cfg5 batch (synthetic Hinglish, seed %d), normalize_text + "
+                       "24k unigram SentencePiece (models/akshar.model), inputs in HBM" % (rows, SEED),
+           "rows": rows, "bytes": nbytes, "ids": n_ids, "ms_per_launch": round(dt * 1e3, 3),
+           "value": round(nbytes / 1e6 / dt, 2), "unit": "MB/s", "tokens_per_s": round(n_ids / dt, 1),
+           "roofline": roof}
+    if not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(args, buf, offs, "spm")
+    return res
+
+
 # ------------------------------------------------------------------------------------------ main
 def main():
     args = parse()
-    dist = args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1
+    # a process group whenever launched by torch.distributed.run (even at world size 1: the RCCL
+    # path then runs with one rank) or asked for N > 1
+    dist = args.gpus > 1 or "RANK" in os.environ
     rank, world, local = 0, 1, 0
     if dist:
         import torch.distributed as tdist
@@ -351,7 +452,7 @@ def main():
     n_ids = int(ids.numel())
     gather_s[0] = 0.0
 
-    engine.profile_enable(True)
+    engine.profile_enable(True)  # HIP events only: the timed kernels are the product kernels
     engine.profile_reset()
     if dist:
         tdist.barrier()
@@ -365,9 +466,9 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     prof = engine.profile_read()
-    passes = engine.profile_tile_passes(local)
-    fb_rows = engine.fallback_rows(local)
     engine.profile_enable(False)
+    fb_rows = engine.fallback_rows(local)
+    passes = pass_split(engine, step, local) if world == 1 else {}  # step() of N > 1 holds a collective
 
     if dist:
         t = torch.tensor([elapsed, gather_s[0]], dtype=torch.float64, device=cdev)
@@ -391,33 +492,16 @@ def main():
     # dominant kernel: per-launch algorithmic bytes / its average launch duration (HIP events the
     # library records around its own launches on the encode stream)
     kern = max(("emit", "tiles", "spm_tiles"), key=lambda k: prof.get(k, (0.0, 0))[0])
-    k_ms, k_n = prof[kern]
-    k_n = max(k_n, 1)
-    avg_s = k_ms / k_n / 1e3
-    launches_per_step = k_n / args.steps
-    rows_l = rows / launches_per_step
-    bytes_l = nbytes / launches_per_step
-    ids_l = n_ids / launches_per_step
-    read_bytes = bytes_l + 8 * (rows_l + 1)  # raw UTF-8 rows + u64 row offsets
-    write_bytes = 4 * ids_l + 4 * rows_l     # u32 ids into the row slots + u32 count per row
-    achieved = read_bytes / avg_s / 1e9 if avg_s > 0 else 0.0
-    traffic, traffic_src = pmc_traffic(kern, int(round(rows_l)), int(round(bytes_l)))
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": KERNEL_NAMES[kern],
-                "kernel_avg_ms": round(avg_s * 1e3, 3), "launches_per_step": launches_per_step,
-                "achieved_is": "SURVEY.md §8(d) read bytes (sum B + 8 (N + 1)) per launch / average launch time",
-                "read_bytes_per_launch": int(read_bytes),
-                "total_algorithmic_bytes_per_launch": int(read_bytes + write_bytes),
-                "total_frac": round((read_bytes + write_bytes) / avg_s / 1e9 / HBM_PEAK_GBS, 5) if avg_s > 0 else 0.0,
-                "kernel_ms_per_step": {k: round(v[0] / max(args.steps, 1), 3) for k, v in prof.items() if v[1]}}
-    if traffic_src:
-        roofline["traffic_source"] = traffic_src
-        roofline["traffic_over_algorithmic"] = round(traffic / (read_bytes + write_bytes), 3)
+    roofline = roofline_of(prof, kern, args.steps, rows, nbytes, n_ids)
     if passes:
         roofline["tile_pass_cycle_frac"] = passes
-        roofline["fallback_rows_per_step"] = fb_rows[0]
+        roofline["tile_pass_source"] = "one extra untimed step with the pass clocks on"
+    roofline["fallback_rows_per_step"] = fb_rows[0]
 
-    others = e2e = cpu = None
+    others = e2e = cpu = c5 = None
+    if rank == 0 and world == 1 and not cfg5 and not args.no_cfg5:
+        log(rank, "cfg5 launch block")
+        c5 = cfg5_block(args, local)
     if rank == 0 and world == 1 and not args.no_others:
         log(rank, "other configs")
         others = other_configs(local)
@@ -451,6 +535,8 @@ def main():
             line["shard_byte_imbalance"] = round(byte_imbalance, 5)
         if e2e:
             line["end_to_end"] = e2e
+        if c5:
+            line["cfg5"] = c5
         if others:
             line["other_configs"] = others
         print(json.dumps(line), flush=True)

@@ -176,7 +176,9 @@ int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, cons
 #define AK_PROF_SPM_TILES 7  /* tile-cooperative SentencePiece kernel */
 #define AK_PROF_ROW_TILES 8  /* tile-cooperative normalize / segment / switches / analyze kernel */
 #define AK_PROF_NKERNELS 9
-int ak_profile_enable(int on);
+/* level 0 off; 1 = HIP events around every launch (ak_profile_read; timing-neutral); 2 = also the
+ * tile kernels' per-pass clocks (ak_profile_tile_passes), which instrument the kernels themselves */
+int ak_profile_enable(int level);
 int ak_profile_read(int kernel, double *total_ms, uint64_t *launches);
 void ak_profile_reset(void);
 
@@ -186,7 +188,7 @@ void ak_profile_reset(void);
 int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
 
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each
- * pass of the tile-cooperative BPE kernel since the last call, while profiling is enabled. Slots:
+ * pass of the tile-cooperative BPE kernel since the last call, while profiling level 2 is on. Slots:
  * 0 byte staging, 1 decode + NFC check + map/filter, 2 fused elongation + HF NFKC + pre-tokenizer,
  * 3 (unused), 4 pre-token start list, 5 BPE merges, 6 fallback-list append, 7 ids into the unit run +
  * counts, 8 (unused), 9 loop overhead.

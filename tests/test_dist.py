@@ -126,3 +126,44 @@ def test_gloo_world2_hip_shards_match_oracle(kind):
     for _, _, _, ids, oo in res:
         assert np.array_equal(ids.astype(np.uint32), ref_ids)
         assert np.array_equal(oo.astype(np.uint64), ref_offs)
+
+
+def _nccl_worker(port, q):
+    """world size 1 over the nccl (= RCCL) backend on cuda:0: librccl loads, both all-gathers of
+    gather_ids run on device tensors, and the reassembled streams equal the rank's own."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        from akshar_amd import engine, synth
+        from tests.conftest import SPM_PATH
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        try:
+            assert dist.get_backend() == "nccl"
+            buf, offs = synth.generate(synth.KIND_HINGLISH, 50000, seed=13)
+            pad = np.zeros(((len(buf) + 15) // 16) * 16 + 16, dtype=np.uint8)
+            pad[:len(buf)] = buf
+            gb, go = engine.to_device(pad, offs.astype(np.int64), dev=0)
+            ids, oo = engine.SPM(SPM_PATH, dev=0).encode_batch(gb, go)
+            all_ids, all_offs = adist.gather_ids(ids, oo)
+            torch.cuda.synchronize()
+            ok = all_ids.is_cuda and torch.equal(all_ids, ids) and torch.equal(all_offs, oo)
+            q.put(("ok" if ok else "mismatch", int(all_ids.numel())))
+        finally:
+            dist.destroy_process_group()
+    except Exception as e:  # reported to the parent, which fails the test with it
+        q.put(("error", repr(e)))
+
+
+@pytest.mark.gpu
+def test_nccl_world1_gather_ids_on_device():
+    """The RCCL code path of bench.py --workload cfg5 / gather_ids, in a child process (the
+    process group never touches the pytest process)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[0] == "ok", res
+    assert p.exitcode == 0 and res[1] > 50000

@@ -319,6 +319,60 @@ def test_spm_bench_launch_shape(eng, spm_model):
         assert np.array_equal(ids_h[oo_h[r]:oo_h[r + 1]].astype(np.uint32), ref[ro[j]:ro[j + 1]]), "row %d differs from the oracle" % r
 
 
+def _oracle_threads(fn, buf, offs, n, parts=16):
+    """An oracle batch call over `parts` row ranges on a thread pool (ctypes releases the GIL);
+    returns the per-part results in order."""
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = [n * k // parts for k in range(parts + 1)]
+
+    def run(k):
+        a, b = cuts[k], cuts[k + 1]
+        return fn(buf[offs[a]:offs[b]].copy(), (offs[a:b + 1] - offs[a]).astype(np.uint64))
+    with ThreadPoolExecutor(parts) as ex:
+        return cuts, list(ex.map(run, range(parts)))
+
+
+def test_segment_cfg2_launch_shape_vs_oracle(eng):
+    """cfg2 exactly as bench.py times it (other_configs): 1 M synthetic Devanagari rows (seed
+    1241) in ONE segment launch of normalized rows (k_rows_tiles<2>) == the oracle on every row."""
+    n = 1_000_000
+    buf, offs = _synth(0, n, 1241)
+    ends, oo = eng.segment_batch(*_to_dev(eng, buf, offs), flags=3)
+    ends, oo = _cpu(ends).astype(np.uint32), _cpu(oo).astype(np.int64)
+    cuts, parts = _oracle_threads(lambda b, o: O.segment_batch(b, o, flags=3), buf, offs, n)
+    for k, (re_, ro) in enumerate(parts):
+        a, b = cuts[k], cuts[k + 1]
+        assert np.array_equal(oo[a:b + 1] - oo[a], ro.astype(np.int64)), "cluster offsets differ in rows %d..%d" % (a, b)
+        assert np.array_equal(ends[oo[a]:oo[b]], re_), "cluster ends differ in rows %d..%d" % (a, b)
+
+
+def test_analyze_cfg3_launch_shape_vs_oracle(eng):
+    """cfg3 exactly as bench.py times it: 1 M synthetic Hinglish rows (seed 1241) in ONE fused
+    normalize + switches + segment launch (k_rows_tiles<7>) == the oracle's normalize_text,
+    segment_akshars(norm) and detect_code_switches(norm) on every row."""
+    n = 1_000_000
+    buf, offs = _synth(1, n, 1241)
+    norm, no, cl, co, runs, labels, ro = eng.analyze_batch(*_to_dev(eng, buf, offs))
+    norm, no, cl, co = _cpu(norm), _cpu(no).astype(np.int64), _cpu(cl).astype(np.uint32), _cpu(co).astype(np.int64)
+    runs, labels, ro = _cpu(runs).astype(np.uint32), _cpu(labels), _cpu(ro).astype(np.int64)
+
+    def ref(b, o):
+        nb, nbo = O.normalize_batch(b, o, flags=3)
+        pad = np.zeros(len(nb) + 16, np.uint8)
+        pad[:len(nb)] = nb
+        return (nb, nbo) + O.segment_batch(pad, nbo, flags=-1) + O.switches_batch(pad, nbo, flags=-1)
+    cuts, parts = _oracle_threads(ref, buf, offs, n)
+    for k, (nb, nbo, ce, ceo, re_, rl, reo) in enumerate(parts):
+        a, b = cuts[k], cuts[k + 1]
+        assert np.array_equal(no[a:b + 1] - no[a], nbo.astype(np.int64)) and \
+            np.array_equal(norm[no[a]:no[b]], nb), "normalized rows differ in %d..%d" % (a, b)
+        assert np.array_equal(co[a:b + 1] - co[a], ceo.astype(np.int64)) and \
+            np.array_equal(cl[co[a]:co[b]], ce), "clusters differ in %d..%d" % (a, b)
+        assert np.array_equal(ro[a:b + 1] - ro[a], reo.astype(np.int64)) and \
+            np.array_equal(runs[ro[a]:ro[b]], re_) and np.array_equal(labels[ro[a]:ro[b]], rl), \
+            "runs differ in %d..%d" % (a, b)
+
+
 def test_wave_primitives_selftest(eng):
     """DPP prefix scan, readlane broadcast and ballot behave as the tile kernels assume."""
     from akshar_amd import _lib

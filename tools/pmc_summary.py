@@ -30,7 +30,9 @@ def counters(path, match="bpe_tiles"):
     return dict(agg), meta
 
 
-KERNEL_CLASS = {"bpe_tiles": ("tiles", "k_bpe_tiles<3>"), "spm_tiles": ("spm_tiles", "k_spm_tiles<3>")}
+KERNEL_CLASS = {"bpe_tiles": ("tiles", "k_bpe_tiles<3>"), "spm_tiles": ("spm_tiles", "k_spm_tiles<3>"),
+                "rows_tiles<2>": ("row_tiles_seg", "k_rows_tiles<2> (segment)"),
+                "rows_tiles<7>": ("row_tiles_analyze", "k_rows_tiles<7> (fused analyze)")}
 
 
 def op_summary(src, tag, match, rows, nbytes):

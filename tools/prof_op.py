@@ -26,6 +26,10 @@ elif op == "normalize":
     fn = lambda: engine.normalize_batch(gb, go)  # noqa: E731
 elif op == "segment":
     fn = lambda: engine.segment_batch(gb, go, flags=-1)  # noqa: E731
+elif op == "segment3":  # cfg2: segment of normalized rows (k_rows_tiles<2>)
+    fn = lambda: engine.segment_batch(gb, go, flags=3)  # noqa: E731
+elif op == "analyze":  # cfg3: the fused normalize + switches + segment pass (k_rows_tiles<7>)
+    fn = lambda: engine.analyze_batch(gb, go)  # noqa: E731
 else:
     fn = lambda: engine.switches_batch(gb, go)  # noqa: E731
 for _ in range(reps):
