@@ -51,6 +51,11 @@ SIGNATURES = {
     "ak_spm_decode": (I32, [P, P, P, P, U64, P, U64, P, P]),
     "ak_spm_create": (I32, [U32, P, P, P, P, ctypes.c_int32, P, ctypes.POINTER(P)]),
     "ak_spm_free": (None, [P]),
+    "ak_bpe_load": (I32, [ctypes.c_char_p, ctypes.POINTER(P)]),
+    "ak_spm_load": (I32, [ctypes.c_char_p, ctypes.POINTER(P)]),
+    "ak_model_load": (I32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(P)]),
+    "ak_model_free": (None, [P, ctypes.c_char_p]),
+    "ak_model_info": (I32, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(U64)]),
     "ak_normalize": (I32, [P, I32, P, P, U64, P, U64, P, P, P]),
     "ak_segment": (I32, [P, I32, I32, P, P, U64, P, U64, P, P, P]),
     "ak_switches": (I32, [P, I32, P, P, U64, P, P, U64, P, P, P]),

@@ -294,6 +294,20 @@ class BPE:
         check(_lib.lib().ak_bpe_set_vocab(h, len(toks), tb.ctypes.data, to.ctypes.data, sp.ctypes.data),
               "ak_bpe_set_vocab")
 
+    @classmethod
+    def load(cls, path, dev=None):
+        """The device model read by the library itself (ak_bpe_load: tokenizer.json parsed in C++, as
+        a non-Python caller of the C-ABI would load it); `model` still holds the Python reader's
+        arrays for the host-side piece strings."""
+        self = cls.__new__(cls)
+        self.model = BPEModel(path)
+        self.dev = _device(dev)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.dev):
+            check(_lib.lib().ak_bpe_load(os.fsencode(path), ctypes.byref(h)), "ak_bpe_load")
+        self.h = h
+        return self
+
     def decode_batch(self, ids, id_offs):
         """Device id rows (int32, int64 offsets) -> (uint8 UTF-8 text, int64 row offsets):
         HF Tokenizer.decode per row (tokenizer.py:219), on the device."""
@@ -341,6 +355,18 @@ class SPM:
                                            m.scores.ctypes.data, m.types.ctypes.data, m.unk_id,
                                            m.byte_ids.ctypes.data, ctypes.byref(h)), "ak_spm_create")
         self.h = h
+
+    @classmethod
+    def load(cls, path, dev=None):
+        """The device model read by the library itself (ak_spm_load: the protobuf parsed in C++)."""
+        self = cls.__new__(cls)
+        self.model = SPMModel(path)
+        self.dev = _device(dev)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.dev):
+            check(_lib.lib().ak_spm_load(os.fsencode(path), ctypes.byref(h)), "ak_spm_load")
+        self.h = h
+        return self
 
     def __del__(self):
         h = getattr(self, "h", None)

@@ -122,6 +122,24 @@ int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_
                   const uint8_t *types, int32_t unk_id, const int32_t *byte_ids, ak_spm **out);
 void ak_spm_free(ak_spm *m);
 
+/* Model files read inside the library (host code, no GPU needed to parse): a caller over the
+ * C-ABI needs no tokenizer.json / protobuf parser of its own. Same acceptance rules as
+ * ak_bpe_create / ak_spm_create above (and akshar_amd/models.py).
+ * ak_bpe_load: HF tokenizer.json -> ak_bpe_create + ak_bpe_set_added + ak_bpe_set_vocab
+ *   (replaces Tokenizer.from_file, tokenizer.py:96-97).
+ * ak_spm_load: SentencePiece .model (ModelProto wire format) -> ak_spm_create
+ *   (replaces SentencePieceProcessor.Load, tokenizer.py:88-90).
+ * ak_model_load: model_type "bpe" (-> ak_bpe*) or "sentencepiece" (-> ak_spm*), the reference's
+ *   aksharTokenizer(model_path, model_type) choice (tokenizer.py:54-102); ak_model_free likewise.
+ * ak_model_info (parse only, no device): info[0] vocab / piece count, BPE: [1] single-char
+ *   entries, [2] merges, [3] bos, [4] eos, [5] added tokens; SPM: [1] unk id; [7] a 64-bit FNV-1a
+ *   of every array the loader would pass to the create calls, in their argument order. */
+int ak_bpe_load(const char *path, ak_bpe **out);
+int ak_spm_load(const char *path, ak_spm **out);
+int ak_model_load(const char *path, const char *model_type, void **out);
+void ak_model_free(void *h, const char *model_type);
+int ak_model_info(const char *path, const char *model_type, uint64_t info[8]);
+
 /* normalize_text(text, normalize_roman, clean_hinglish) (normalize.py:117-148) per row, flags
  * 0..3; or AK_NORM_STAGES | AK_ST_* for any subset of its steps (above).
  * out: UTF-8 bytes; a sufficient cap is ak_normalize_cap(). */
