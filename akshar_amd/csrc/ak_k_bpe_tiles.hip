@@ -232,7 +232,7 @@ int ws_unit_fb_reserve(AkWs *w, uint64_t nunits) {
     return AK_OK;
 }
 
-// wave-primitive self-test (ak_selftest): DPP scan, readlane broadcast, ballot on known patterns
+// wave-primitive self-test (ak_selftest): DPP scan, readlane broadcast, ballot, DPP wave_shr on known patterns
 __global__ __launch_bounds__(64) void k_selftest(uint32_t *out) {
     const int lane = w_lane();
     uint32_t tot;
@@ -243,15 +243,16 @@ __global__ __launch_bounds__(64) void k_selftest(uint32_t *out) {
     const uint64_t b = w_bcast(((uint64_t)lane << 40) | (uint64_t)(lane + 5), 63);
     out[192 + lane] = (uint32_t)(b >> 40) + (uint32_t)(b & 0xFFFFFFFFu);
     out[256 + lane] = (uint32_t)w_popc(w_ballot((lane % 3) == 0) & w_lanemask_lt());
+    out[320 + lane] = w_prev((uint32_t)(lane * 5 + 2), 999u);
 }
 
 int selftest_wave() {
     uint32_t *d = nullptr;
-    HIP_TRY(hipMalloc(&d, 320 * 4));
-    HIP_TRY(hipMemset(d, 0xFF, 320 * 4));
+    HIP_TRY(hipMalloc(&d, 384 * 4));
+    HIP_TRY(hipMemset(d, 0xFF, 384 * 4));
     k_selftest<<<1, 64>>>(d);
     HIP_TRY(hipGetLastError());
-    uint32_t h[320];
+    uint32_t h[384];
     HIP_TRY(hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost));
     (void)hipFree(d);
     uint32_t ex = 0, total = 0;
@@ -259,11 +260,12 @@ int selftest_wave() {
     for (int l = 0; l < 64; ++l) {
         uint32_t below = 0;
         for (int j = 0; j < l; ++j) below += (j % 3) == 0;
+        const uint32_t prev = l ? (uint32_t)((l - 1) * 5 + 2) : 999u;
         if (h[l] != ex || h[64 + l] != total || h[128 + l] != 37u * 3 + 1 || h[192 + l] != 63u + 68u ||
-            h[256 + l] != below) {
-            char msg[160];
-            snprintf(msg, sizeof(msg), "wave self-test failed at lane %d: exscan %u/%u total %u/%u bcast %u bcast64 %u ballot %u/%u",
-                     l, h[l], ex, h[64 + l], total, h[128 + l], h[192 + l], h[256 + l], below);
+            h[256 + l] != below || h[320 + l] != prev) {
+            char msg[200];
+            snprintf(msg, sizeof(msg), "wave self-test failed at lane %d: exscan %u/%u total %u/%u bcast %u bcast64 %u ballot %u/%u prev %u/%u",
+                     l, h[l], ex, h[64 + l], total, h[128 + l], h[192 + l], h[256 + l], below, h[320 + l], prev);
             return set_error(AK_ERR_HIP, msg);
         }
         ex += (uint32_t)(l * 7 + 3) % 11u;

@@ -46,6 +46,11 @@ inline T w_shfl(T v, int src) {
 // value of lane src (src wave-uniform)
 template <typename T>
 inline T w_bcast(T v, int src) { return w_shfl(v, src); }
+// value of lane - 1; lane 0 gets `fill`
+inline uint32_t w_prev(uint32_t v, uint32_t fill) {
+    const uint32_t x = w_shfl(v, t_lane ? t_lane - 1 : 0);
+    return t_lane ? x : fill;
+}
 // exclusive prefix sum over lanes; *total gets the wave sum
 inline uint32_t w_exscan(uint32_t v, uint32_t *total) {
     t_wave->slot[t_lane] = v;
@@ -111,6 +116,11 @@ __device__ __forceinline__ T w_bcast(T v, int src) {
         const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), src);
         return __builtin_bit_cast(T, ((uint64_t)hi << 32) | lo);
     }
+}
+// value of lane - 1, lane 0 gets `fill`: DPP wave_shr:1 (a VALU op, no LDS round trip like
+// ds_bpermute); all 64 lanes must be active
+__device__ __forceinline__ uint32_t w_prev(uint32_t v, uint32_t fill) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
 }
 // inclusive wave64 prefix sum in DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31
 // across rows); all 64 lanes must be active

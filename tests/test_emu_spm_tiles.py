@@ -55,6 +55,36 @@ def test_synthetic_vs_oracle(em, spm_model, kind):
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+def test_trie_walking_lattice_vs_oracle(spm_model, kind):
+    """Models whose pieces pass the register window (ak_tile_spm.h SPM_WIN) take word_dp, the
+    lattice that walks the trie itself: forced here on the trained model (its pieces fit)."""
+    from akshar_amd import synth
+    m = emu.Model(spm=spm_model)
+    emu.lib().emu_spm_set_max_piece(m.h, 99)
+    buf, offs = synth.generate(kind, 500, seed=700 + kind)
+    ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_userdef_model_vs_golden():
+    """A model with USER_DEFINED pieces and pieces past the window (tests/golden/spm_userdef.model,
+    longest 12 chars): the reference's ids (tools/gen_golden_spm_rebase.py)."""
+    import gzip
+    import json
+    import os
+    from akshar_amd.models import SPMModel
+    from tests.conftest import ROOT
+    from tests.test_spm_rebase import _userdef_lines
+    m = emu.Model(spm=SPMModel(os.path.join(ROOT, "tests", "golden", "spm_userdef.model")))
+    with gzip.open(os.path.join(ROOT, "tests", "golden", "spm_rebase.json.gz"), "rt", encoding="utf-8") as f:
+        want = json.load(f)["userdef_rows"]
+    buf, offs = O.pack(_userdef_lines())
+    ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
+    assert rows_ints(ids, oo) == want
+
+
 def test_margin_rule_keeps_hinglish_on_the_tile_path(em):
     """The word-parallel lattice's rounding bound almost never sends a synthetic row back to the
     sequential kernels (the model's winners beat the runners-up by >= 0.5; the bound is ~1e-2)."""
