@@ -293,21 +293,11 @@ __device__ __forceinline__ float word_dp_win(SpmWaveMem &M, const SpmDev &m, con
     bk[0] = 0;
 #pragma unroll
     for (int j = 1; j <= SPM_WIN; ++j) { win[j] = 0.0f; bk[j] = BK_NONE; }
-    auto put = [&](float &wv, uint32_t &bv, float c, uint32_t b) {
-        if (bv == BK_NONE || c > wv) {
-            if (MARGIN && bv != BK_NONE) minm = fminf(minm, c - wv);
-            wv = c;
-            bv = b;
-        } else if (MARGIN) {
-            minm = fminf(minm, wv - c);
-        }
-    };
     for (int s = p0; s < p1; ++s) {
         float till = win[0];
         if (till < -SPM_REBASE || till > SPM_REBASE) {  // sentencepiece's rebase (never at tile sizes)
 #pragma unroll
-            for (int j = 1; j <= SPM_WIN; ++j)
-                if (bk[j] != BK_NONE) win[j] -= till;
+            for (int j = 1; j <= SPM_WIN; ++j) win[j] = bk[j] != BK_NONE ? win[j] - till : win[j];
             till = 0.0f;
         }
         const uint32_t x = M.w[s];
@@ -336,15 +326,29 @@ __device__ __forceinline__ float word_dp_win(SpmWaveMem &M, const SpmDev &m, con
             c1 = m.unk_score + till;
             b1 = ((uint32_t)m.unk_id << 8) | 1u;
         }
-        put(win[1], bk[1], c1, b1);
-        // lengths 2..SPM_WIN from pass A, in increasing length (the lattice's order of arrival)
+        // lengths 2..SPM_WIN from pass A, in increasing length (the lattice's order of arrival);
+        // every slot is updated by selects (no per-slot branch)
         const uint32_t lm = eo >> 9, off = eo & 511u;
 #pragma unroll
-        for (int j = 2; j <= SPM_WIN; ++j) {
-            if ((lm >> (j - 2)) & 1u) {
-                const SpmEdge ed = M.edges[off + (uint32_t)__builtin_popcount(lm & ((1u << (j - 2)) - 1u))];
-                put(win[j], bk[j], ed.score + till, ((ed.v & 0xFFFFFFu) << 8) | (uint32_t)j);
+        for (int j = 1; j <= SPM_WIN; ++j) {
+            bool has = true;
+            float c = c1;
+            uint32_t b = b1;
+            if (j > 1) {
+                has = ((lm >> (j - 2)) & 1u) != 0u;
+                const uint32_t idx = off + (uint32_t)__builtin_popcount(lm & ((1u << (j - 2)) - 1u));
+                const SpmEdge ed = has ? M.edges[idx] : SpmEdge{0.0f, 0u};
+                c = ed.score + till;
+                b = ((ed.v & 0xFFFFFFu) << 8) | (uint32_t)j;
             }
+            const bool fresh = bk[j] == BK_NONE;
+            const bool take = has && (fresh || c > win[j]);
+            if (MARGIN) {
+                const float gap = take ? c - win[j] : win[j] - c;
+                minm = (has && !fresh) ? fminf(minm, gap) : minm;
+            }
+            win[j] = take ? c : win[j];
+            bk[j] = take ? b : bk[j];
         }
         M.back[s + 1] = bk[1];  // position s + 1 is final
 #pragma unroll
@@ -449,7 +453,11 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     // is redone exactly below (pass V2); then the backtrack into forward links + id counts.
     uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
     uint16_t *eoff = M.v;  // pass A -> V / V2 (the backtrack's nxt + wcnt replace it)
+#ifdef AK_SPM_FORCE_OLD
+    const bool win_path = false;  // development aid: the trie-walking lattice for every model
+#else
     const bool win_path = m.max_piece_cps <= (uint16_t)SPM_WIN;
+#endif
     if (win_path && nw) {
         if (!spm_walks(M, m, root, wlen, eoff)) {  // more edges than the tile holds: its rows fall back
             if (lane < nr) M.fb[lane] = 1;
@@ -458,6 +466,21 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         w_sync();
     }
     pc.mark(TP_P);
+#ifdef AK_SPM_DEBUG
+    if (win_path && r0 == 0 && lane == 0) {
+        printf("AKDBG wlen %u nw %u\n", wlen, nw);
+        for (uint32_t q = 0; q < wlen && q < 40; ++q) {
+            const uint32_t eo = eoff[q];
+            printf("AKDBG pos %u w %04x eoff %04x off %u mask %x", q, (unsigned)M.w[q], eo, eo & 511u, eo >> 9);
+            const uint32_t lm = eo >> 9;
+            for (int i = 0; i < __builtin_popcount(lm); ++i) {
+                const SpmEdge ed = M.edges[(eo & 511u) + i];
+                printf(" [%u len %u id %u sc %f]", (eo & 511u) + i, ed.v >> 24, ed.v & 0xFFFFFFu, ed.score);
+            }
+            printf("\n");
+        }
+    }
+#endif
     for (uint32_t jb = 0; jb < nw; jb += 64) {
         const uint32_t j = jb + (uint32_t)lane;
         const bool act = j < nw;
