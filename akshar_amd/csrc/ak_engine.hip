@@ -298,7 +298,6 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.unk_score = t.min_score - 10.0f;
     m->dev.abs_score_max = t.abs_score_max;
     m->dev.ws_code = t.ws_code;
-    m->dev.max_piece_cps = (uint16_t)std::min<uint32_t>(t.max_piece_cps, 0xFFFFu);
     {   // DecodeIds tables: pieces with U+2581 -> ' ', kinds, byte values of <0xXX>
         std::vector<uint8_t> text, kind(n), bv(n, 0);
         std::vector<uint32_t> off(n + 1, 0);

@@ -151,7 +151,6 @@ struct SpmTables {
     float min_score = 0;
     float abs_score_max = 0;          // largest |score| one lattice node adds (normal, user defined, unk)
     uint16_t ws_code = 0;             // tile-path W entry of U+2581 (0x8000 | code, or 0x2581 if no piece holds it)
-    uint32_t max_piece_cps = 0;       // longest NORMAL / USER_DEFINED piece in code points (the tile lattice's window)
 };
 
 constexpr uint32_t SPM_CMAP_PAGES = 0x110000u >> 7;
@@ -204,7 +203,6 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
         if (s.find("\xe2\x96\x81", 1) != std::string::npos) return "piece with an inner U+2581";
         if (utf8_decode_piece(s, cps)) return "piece with invalid UTF-8";
         const int kind = ty == 1 ? 0 : ty == 4 ? 1 : 2;
-        if (kind != 2) out.max_piece_cps = std::max(out.max_piece_cps, (uint32_t)cps.size());
         int aux = 0;
         const float sc = kind == 1 ? user_defined_score(s.size()) : scores[i];
         if (kind != 2) memcpy(&aux, &sc, 4);

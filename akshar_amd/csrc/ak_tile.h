@@ -541,11 +541,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     {
         // 64 rank rows fit bytes + the part of V below the kept starts (at most T_SCAP of them)
         static_assert(64 * 2 * WREG <= (T_BCAP + 32) + 2 * (T_E - T_SCAP), "rank rows overlap the starts");
-        // a lane's 16 pair values as two 16-byte halves, lane-contiguous per half (lane * 16 and
-        // 1024 + lane * 16): each ds_read_b128 of the wave covers 1 KB without bank conflicts
-        static_assert(WREG == 16, "rank rows are two 8 x u16 halves");
-        uint8_t *rkb = M.bytes + lane * 16;
-        auto rk = [&](int i) -> uint16_t & { return *(uint16_t *)(rkb + 2 * (i & 7) + (i >> 3) * 1024); };
+        uint16_t *rk16 = (uint16_t *)(M.bytes + lane * (2 * WREG));
         for (uint32_t wb = 0; wb < nw; wb += 64) {
             const uint32_t j = wb + lane;
             const bool act = j < nw;
@@ -570,15 +566,17 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             }
             w_sync();  // every lane has read V and its window before rank rows overwrite bytes / V
             {  // every lane writes its rank row (all 0xFFFF unless reg): the merge rounds read it unmasked
-                *(uint4 *)rkb = make_uint4(d[0], d[1], d[2], d[3]);
-                *(uint4 *)(rkb + 1024) = make_uint4(d[4], d[5], d[6], d[7]);
+                uint4 *r4 = (uint4 *)rk16;
+                r4[0] = make_uint4(d[0], d[1], d[2], d[3]);
+                r4[1] = make_uint4(d[4], d[5], d[6], d[7]);
             }
             if (reg) M.w[st] = (uint16_t)(sy[0] & 0x7FFFu);
             uint32_t alive = reg ? (1u << n) - 1u : 0u;
             for (;;) {
                 uint32_t e[WREG / 2];
                 {
-                    const uint4 x0 = *(const uint4 *)rkb, x1 = *(const uint4 *)(rkb + 1024);
+                    const uint4 *r4 = (const uint4 *)rk16;
+                    const uint4 x0 = r4[0], x1 = r4[1];
                     e[0] = x0.x; e[1] = x0.y; e[2] = x0.z; e[3] = x0.w; e[4] = x1.x; e[5] = x1.y; e[6] = x1.z; e[7] = x1.w;
                 }
                 // packed-u16 min as a tree (no dependent VOP3P chain)
@@ -617,9 +615,9 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     alive &= ~(1u << jn);
                     const uint32_t L = pl >= 0 ? merge_lookup_c(m, left, minv) & 0xFFFFu : 0xFFFFu;
                     const uint32_t R = q >= 0 ? merge_lookup_c(m, minv, right) & 0xFFFFu : 0xFFFFu;
-                    if (pl >= 0) rk(pl) = (uint16_t)L;
-                    rk(bi) = (uint16_t)R;
-                    rk(jn) = 0xFFFFu;
+                    if (pl >= 0) rk16[pl] = (uint16_t)L;
+                    rk16[bi] = (uint16_t)R;
+                    rk16[jn] = 0xFFFFu;
                 }
             }
             if (act && !reg) {  // long pre-token: merge in LDS

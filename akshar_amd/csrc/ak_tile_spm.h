@@ -38,7 +38,7 @@ namespace ak {
 constexpr int S_BCAP = AK_S_BCAP;           // staged bytes per tile (4 blocks of 4 waves fit a CU's LDS)
 constexpr int S_E = S_BCAP + 2 * T_MAXR + 64;  // entries of V
 constexpr int S_W = S_E + T_MAXR + 16;      // entries of W (chars, "▁", row sentinels)
-constexpr int S_WORDS = (S_BCAP + 32) / 2 < 256 ? (S_BCAP + 32) / 2 : 256;  // words per tile (more: the rows fall back)
+constexpr int S_WORDS = 256;                // words per tile (more: the tile's rows fall back)
 
 constexpr uint16_t W_CODED = 0x8000;  // W entry: 0x8000 | dense code (a char some piece holds), else the code point
 constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: the trie walk stops there)
@@ -54,24 +54,11 @@ __device__ __forceinline__ int4 spm_root_entry(const SpmDev &m, uint32_t c) {
     return e.x == 0 ? make_int4(t, e.y, e.z, e.w) : make_int4(-1, 0, -1, 0);
 }
 
-// windowed lattice (word_dp_win): depth >= 2 lattice edges of a tile, grouped by start, increasing length
-struct SpmEdge {
-    float score;
-    uint32_t v;  // piece id | length << 24
-};
-constexpr int SPM_WIN = 8;    // register window of word_dp_win: the longest piece it handles (code points)
-constexpr int S_ECAP = 288;   // depth >= 2 edges per tile (more: the tile's rows fall back; text has ~0.4 per char)
-constexpr int S_EMAX = 4;     // depth >= 2 edges of one start held by its walk (more: the tile's rows fall back)
-
 struct SpmWaveMem {
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
-    uint16_t v[S_W];                         // V; after pass W: per-position edge words (pass A); after the
-                                             // lattice: nxt (u8 per W position) + word id counts
+    uint16_t v[S_E];                         // V; after pass W: nxt (u8 per W position)
     uint16_t w[S_W];                         // P (pass D1), then W
-    union {
-        float best[S_W];                     // word_dp: Viterbi best score per W position (word-local)
-        SpmEdge edges[S_ECAP];               // word_dp_win: the tile's depth >= 2 lattice edges (pass A)
-    };
+    float best[S_W];                         // Viterbi best score per W position (word-local)
     uint32_t back[S_W];                      // best piece ending here: id << 8 | chars
     uint8_t wrow[S_WORDS];                   // row of each word
     uint8_t fb[T_MAXR];
@@ -86,9 +73,7 @@ struct SpmWaveMem {
     uint64_t ufbm;                           // the unit's rows (bit r - u0) sent to the fallback kernels
 };
 static_assert(S_WORDS * 2 <= S_BCAP + 32, "word starts live in the byte buffer");
-static_assert(S_W + 2 * S_WORDS <= 2 * S_W, "nxt + word id counts live in V");
-static_assert(S_E <= S_W, "V fits its array");
-static_assert(S_ECAP <= 512 && SPM_WIN - 1 <= 7, "edge word: 9-bit offset + 7-bit length mask");
+static_assert(S_W + 2 * S_WORDS <= 2 * S_E, "nxt + word id counts live in V");
 
 // W entry of a normalized char: LDS code table for the hot range, the model's paged map otherwise
 __device__ __forceinline__ uint16_t spm_wcode(const SpmDev &m, const uint16_t *scode, uint32_t cp) {
@@ -137,9 +122,6 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const in
                 if (e.x != 0) break;
                 e.x = t;
             } else {
-#if defined(AK_SPM_EXP) && AK_SPM_EXP == 2
-                break;  // experiment: depth-1 walks only (no global trie loads)
-#endif
                 t = nb + (int)(v & 0x7FFFu);
                 e = m.trie[t];
                 if (e.x != node) break;
@@ -177,186 +159,6 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const in
             }
         }
     }
-}
-
-// Pass A (windowed lattice): every W position's trie walk past its first char, on lanes that take
-// the next position as soon as their walk ends (the wave's dependent L2 chain is ~(positions +
-// probes) / 64 trips, instead of the longest word's sum of walk depths); the depth >= 2 matches of
-// start s go to edges[] (increasing length) and eoff[s] = offset | mask of their lengths (bit
-// len - 2) << 9. Depth 1 stays with the LDS root cache (word_dp_win reads it). Returns false if the
-// tile's edges overflow S_ECAP or a start holds more than S_EMAX (its rows then fall back).
-__device__ __forceinline__ bool spm_walks(SpmWaveMem &M, const SpmDev &m, const int4 *root, uint32_t wlen,
-                                          uint16_t *eoff) {
-    int s = -1;  // current start; -1 idle, -2 no positions left
-    int k = 0, node = -1, nb = 0;
-    uint32_t ne = 0, lmask = 0;
-    float sc0 = 0.0f, sc1 = 0.0f, sc2 = 0.0f, sc3 = 0.0f;
-    uint32_t ev0 = 0, ev1 = 0, ev2 = 0, ev3 = 0;
-    uint32_t cursor = 0, etot = 0;
-    bool over = false;
-    for (;;) {
-        const bool idle = s == -1;
-        const uint64_t IM = w_ballot(idle);
-        if (idle) {
-            const uint32_t c = cursor + w_rank(IM);
-            s = c < wlen ? (int)c : -2;
-            if (s >= 0) {
-                ne = 0;
-                lmask = 0;
-                node = -1;
-                nb = 0;
-                k = s + 1;
-                const uint32_t x = M.w[s];
-                if (x & W_CODED) {
-                    const uint32_t code = x & 0x7FFFu;
-                    if (code < SPM_ROOT_CAP) {
-                        const int4 e = root[code];
-                        node = e.x;
-                        nb = e.x >= 0 ? e.y : 0;
-                    } else {  // a code past the LDS root cache
-                        const int t = m.root_base + (int)code;
-                        const int4 e = m.trie[t];
-                        node = e.x == 0 ? t : -1;
-                        nb = e.x == 0 ? e.y : 0;
-                    }
-                }
-            }
-        }
-        cursor += (uint32_t)w_popc(IM);
-        // one trie probe per walking lane: the next char must be a coded char inside the word
-        uint32_t nx = 0;
-        bool probe = s >= 0 && node >= 0 && nb != 0 && k < (int)wlen && k - s < SPM_WIN;
-        if (probe) {
-            nx = M.w[k];
-            probe = (nx & W_CODED) && nx != m.ws_code;
-        }
-        bool hit = false;
-        if (probe) {
-            const int t = nb + (int)(nx & 0x7FFFu);
-            const int4 e = m.trie[t];
-            hit = e.x == node;
-            if (hit) {
-                node = t;
-                nb = e.y;
-                const int value = e.z;
-                if (value >= 0 && ((value >> 24) & 3) != 2) {  // a piece (not an unused one) ends here
-                    const uint32_t len = (uint32_t)(k - s + 1);
-                    const uint32_t ev = (uint32_t)(value & 0xFFFFFF) | (len << 24);
-                    const float sc = __int_as_float(e.w);
-                    if (ne == 0) { sc0 = sc; ev0 = ev; }
-                    else if (ne == 1) { sc1 = sc; ev1 = ev; }
-                    else if (ne == 2) { sc2 = sc; ev2 = ev; }
-                    else if (ne == 3) { sc3 = sc; ev3 = ev; }
-                    else over = true;
-                    ++ne;
-                    lmask |= 1u << (len - 2);
-                }
-                ++k;
-            }
-        }
-        const bool fin = s >= 0 && !hit;
-        if (w_ballot(fin)) {
-            const uint32_t cnt = fin ? (ne < (uint32_t)S_EMAX ? ne : (uint32_t)S_EMAX) : 0u;
-            uint32_t tot;
-            const uint32_t off = etot + w_exscan(cnt, &tot);
-            if (fin) {
-                if (off + cnt <= (uint32_t)S_ECAP) {
-                    if (cnt > 0) M.edges[off] = SpmEdge{sc0, ev0};
-                    if (cnt > 1) M.edges[off + 1] = SpmEdge{sc1, ev1};
-                    if (cnt > 2) M.edges[off + 2] = SpmEdge{sc2, ev2};
-                    if (cnt > 3) M.edges[off + 3] = SpmEdge{sc3, ev3};
-                } else {
-                    over = true;
-                }
-                eoff[s] = (uint16_t)((off & 511u) | (lmask << 9));
-                s = -1;
-            }
-            etot += tot;
-        }
-        if (!w_ballot(s != -2)) break;
-    }
-    return !w_ballot(over);
-}
-
-// The unigram lattice of one word (W positions [p0, p1)) as word_dp computes it, over the edges of
-// pass A: the best scores and back links of the next SPM_WIN positions live in registers (a window
-// sliding one position per start), so a start costs its edge reads from LDS, not a trie walk; a
-// position leaves the window final and its back link goes to M.back. Returns the best score at p1
-// (the carried base of the row's next word). Same arithmetic, order of arrival and rebase as
-// word_dp / ak_dev.h SpmSink. MARGIN: the smallest gap between a candidate and the stored leader.
-template <bool MARGIN>
-__device__ __forceinline__ float word_dp_win(SpmWaveMem &M, const SpmDev &m, const int4 *root, const uint16_t *eoff,
-                                             int p0, int p1, float base, float &minm) {
-    float win[SPM_WIN + 1];
-    uint32_t bk[SPM_WIN + 1];
-    win[0] = base;
-    bk[0] = 0;
-#pragma unroll
-    for (int j = 1; j <= SPM_WIN; ++j) { win[j] = 0.0f; bk[j] = BK_NONE; }
-    for (int s = p0; s < p1; ++s) {
-        float till = win[0];
-        if (till < -SPM_REBASE || till > SPM_REBASE) {  // sentencepiece's rebase (never at tile sizes)
-#pragma unroll
-            for (int j = 1; j <= SPM_WIN; ++j) win[j] = bk[j] != BK_NONE ? win[j] - till : win[j];
-            till = 0.0f;
-        }
-        const uint32_t x = M.w[s];
-        const uint32_t eo = eoff[s];
-        // length 1: the first char's piece (root cache) or, if there is none, the unk node
-        bool single = false;
-        float c1 = 0.0f;
-        uint32_t b1 = 0;
-        if (x & W_CODED) {
-            const uint32_t code = x & 0x7FFFu;
-            int4 r;
-            if (code < SPM_ROOT_CAP) {
-                r = root[code];
-            } else {
-                const int t = m.root_base + (int)code;
-                r = m.trie[t];
-                r.x = r.x == 0 ? t : -1;
-            }
-            if (r.x >= 0 && r.z >= 0 && ((r.z >> 24) & 3) != 2) {
-                single = true;
-                c1 = __int_as_float(r.w) + till;
-                b1 = ((uint32_t)(r.z & 0xFFFFFF) << 8) | 1u;
-            }
-        }
-        if (!single) {
-            c1 = m.unk_score + till;
-            b1 = ((uint32_t)m.unk_id << 8) | 1u;
-        }
-        // lengths 2..SPM_WIN from pass A, in increasing length (the lattice's order of arrival);
-        // every slot is updated by selects (no per-slot branch)
-        const uint32_t lm = eo >> 9, off = eo & 511u;
-#pragma unroll
-        for (int j = 1; j <= SPM_WIN; ++j) {
-            bool has = true;
-            float c = c1;
-            uint32_t b = b1;
-            if (j > 1) {
-                has = ((lm >> (j - 2)) & 1u) != 0u;
-                const uint32_t idx = off + (uint32_t)__builtin_popcount(lm & ((1u << (j - 2)) - 1u));
-                const SpmEdge ed = has ? M.edges[idx] : SpmEdge{0.0f, 0u};
-                c = ed.score + till;
-                b = ((ed.v & 0xFFFFFFu) << 8) | (uint32_t)j;
-            }
-            const bool fresh = bk[j] == BK_NONE;
-            const bool take = has && (fresh || c > win[j]);
-            if (MARGIN) {
-                const float gap = take ? c - win[j] : win[j] - c;
-                minm = (has && !fresh) ? fminf(minm, gap) : minm;
-            }
-            win[j] = take ? c : win[j];
-            bk[j] = take ? b : bk[j];
-        }
-        M.back[s + 1] = bk[1];  // position s + 1 is final
-#pragma unroll
-        for (int j = 0; j < SPM_WIN; ++j) { win[j] = win[j + 1]; bk[j] = bk[j + 1]; }
-        win[SPM_WIN] = 0.0f;
-        bk[SPM_WIN] = BK_NONE;
-    }
-    return win[0];
 }
 
 // backtrack a solved word into forward links nxt[s] = chars of the piece at s; returns its id
@@ -447,40 +249,9 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     w_sync();
     pc.mark(TP_E);
 
-    // ---------------- pass A (models whose pieces fit the register window): every position's trie
-    // walk, edges into LDS; then pass V: lane per word, Viterbi from base 0 with the running margin
-    // check (word_dp_win over the edges, or word_dp walking the trie itself); a row with a close call
-    // is redone exactly below (pass V2); then the backtrack into forward links + id counts.
+    // ---------------- pass V: lane per word, Viterbi from base 0 with the running margin check
+    // (word_dp); a row with a close call is redone exactly below (pass V2)
     uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
-    uint16_t *eoff = M.v;  // pass A -> V / V2 (the backtrack's nxt + wcnt replace it)
-#ifdef AK_SPM_FORCE_OLD
-    const bool win_path = false;  // development aid: the trie-walking lattice for every model
-#else
-    const bool win_path = m.max_piece_cps <= (uint16_t)SPM_WIN;
-#endif
-    if (win_path && nw) {
-        if (!spm_walks(M, m, root, wlen, eoff)) {  // more edges than the tile holds: its rows fall back
-            if (lane < nr) M.fb[lane] = 1;
-            nw = 0;
-        }
-        w_sync();
-    }
-    pc.mark(TP_P);
-#ifdef AK_SPM_DEBUG
-    if (win_path && r0 == 0 && lane == 0) {
-        printf("AKDBG wlen %u nw %u\n", wlen, nw);
-        for (uint32_t q = 0; q < wlen && q < 40; ++q) {
-            const uint32_t eo = eoff[q];
-            printf("AKDBG pos %u w %04x eoff %04x off %u mask %x", q, (unsigned)M.w[q], eo, eo & 511u, eo >> 9);
-            const uint32_t lm = eo >> 9;
-            for (int i = 0; i < __builtin_popcount(lm); ++i) {
-                const SpmEdge ed = M.edges[(eo & 511u) + i];
-                printf(" [%u len %u id %u sc %f]", (eo & 511u) + i, ed.v >> 24, ed.v & 0xFFFFFFu, ed.score);
-            }
-            printf("\n");
-        }
-    }
-#endif
     for (uint32_t jb = 0; jb < nw; jb += 64) {
         const uint32_t j = jb + (uint32_t)lane;
         const bool act = j < nw;
@@ -488,19 +259,14 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const int p0 = act ? (int)starts[j] : 0;
         const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
         float minm = 3.0e38f;
-#if defined(AK_SPM_EXP) && AK_SPM_EXP == 1
-        for (int i = p0 + 1; i <= p1; ++i) M.back[i] = ((uint32_t)m.unk_id << 8) | 1u;  // experiment: no lattice
-#else
-        if (win_path) word_dp_win<true>(M, m, root, eoff, p0, p1, 0.0f, minm);
-        else word_dp<true>(M, m, root, p0, p1, 0.0f, minm);
-#endif
+        word_dp<true>(M, m, root, p0, p1, 0.0f, minm);
         if (act) {
             // rounding bound of this word (header comment): M = (chars from the row start to the word
             // end + 1) x the largest |score|, at most 1e5 + that score
             const float Mb = fminf((float)(p1 - (int)M.rowpos[row] + 1) * m.abs_score_max, SPM_REBASE + m.abs_score_max) + 1.0f;
             const float tau = (float)(p1 - p0 + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
             if (!(minm > tau)) M.mfail[row] = 1;
-            if (!win_path) wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
+            wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
         }
     }
     w_sync();
@@ -516,29 +282,13 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     const int p0 = (int)starts[j];
                     const int p1 = j + 1 < j1 ? (int)starts[j + 1] : (int)M.rowpos[lane + 1] - 1;
                     float unused = 0.0f;
-                    if (win_path) {
-                        base = word_dp_win<false>(M, m, root, eoff, p0, p1, base, unused);
-                    } else {
-                        word_dp<false>(M, m, root, p0, p1, base, unused);
-                        wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
-                        base = M.best[p1];
-                    }
+                    word_dp<false>(M, m, root, p0, p1, base, unused);
+                    wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
+                    base = M.best[p1];
                 }
             }
             w_sync();
         }
-    }
-    if (win_path) {  // every word's forward links + id count (eoff is dead from here)
-        for (uint32_t jb = 0; jb < nw; jb += 64) {
-            const uint32_t j = jb + (uint32_t)lane;
-            if (j < nw) {
-                const int row = (int)wrow[j];
-                const int p0 = (int)starts[j];
-                const int p1 = (j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1;
-                wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
-            }
-        }
-        w_sync();
     }
     pc.mark(TP_B);
 

@@ -64,12 +64,8 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->sdev.unk_score = m->spm.min_score - 10.0f;
     m->sdev.abs_score_max = m->spm.abs_score_max;
     m->sdev.ws_code = m->spm.ws_code;
-    m->sdev.max_piece_cps = (uint16_t)m->spm.max_piece_cps;
     return m;
 }
-
-// test hook: the longest piece the tile lattice assumes (> SPM_WIN selects word_dp, the trie-walking lattice)
-extern "C" void emu_spm_set_max_piece(void *m, uint32_t cps) { ((EmuModel *)m)->sdev.max_piece_cps = (uint16_t)cps; }
 
 extern "C" void emu_free(void *m) { delete (EmuModel *)m; }
 

@@ -27,7 +27,6 @@ def lib():
         L.emu_spm_create.restype = P
         L.emu_spm_create.argtypes = [ctypes.c_uint32, P, P, P, P, ctypes.c_int32, P]
         L.emu_free.argtypes = [P]
-        L.emu_spm_set_max_piece.argtypes = [P, ctypes.c_uint32]
         L.emu_bpe_tiles.restype = ctypes.c_int64
         L.emu_bpe_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
         L.emu_spm_tiles.restype = ctypes.c_int64

@@ -55,22 +55,9 @@ def test_synthetic_vs_oracle(em, spm_model, kind):
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
 
 
-@pytest.mark.parametrize("kind", [0, 1])
-def test_trie_walking_lattice_vs_oracle(spm_model, kind):
-    """Models whose pieces pass the register window (ak_tile_spm.h SPM_WIN) take word_dp, the
-    lattice that walks the trie itself: forced here on the trained model (its pieces fit)."""
-    from akshar_amd import synth
-    m = emu.Model(spm=spm_model)
-    emu.lib().emu_spm_set_max_piece(m.h, 99)
-    buf, offs = synth.generate(kind, 500, seed=700 + kind)
-    ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
-    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
-    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
-
-
 def test_userdef_model_vs_golden():
-    """A model with USER_DEFINED pieces and pieces past the window (tests/golden/spm_userdef.model,
-    longest 12 chars): the reference's ids (tools/gen_golden_spm_rebase.py)."""
+    """A model with USER_DEFINED pieces (tests/golden/spm_userdef.model, pieces up to 12 chars): the
+    reference's ids (tools/gen_golden_spm_rebase.py)."""
     import gzip
     import json
     import os
