@@ -153,7 +153,6 @@ static int upload_dec(uint8_t *&mem, DecTab &t, const std::vector<uint8_t> &text
 struct ak_spm {
     SpmDev dev;
     int4 *d_trie = nullptr;
-    void *d_d2 = nullptr;  // second-level trie cache: bits, offsets, records (one allocation)
     uint16_t *d_cmap_page = nullptr;
     uint16_t *d_cmap = nullptr;
     uint32_t *d_code_cp = nullptr;
@@ -299,18 +298,6 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.unk_score = t.min_score - 10.0f;
     m->dev.abs_score_max = t.abs_score_max;
     m->dev.ws_code = t.ws_code;
-    {   // the tile lattice's second-level cache (copied into LDS by k_spm_tiles)
-        const size_t nb = t.d2bits.size() * 4, no = t.d2off.size() * 2, nr = t.d2rec.size() * 4;
-        const size_t o_off = nb, o_rec = (nb + no + 15) & ~(size_t)15;
-        HIP_TRY(hipMalloc(&m->d_d2, o_rec + nr + 16));
-        HIP_TRY(hipMemcpy(m->d_d2, t.d2bits.data(), nb, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy((char *)m->d_d2 + o_off, t.d2off.data(), no, hipMemcpyHostToDevice));
-        if (nr) HIP_TRY(hipMemcpy((char *)m->d_d2 + o_rec, t.d2rec.data(), nr, hipMemcpyHostToDevice));
-        m->dev.d2bits = (const uint32_t *)m->d_d2;
-        m->dev.d2off = (const uint16_t *)((char *)m->d_d2 + o_off);
-        m->dev.d2rec = (const int4 *)((char *)m->d_d2 + o_rec);
-        m->dev.d2n = (uint32_t)(t.d2rec.size() / 4);
-    }
     {   // DecodeIds tables: pieces with U+2581 -> ' ', kinds, byte values of <0xXX>
         std::vector<uint8_t> text, kind(n), bv(n, 0);
         std::vector<uint32_t> off(n + 1, 0);
@@ -348,7 +335,6 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
 extern "C" void ak_spm_free(ak_spm *m) {
     if (!m) return;
     (void)hipFree(m->d_trie);
-    (void)hipFree(m->d_d2);
     (void)hipFree(m->d_cmap_page);
     (void)hipFree(m->d_cmap);
     (void)hipFree(m->d_code_cp);

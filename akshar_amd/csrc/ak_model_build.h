@@ -151,17 +151,7 @@ struct SpmTables {
     float min_score = 0;
     float abs_score_max = 0;          // largest |score| one lattice node adds (normal, user defined, unk)
     uint16_t ws_code = 0;             // tile-path W entry of U+2581 (0x8000 | code, or 0x2581 if no piece holds it)
-    // the tile lattice's LDS cache of the trie's second level (ak_tile_spm.h SpmTrieCache): for root
-    // codes c1 < SPM_CACHE_CODES, bit c2 of d2bits[c1 * 4 + c2 / 32] marks a node (c1, c2) with c2 <
-    // SPM_CACHE_CODES; d2off[c1 * 4 + w] is the record of its first such node in word w (0xFFFF: c1 not
-    // cached); d2rec holds the nodes {index, base, value, aux}, at most SPM_D2_CAP of them
-    std::vector<uint32_t> d2bits;
-    std::vector<uint16_t> d2off;
-    std::vector<int> d2rec;
 };
-
-constexpr uint32_t SPM_CACHE_CODES = 128;  // == ak_tile_spm.h SPM_ROOT_CAP
-constexpr uint32_t SPM_D2_CAP = 1024;
 
 constexpr uint32_t SPM_CMAP_PAGES = 0x110000u >> 7;
 
@@ -312,30 +302,6 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
     }
     out.n_nodes = (uint32_t)nn;
     out.root_base = base[0];
-    // second-level cache: the children (codes < SPM_CACHE_CODES) of every root child c1 < SPM_CACHE_CODES
-    out.d2bits.assign(SPM_CACHE_CODES * 4, 0u);
-    out.d2off.assign(SPM_CACHE_CODES * 4, 0xFFFFu);
-    out.d2rec.clear();
-    for (uint32_t c1 = 1; c1 < SPM_CACHE_CODES && (int)c1 <= K; ++c1) {
-        const size_t t1 = (size_t)base[0] + c1;
-        if (t1 >= nn || check[t1] != 0) continue;
-        auto child = [&](uint32_t c2) {
-            const size_t t2 = (size_t)base[t1] + c2;
-            return t2 < nn && check[t2] == (int)t1 ? (int)t2 : -1;
-        };
-        uint32_t cnt = 0;
-        for (uint32_t c2 = 1; c2 < SPM_CACHE_CODES; ++c2) cnt += child(c2) >= 0 ? 1u : 0u;
-        if (out.d2rec.size() / 4 + cnt > SPM_D2_CAP) continue;  // past the cap: this c1 walks in HBM
-        for (uint32_t w = 0; w < 4; ++w) {
-            out.d2off[c1 * 4 + w] = (uint16_t)(out.d2rec.size() / 4);
-            for (uint32_t c2 = 32 * w; c2 < 32 * w + 32; ++c2) {
-                const int t2 = c2 ? child(c2) : -1;
-                if (t2 < 0) continue;
-                out.d2bits[c1 * 4 + w] |= 1u << (c2 & 31u);
-                out.d2rec.insert(out.d2rec.end(), {t2, base[t2], value[t2], aux[t2]});
-            }
-        }
-    }
     out.min_score = min_score;
     // the tile path's rounding bound (ak_tile_spm.h): normal scores, user-defined bonuses and the
     // unk score (min - 10)

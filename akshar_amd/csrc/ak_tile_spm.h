@@ -29,7 +29,6 @@
 // Reference semantics: normalize.py:117-148, tokenizer.py:190-191, cli.py:232-248.
 #pragma once
 #include "ak_tile.h"
-#include "ak_model_build.h"
 
 namespace ak {
 
@@ -45,10 +44,7 @@ constexpr uint16_t W_CODED = 0x8000;  // W entry: 0x8000 | dense code (a char so
 constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: the trie walk stops there)
 constexpr uint16_t W_END = 0x7FFF;
 constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
-constexpr uint32_t SPM_ROOT_CAP = 128;  // trie levels 1-2 of codes below this are cached in LDS (SpmTrieCache)
-
-constexpr uint32_t SPM_D2_LDS = 1024;  // second-level nodes the LDS cache holds (ak_model_build.h SPM_D2_CAP)
-static_assert(SPM_ROOT_CAP == akb::SPM_CACHE_CODES && SPM_D2_LDS == akb::SPM_D2_CAP, "ak_model_build.h cache sizes");
+constexpr uint32_t SPM_ROOT_CAP = 128;  // root children of codes below this are cached in LDS (spm_root_entry)
 
 // LDS cache entry of the trie root's child for code c: {node index or -1, base, value, aux}
 __device__ __forceinline__ int4 spm_root_entry(const SpmDev &m, uint32_t c) {
@@ -56,27 +52,6 @@ __device__ __forceinline__ int4 spm_root_entry(const SpmDev &m, uint32_t c) {
     if (c == 0 || (uint32_t)t >= m.n_nodes) return make_int4(-1, 0, -1, 0);
     const int4 e = m.trie[t];
     return e.x == 0 ? make_int4(t, e.y, e.z, e.w) : make_int4(-1, 0, -1, 0);
-}
-
-// The trie's first two levels in LDS (one copy per block, shared by its waves): a walk's first
-// char reads root[], its second char the bitmap + record of (c1, c2) for codes below SPM_ROOT_CAP;
-// only the third char on goes to HBM / L2 (text walks are mostly 1-2 chars deep).
-struct SpmTrieCache {
-    int4 root[SPM_ROOT_CAP];
-    uint32_t d2bits[SPM_ROOT_CAP * 4];
-    uint16_t d2off[SPM_ROOT_CAP * 4];  // 0xFFFF: c1's second level is not cached
-    int4 d2rec[SPM_D2_LDS];
-};
-
-// threads [tid, tid + stride, ...) of a block fill the cache (the caller synchronizes)
-__device__ __forceinline__ void spm_cache_fill(SpmTrieCache &tc, const SpmDev &m, uint32_t tid, uint32_t stride) {
-    for (uint32_t i = tid; i < SPM_ROOT_CAP; i += stride) tc.root[i] = spm_root_entry(m, i);
-    for (uint32_t i = tid; i < SPM_ROOT_CAP * 4; i += stride) {
-        tc.d2bits[i] = m.d2bits[i];
-        tc.d2off[i] = m.d2off[i];
-    }
-    const uint32_t n = m.d2n < SPM_D2_LDS ? m.d2n : SPM_D2_LDS;
-    for (uint32_t i = tid; i < n; i += stride) tc.d2rec[i] = m.d2rec[i];
 }
 
 struct SpmWaveMem {
@@ -116,11 +91,11 @@ __device__ __forceinline__ uint32_t spm_wcp(const SpmDev &m, uint16_t x) {
 // sentencepiece 0.2.2's arithmetic (float candidates, first arrival wins ties, the rebase of a start
 // whose best leaves [-1e5, 1e5]: ak_dev.h SpmSink). The word owns best / back at (p0, p1] (p0 is the
 // previous word's end node: the base stays in a register). MARGIN: track the smallest gap between a
-// candidate and the stored leader. Inactive lanes pass p1 <= p0. `tc` caches the trie's first two
-// levels in LDS.
+// candidate and the stored leader. Inactive lanes pass p1 <= p0. `root` caches the trie's root
+// children (code -> node) in LDS.
 template <bool MARGIN>
-__device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const SpmTrieCache &tc, int p0, int p1,
-                                        float base, float &minm) {
+__device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const int4 *root, int p0, int p1, float base,
+                                        float &minm) {
     for (int i = p0 + 1; i <= p1; ++i) M.back[i] = BK_NONE;
     int reach = p0;
     for (int s = p0; s < p1; ++s) {
@@ -132,31 +107,22 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const Sp
         }
         bool has_single = false;
         int node = 0, nb = 0;
-        uint32_t c1 = SPM_ROOT_CAP;  // first code of the walk (its second level may be in LDS)
         for (int k = s; k < p1; ++k) {
             const uint32_t v = M.w[k];
             if (!(v & W_CODED)) break;
-            const uint32_t c = v & 0x7FFFu;
             int t;
             int4 e;
-            if (k == s && c < SPM_ROOT_CAP) {  // root child from LDS
-                e = tc.root[c];
+            if (k == s && (v & 0x7FFFu) < SPM_ROOT_CAP) {  // root child from LDS
+                e = root[v & 0x7FFFu];
                 t = e.x;  // root[] holds {node index, base, value, aux}: a miss has index -1
                 if (t < 0) break;
-                c1 = c;
             } else if (k == s) {
-                t = m.root_base + (int)c;
+                t = m.root_base + (int)(v & 0x7FFFu);
                 e = m.trie[t];
                 if (e.x != 0) break;
                 e.x = t;
-            } else if (k == s + 1 && c1 < SPM_ROOT_CAP && c < SPM_ROOT_CAP && tc.d2off[c1 * 4] != 0xFFFFu) {
-                const uint32_t wi = c1 * 4 + (c >> 5);  // second level from LDS
-                const uint32_t bits = tc.d2bits[wi];
-                if (!((bits >> (c & 31u)) & 1u)) break;
-                e = tc.d2rec[tc.d2off[wi] + (uint32_t)__builtin_popcount(bits & ((1u << (c & 31u)) - 1u))];
-                t = e.x;
             } else {
-                t = nb + (int)c;
+                t = nb + (int)(v & 0x7FFFu);
                 e = m.trie[t];
                 if (e.x != node) break;
             }
@@ -213,7 +179,7 @@ __device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &
 
 template <int FLAGS>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
-                        const SpmTrieCache &tc, SpmWaveMem &M, PassClock &pc) {
+                        const int4 *root, SpmWaveMem &M, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
@@ -293,7 +259,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const int p0 = act ? (int)starts[j] : 0;
         const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
         float minm = 3.0e38f;
-        word_dp<true>(M, m, tc, p0, p1, 0.0f, minm);
+        word_dp<true>(M, m, root, p0, p1, 0.0f, minm);
         if (act) {
             // rounding bound of this word (header comment): M = (chars from the row start to the word
             // end + 1) x the largest |score|, at most 1e5 + that score
@@ -316,7 +282,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     const int p0 = (int)starts[j];
                     const int p1 = j + 1 < j1 ? (int)starts[j + 1] : (int)M.rowpos[lane + 1] - 1;
                     float unused = 0.0f;
-                    word_dp<false>(M, m, tc, p0, p1, base, unused);
+                    word_dp<false>(M, m, root, p0, p1, base, unused);
                     wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
                     base = M.best[p1];
                 }
@@ -402,7 +368,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
 }
 
 template <int FLAGS>
-__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, const SpmTrieCache &tc,
+__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, const int4 *root,
                                SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
@@ -417,7 +383,7 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
             M.ufbm = 0;
         }
         w_sync();
-        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, tc, M, pc);
+        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, root, M, pc);
         if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
     }
     pc.flush(ta.passprof);

@@ -64,10 +64,6 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->sdev.unk_score = m->spm.min_score - 10.0f;
     m->sdev.abs_score_max = m->spm.abs_score_max;
     m->sdev.ws_code = m->spm.ws_code;
-    m->sdev.d2bits = m->spm.d2bits.data();
-    m->sdev.d2off = m->spm.d2off.data();
-    m->sdev.d2rec = (const int4 *)m->spm.d2rec.data();
-    m->sdev.d2n = (uint32_t)(m->spm.d2rec.size() / 4);
     return m;
 }
 
@@ -259,8 +255,8 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     static uint2 fast[FAST_N];
     static uint32_t hot_tab[HOT_N];
     static uint16_t scode[HOT_N];
-    static SpmTrieCache tc;
-    spm_cache_fill(tc, m->sdev, 0, 1);
+    static int4 root[SPM_ROOT_CAP];
+    for (uint32_t i = 0; i < SPM_ROOT_CAP; ++i) root[i] = spm_root_entry(m->sdev, i);
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
     for (uint32_t i = 0; i < HOT_N; ++i) {
         const uint32_t cp = hot_cp(i);
@@ -288,7 +284,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         th.emplace_back([&, lane] {
             t_lane = lane;
             t_wave = &W;
-            spm_tiles_wave<3>(ta, hot_tab, scode, tc, *M, 0, 1);
+            spm_tiles_wave<3>(ta, hot_tab, scode, root, *M, 0, 1);
         });
     for (auto &x : th) x.join();
     delete M;
