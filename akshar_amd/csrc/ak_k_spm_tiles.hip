@@ -23,9 +23,7 @@ template <int FLAGS>
 __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
-    __shared__ int4 root[SPM_ROOT_CAP];
     __shared__ SpmWaveMem wm[SPM_TILE_BLOCK / 64];
-    for (uint32_t i = threadIdx.x; i < SPM_ROOT_CAP; i += SPM_TILE_BLOCK) root[i] = spm_root_entry(ta.ra.spm, i);
     for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
         const uint32_t cp = hot_cp(i);
         hot_tab[i] = hot_of(prop_global(cp));
@@ -34,7 +32,7 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     }
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
-    spm_tiles_wave<FLAGS>(ta, hot_tab, scode, root, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
+    spm_tiles_wave<FLAGS>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
                           gridDim.x * (SPM_TILE_BLOCK / 64));
 }
 

@@ -5,8 +5,9 @@
 //   W  elongation collapse + the identity normalizer's whitespace rule (strip, collapse, dummy
 //      prefix, ' ' -> "▁") + the SPM code of every char, compacted into W; word starts ("▁")
 //      listed with their rows
-//   V  lane per "▁word": the unigram Viterbi over the word (the code-point trie in HBM / L2,
-//      best / back per position in LDS), backtrack into forward links
+//   V  lane per "▁word": the unigram Viterbi over the word as one flattened loop of trie steps
+//      (word_dp_flat: the code-point trie in HBM / L2, best / back per position in LDS),
+//      backtrack into forward links
 //   F  ids (pieces; byte fallback for unk chars) into the unit's staging run (ak_tile.h: the rows
 //      of a 64-row unit back to back, fallback rows in a second staging half), per-row counts
 // Words run in parallel from base 0 instead of from the row's carried float score. The carried base
@@ -38,21 +39,12 @@ namespace ak {
 constexpr int S_BCAP = AK_S_BCAP;           // staged bytes per tile (4 blocks of 4 waves fit a CU's LDS)
 constexpr int S_E = S_BCAP + 2 * T_MAXR + 64;  // entries of V
 constexpr int S_W = S_E + T_MAXR + 16;      // entries of W (chars, "▁", row sentinels)
-constexpr int S_WORDS = 256;                // words per tile (more: the tile's rows fall back)
+constexpr int S_WORDS = (S_BCAP + 32) / 2 >= 256 ? 256 : 128;  // words per tile (more: the tile's rows fall back)
 
 constexpr uint16_t W_CODED = 0x8000;  // W entry: 0x8000 | dense code (a char some piece holds), else the code point
 constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: the trie walk stops there)
 constexpr uint16_t W_END = 0x7FFF;
 constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
-constexpr uint32_t SPM_ROOT_CAP = 128;  // root children of codes below this are cached in LDS (spm_root_entry)
-
-// LDS cache entry of the trie root's child for code c: {node index or -1, base, value, aux}
-__device__ __forceinline__ int4 spm_root_entry(const SpmDev &m, uint32_t c) {
-    const int t = m.root_base + (int)c;
-    if (c == 0 || (uint32_t)t >= m.n_nodes) return make_int4(-1, 0, -1, 0);
-    const int4 e = m.trie[t];
-    return e.x == 0 ? make_int4(t, e.y, e.z, e.w) : make_int4(-1, 0, -1, 0);
-}
 
 struct SpmWaveMem {
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
@@ -91,10 +83,9 @@ __device__ __forceinline__ uint32_t spm_wcp(const SpmDev &m, uint16_t x) {
 // sentencepiece 0.2.2's arithmetic (float candidates, first arrival wins ties, the rebase of a start
 // whose best leaves [-1e5, 1e5]: ak_dev.h SpmSink). The word owns best / back at (p0, p1] (p0 is the
 // previous word's end node: the base stays in a register). MARGIN: track the smallest gap between a
-// candidate and the stored leader. Inactive lanes pass p1 <= p0. `root` caches the trie's root
-// children (code -> node) in LDS.
+// candidate and the stored leader. Inactive lanes pass p1 <= p0.
 template <bool MARGIN>
-__device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const int4 *root, int p0, int p1, float base,
+__device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, int p0, int p1, float base,
                                         float &minm) {
     for (int i = p0 + 1; i <= p1; ++i) M.back[i] = BK_NONE;
     int reach = p0;
@@ -112,11 +103,7 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const in
             if (!(v & W_CODED)) break;
             int t;
             int4 e;
-            if (k == s && (v & 0x7FFFu) < SPM_ROOT_CAP) {  // root child from LDS
-                e = root[v & 0x7FFFu];
-                t = e.x;  // root[] holds {node index, base, value, aux}: a miss has index -1
-                if (t < 0) break;
-            } else if (k == s) {
+            if (k == s) {
                 t = m.root_base + (int)(v & 0x7FFFu);
                 e = m.trie[t];
                 if (e.x != 0) break;
@@ -161,6 +148,90 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, const in
     }
 }
 
+// One lattice update: candidate `cand` for W position ee (piece `id` of `len` chars), sentencepiece's
+// rule (first arrival wins ties); MARGIN tracks the gap to the stored leader.
+template <bool MARGIN>
+__device__ __forceinline__ void spm_relax(SpmWaveMem &M, int ee, float cand, uint32_t id, uint32_t len, float &minm) {
+    const uint32_t bk = M.back[ee];
+    const float bb = M.best[ee];
+    const bool none = bk == BK_NONE;
+    const bool take = none || cand > bb;
+    if (MARGIN && !none) minm = fminf(minm, take ? cand - bb : bb - cand);
+    if (take) {
+        M.best[ee] = cand;
+        M.back[ee] = (id << 8) | len;
+    }
+}
+
+// Pass V's lattice of one word (W positions [p0, p1), "▁" at p0) from base 0, the same arithmetic and
+// decisions as word_dp<true> with a flattened loop: one iteration = one trie step of one start s on
+// every lane, so the wave runs max over lanes of sum_s (walk(s) + 1) iterations instead of, for each
+// s in turn, the longest walk any lane has at it. A walk ends at a failed probe, at the word end, or
+// before a char no piece holds (no probe spent on those two). The node is loaded only by the lanes
+// that step; the rare branches (a start with no single-char piece, a rebase) sit behind ballots.
+// back[] of (p0, p1] must be BK_NONE on entry. Inactive lanes pass p1 <= p0. Returns the smallest
+// gap between a candidate and the stored leader (the margin).
+__device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, int p0, int p1) {
+    float minm = 3.0e38f;
+    bool act = p0 < p1;
+    int s = p0, k = p0, node = 0, nb = m.root_base, reach = p0;
+    float till = 0.0f;
+    bool hs = false;
+    uint32_t v = act ? M.w[p0] : 0u;
+    while (w_ballot(act)) {
+        const bool coded = act && (v & W_CODED);
+        const int t = coded ? nb + (int)(v & 0x7FFFu) : 0;
+        int4 e = make_int4(-1, 0, -1, 0);
+        if (coded) e = m.trie[t];
+        const bool ok = coded && e.x == node;
+        const int value = e.z;
+        const bool hv = ok && value >= 0 && ((value >> 24) & 3) != 2;
+        const int ee = k + 1;
+        if (hv) {
+            spm_relax<true>(M, ee, __int_as_float(e.w) + till, (uint32_t)(value & 0xFFFFFF), (uint32_t)(ee - s), minm);
+            reach = ee > reach ? ee : reach;
+            hs = hs || k == s;
+        }
+        if (ok) {
+            node = t;
+            nb = e.y;
+            k = ee;
+        }
+        const uint32_t vn = M.w[k < S_W ? k : S_W - 1];
+        const bool end = act && (!ok || k >= p1 || !(vn & W_CODED));
+        if (w_ballot(end && !hs)) {  // rare: no piece of exactly the first char -> an unk node
+            if (end && !hs) {
+                reach = s + 1 > reach ? s + 1 : reach;
+                spm_relax<true>(M, s + 1, m.unk_score + till, (uint32_t)m.unk_id, 1u, minm);
+            }
+        }
+        const int sn = s + 1;
+        const bool fin = end && sn >= p1;
+        const bool next = end && !fin;
+        const int sc = next ? sn : p0;
+        const float tn = M.best[sc];
+        const uint32_t vs = M.w[sc];
+        if (next) {
+            s = sn;
+            k = sn;
+            node = 0;
+            nb = m.root_base;
+            hs = false;
+            till = tn;
+        }
+        v = next ? vs : vn;
+        act = act && !fin;
+        if (w_ballot(next && (till < -SPM_REBASE || till > SPM_REBASE))) {  // rare: sentencepiece's rebase
+            if (next && (till < -SPM_REBASE || till > SPM_REBASE)) {
+                for (int q = s + 1; q <= reach; ++q)
+                    if (M.back[q] != BK_NONE) M.best[q] -= till;
+                till = 0.0f;
+            }
+        }
+    }
+    return minm;
+}
+
 // backtrack a solved word into forward links nxt[s] = chars of the piece at s; returns its id
 // count (byte fallback: one id per UTF-8 byte of an unk char)
 __device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &m, uint8_t *nxt, int p0, int p1) {
@@ -179,7 +250,7 @@ __device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &
 
 template <int FLAGS>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
-                        const int4 *root, SpmWaveMem &M, PassClock &pc) {
+                        SpmWaveMem &M, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
@@ -252,14 +323,20 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     // ---------------- pass V: lane per word, Viterbi from base 0 with the running margin check
     // (word_dp); a row with a close call is redone exactly below (pass V2)
     uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
+    for (uint32_t i = (uint32_t)lane; i < wlen; i += 64) M.back[i] = BK_NONE;  // word_dp_flat's entry state
+    w_sync();
     for (uint32_t jb = 0; jb < nw; jb += 64) {
         const uint32_t j = jb + (uint32_t)lane;
         const bool act = j < nw;
         const int row = act ? (int)wrow[j] : 0;
         const int p0 = act ? (int)starts[j] : 0;
         const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
+#ifdef AK_SPM_NESTED_DP  // development aid: the nested-loop lattice for A/B
         float minm = 3.0e38f;
-        word_dp<true>(M, m, root, p0, p1, 0.0f, minm);
+        word_dp<true>(M, m, p0, p1, 0.0f, minm);
+#else
+        const float minm = word_dp_flat(M, m, p0, p1);
+#endif
         if (act) {
             // rounding bound of this word (header comment): M = (chars from the row start to the word
             // end + 1) x the largest |score|, at most 1e5 + that score
@@ -282,7 +359,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     const int p0 = (int)starts[j];
                     const int p1 = j + 1 < j1 ? (int)starts[j + 1] : (int)M.rowpos[lane + 1] - 1;
                     float unused = 0.0f;
-                    word_dp<false>(M, m, root, p0, p1, base, unused);
+                    word_dp<false>(M, m, p0, p1, base, unused);
                     wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
                     base = M.best[p1];
                 }
@@ -368,8 +445,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
 }
 
 template <int FLAGS>
-__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, const int4 *root,
-                               SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
+__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
     // static stride over units of TILE_UNIT rows (units are near-equal); inside a unit, each tile
@@ -383,7 +459,7 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
             M.ufbm = 0;
         }
         w_sync();
-        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, root, M, pc);
+        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, M, pc);
         if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
     }
     pc.flush(ta.passprof);

@@ -255,8 +255,6 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     static uint2 fast[FAST_N];
     static uint32_t hot_tab[HOT_N];
     static uint16_t scode[HOT_N];
-    static int4 root[SPM_ROOT_CAP];
-    for (uint32_t i = 0; i < SPM_ROOT_CAP; ++i) root[i] = spm_root_entry(m->sdev, i);
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
     for (uint32_t i = 0; i < HOT_N; ++i) {
         const uint32_t cp = hot_cp(i);
@@ -284,7 +282,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         th.emplace_back([&, lane] {
             t_lane = lane;
             t_wave = &W;
-            spm_tiles_wave<3>(ta, hot_tab, scode, root, *M, 0, 1);
+            spm_tiles_wave<3>(ta, hot_tab, scode, *M, 0, 1);
         });
     for (auto &x : th) x.join();
     delete M;
