@@ -82,6 +82,18 @@ template <class T>
 int copy_staged(const T *stage, uint64_t stage_cap, const uint64_t *offs, const uint64_t *out_offs, uint64_t n, T *out,
                 uint64_t cap, uint32_t mul, uint32_t add, hipStream_t st);
 int num_cus();
+
+// Grid of a fallback-row kernel: as many blocks as stay resident on every CU (its rows run one lane
+// each, sequential and latency-bound, so resident lanes are the lever); the occupancy is cached.
+template <class K>
+unsigned resident_grid(K kernel, int block, int &cache) {
+    if (!cache) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, block, 0) != hipSuccess) b = 1;
+        cache = b > 1 ? b : 1;
+    }
+    return (unsigned)num_cus() * (unsigned)cache;
+}
 // unit-run staging (tile BPE, row tiles): per-unit fallback masks, and the streaming unit copy
 int ws_unit_fb_reserve(AkWs *w, uint64_t nunits);
 template <class T>

@@ -349,7 +349,8 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
-    k_tile_fb<3><<<(unsigned)num_cus(), FB_BLOCK, 0, st>>>(tfb);
+    static int fb_bpc = 0;
+    k_tile_fb<3><<<resident_grid(k_tile_fb<3>, FB_BLOCK, fb_bpc), FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;
     ra.counts = w->counts;
     ra.err = w->ctr + CTR_ERR;

@@ -144,7 +144,8 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
-    k_spm_tile_fb<3><<<(unsigned)num_cus() * 2, SPM_FB_BLOCK, 0, st>>>(tfb);
+    static int fb_bpc = 0;
+    k_spm_tile_fb<3><<<resident_grid(k_spm_tile_fb<3>, SPM_FB_BLOCK, fb_bpc), SPM_FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;
     ra.counts = w->counts;
     ra.err = w->ctr + CTR_ERR;

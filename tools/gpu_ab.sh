@@ -10,3 +10,7 @@ rm -f gpurun_out/ab.jsonl
 bash tools/ab_run.sh default "$@"
 bash tools/ab_run.sh default "$@"
 cat gpurun_out/ab.jsonl
+if [ -n "$AB_FALLBACK" ]; then
+  timeout -k 10 300 python -u tools/fallback_realism.py > gpurun_out/fallback_realism.json 2> gpurun_out/fallback_realism.err
+  tail -c 400 gpurun_out/fallback_realism.json
+fi
