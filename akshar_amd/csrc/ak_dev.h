@@ -563,38 +563,6 @@ __device__ __forceinline__ uint32_t merge_lookup_c(const BpeDev &m, uint32_t a, 
     return v == 0x7FFFu ? 0xFFFFu : v;
 }
 
-// Two independent compact-table lookups with both first-choice loads in flight before either is
-// waited on (one L2 round trip for the pair; the rare second-choice probes follow behind a ballot).
-// A lookup with ok == false returns 0xFFFF (its load reads an arbitrary slot). No wave primitives:
-// callable from divergent code.
-__device__ __forceinline__ void merge_lookup_c2(const BpeDev &m, uint32_t a0, uint32_t b0, bool ok0, uint32_t a1,
-                                                uint32_t b1, bool ok1, uint32_t &r0, uint32_t &r1) {
-    const uint32_t k0 = (a0 << 16) | b0, k1 = (a1 << 16) | b1;
-    const uint32_t lowmask = (1u << m.ctab_shift) - 1u;
-    const char *base = (const char *)m.merge_ctab;
-    const uint32_t p0 = k0 * 0x9E3779B1u, p1 = k1 * 0x9E3779B1u;
-    const uint32_t e0 = *(const uint32_t *)(base + ((p0 >> m.ctab_shift) << 2));
-    const uint32_t e1 = *(const uint32_t *)(base + ((p1 >> m.ctab_shift) << 2));
-    const bool h0 = ((e0 ^ ((p0 & lowmask) << 17)) & 0xFFFE8000u) == 0u;
-    const bool h1 = ((e1 ^ ((p1 & lowmask) << 17)) & 0xFFFE8000u) == 0u;
-    uint32_t v0 = h0 ? e0 & 0x7FFFu : 0x7FFFu, v1 = h1 ? e1 & 0x7FFFu : 0x7FFFu;
-    const bool s0 = ok0 && !h0 && (e0 & 0x10000u), s1 = ok1 && !h1 && (e1 & 0x10000u);
-    if (s0 || s1) {  // rare: a key that lives at its second choice
-        if (s0) {
-            const uint32_t q = (k0 ^ 0x5BD1E995u) * 0x85EBCA77u;
-            const uint32_t f = *(const uint32_t *)(base + ((q >> m.ctab_shift) << 2));
-            if (((f ^ (((q & lowmask) << 17) | 0x8000u)) & 0xFFFE8000u) == 0u) v0 = f & 0x7FFFu;
-        }
-        if (s1) {
-            const uint32_t q = (k1 ^ 0x5BD1E995u) * 0x85EBCA77u;
-            const uint32_t f = *(const uint32_t *)(base + ((q >> m.ctab_shift) << 2));
-            if (((f ^ (((q & lowmask) << 17) | 0x8000u)) & 0xFFFE8000u) == 0u) v1 = f & 0x7FFFu;
-        }
-    }
-    r0 = ok0 && v0 != 0x7FFFu ? v0 : 0xFFFFu;
-    r1 = ok1 && v1 != 0x7FFFu ? v1 : 0xFFFFu;
-}
-
 __device__ __forceinline__ int bpe_merge_word(const BpeDev &m, uint16_t *w, uint32_t *pr, int n) {
     for (int i = 0; i + 1 < n; ++i) pr[i] = merge_lookup(m, w[i], w[i + 1]);
     while (n > 1) {

@@ -45,11 +45,16 @@ template <int FLAGS>
 __global__ __launch_bounds__(SPM_FB_BLOCK) void k_spm_tile_fb(TileArgs ta) {
     __shared__ uint2 fast[FAST_N];
     __shared__ uint16_t sfast[1];
+#if AK_SPM_FB_SCRATCH
+    uint32_t lanebuf[SPM_FB_LANE_U32];
+    uint32_t *b = lanebuf;
+#else
     __shared__ uint32_t lanebuf[SPM_FB_BLOCK * SPM_FB_LANE_U32];
+    uint32_t *b = lanebuf + threadIdx.x * SPM_FB_LANE_U32;
+#endif
     const uint32_t nl = *ta.fb_count;
     if (nl == 0) return;  // uniform: the common case
     stage_tables(fast, sfast, nullptr, false);
-    uint32_t *b = lanebuf + threadIdx.x * SPM_FB_LANE_U32;
     Scratch sc;
     small_scratch(sc, b, b + FAST_SEG, b + 2 * FAST_SEG, b + 6 * FAST_SEG, FAST_SEG);
     b += 10 * FAST_SEG;

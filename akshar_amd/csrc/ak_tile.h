@@ -45,9 +45,6 @@ constexpr int WREG = 16;                // pre-tokens up to WREG-1 symbols take 
 // a tile with more (never in text: 240 two-symbol pre-tokens in 768 bytes) sends its rows to the
 // fallback kernels
 constexpr int T_SCAP = 240;
-#ifndef AK_BPE_PAIR_LOOKUP
-#define AK_BPE_PAIR_LOOKUP 1
-#endif
 
 struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
@@ -611,16 +608,6 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     const int pl = below ? 31 - __builtin_clz(below) : -1;
                     const uint32_t aj = jn + 1 < 32 ? alive >> (jn + 1) : 0u;
                     const int q = aj ? jn + 1 + __builtin_ctz(aj) : -1;
-#if AK_BPE_PAIR_LOOKUP
-                    // both neighbours read unconditionally (clamped), both lookups in flight at once
-                    const uint32_t left = M.w[st + (pl >= 0 ? pl : bi)];
-                    const uint32_t right = M.w[st + (q >= 0 ? q : jn)];
-                    M.w[st + bi] = (uint16_t)minv;
-                    M.w[st + jn] = V_DEAD;
-                    alive &= ~(1u << jn);
-                    uint32_t L, R;
-                    merge_lookup_c2(m, left, minv, pl >= 0, minv, right, q >= 0, L, R);
-#else
                     const uint32_t left = pl >= 0 ? M.w[st + pl] : 0u;
                     const uint32_t right = q >= 0 ? M.w[st + q] : 0u;
                     M.w[st + bi] = (uint16_t)minv;
@@ -628,7 +615,6 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     alive &= ~(1u << jn);
                     const uint32_t L = pl >= 0 ? merge_lookup_c(m, left, minv) & 0xFFFFu : 0xFFFFu;
                     const uint32_t R = q >= 0 ? merge_lookup_c(m, minv, right) & 0xFFFFu : 0xFFFFu;
-#endif
                     if (pl >= 0) rk16[pl] = (uint16_t)L;
                     rk16[bi] = (uint16_t)R;
                     rk16[jn] = 0xFFFFu;
