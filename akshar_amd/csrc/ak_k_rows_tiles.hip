@@ -39,11 +39,11 @@ template <int OPS>
 __global__ __launch_bounds__(RT_FB_BLOCK) void k_rows_tile_fb(TileArgs ta, RowsOut o, uint32_t *err) {
     __shared__ uint2 fast[FAST_N];
     __shared__ uint16_t sfast[1];
-    __shared__ uint32_t lanebuf[RT_FB_BLOCK * RT_FB_LANE_U32];
+    uint32_t lanebuf[RT_FB_LANE_U32];  // scratch: the `fast` table is the block's only LDS, so twice
+    uint32_t *b = lanebuf;              // the blocks stay resident (fuzz rows 1.45x, profiles/r03e_*)
     const uint32_t nl = *ta.fb_count;
     if (nl == 0) return;  // uniform: the common case
     stage_tables(fast, sfast, nullptr, false);
-    uint32_t *b = lanebuf + threadIdx.x * RT_FB_LANE_U32;
     Scratch sc;
     small_scratch(sc, b, b + FAST_SEG, b + 2 * FAST_SEG, b + 6 * FAST_SEG, FAST_SEG);
     for (uint32_t i = blockIdx.x * RT_FB_BLOCK + threadIdx.x; i < nl; i += gridDim.x * RT_FB_BLOCK) {

@@ -37,21 +37,18 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
 }
 
 // fallback rows with the fast row kernel's buffer sizes, straight into the row's tile slot. The
-// lattice and NFC buffers of each lane live in LDS (private arrays would be scratch: one HBM round
-// trip per access, serialized per lane).
+// lattice and NFC buffers of each lane are a private array, i.e. scratch (cached, lane-interleaved):
+// in LDS (1.1 KB per lane) they held the kernel to one wave per CU; as scratch eight 64-lane blocks
+// stay resident per CU (the `fast` table is the only LDS), 3-4x faster on fallback-heavy sets
+// (profiles/r03e_fallback_realism.json).
 constexpr int SPM_FB_LANE_U32 = 2 * FAST_SEG + 8 * FAST_SEG + FAST_VCAP + 3 * (FAST_VCAP + 1);
 
 template <int FLAGS>
 __global__ __launch_bounds__(SPM_FB_BLOCK) void k_spm_tile_fb(TileArgs ta) {
     __shared__ uint2 fast[FAST_N];
     __shared__ uint16_t sfast[1];
-#if AK_SPM_FB_SCRATCH
-    uint32_t lanebuf[SPM_FB_LANE_U32];
+    uint32_t lanebuf[SPM_FB_LANE_U32];  // scratch (see above)
     uint32_t *b = lanebuf;
-#else
-    __shared__ uint32_t lanebuf[SPM_FB_BLOCK * SPM_FB_LANE_U32];
-    uint32_t *b = lanebuf + threadIdx.x * SPM_FB_LANE_U32;
-#endif
     const uint32_t nl = *ta.fb_count;
     if (nl == 0) return;  // uniform: the common case
     stage_tables(fast, sfast, nullptr, false);

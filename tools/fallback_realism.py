@@ -1,6 +1,6 @@
 """How often realistic rows leave the tile kernels for the sequential fallback,
-and what that costs: for each input set, BPE and SentencePiece encode on the GPU with the tile
-path, the number of rows the tile kernel sent to the fallback kernels, and MB/s of the whole encode
+and what that costs: for each input set, BPE and SentencePiece encode and the fused analyze
+(normalize + segment + switches) on the GPU with the tile path, the number of rows the tile kernel sent to the fallback kernels, and MB/s of the whole encode
 (kernel time from the library's HIP events) next to the synthetic bench corpus.
 
 Sets (each replicated to --rows rows so the launch is full-size): the reference's data/corpus.txt
@@ -38,13 +38,14 @@ def sets():
 
 
 def measure(model, gb, go, nbytes, reps=3):
-    model.encode_batch(gb, go, nbytes=nbytes)
+    fn = (lambda: engine.analyze_batch(gb, go)) if model is None else (lambda: model.encode_batch(gb, go, nbytes=nbytes))
+    fn()
     torch.cuda.synchronize()
     fb = engine.fallback_rows()
     engine.profile_enable(True)
     engine.profile_reset()
     for _ in range(reps):
-        model.encode_batch(gb, go, nbytes=nbytes)
+        fn()
     torch.cuda.synchronize()
     prof = engine.profile_read()
     engine.profile_enable(False)
@@ -71,8 +72,9 @@ def main():
         else:
             gb, go = engine.pack(texts)
             nbytes = int(go[-1].item())
-        res = {"bytes": nbytes, "bpe": measure(bpe, gb, go, nbytes), "spm": measure(spm, gb, go, nbytes)}
-        for k in ("bpe", "spm"):
+        res = {"bytes": nbytes, "bpe": measure(bpe, gb, go, nbytes), "spm": measure(spm, gb, go, nbytes),
+               "analyze": measure(None, gb, go, nbytes)}
+        for k in ("bpe", "spm", "analyze"):
             res[k]["fallback_rate"] = round(res[k]["fallback_rows"] / args.rows, 5)
         out["sets"][name] = res
         print(name, json.dumps(res), file=sys.stderr, flush=True)
