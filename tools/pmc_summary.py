@@ -41,13 +41,22 @@ def op_summary(src, tag, match, rows, nbytes):
     out = os.path.join(ROOT, "profiles")
     cls, kname = KERNEL_CLASS[match]
     allc, meta = {}, {}
-    for name in ("fetch", "write", "sq1", "sq2"):
+    for name in ("fetch", "write", "sq1", "sq2", "mem", "tcp"):
         p = os.path.join(src, name, name + "_counter_collection.csv")
         if os.path.exists(p):
             c, m = counters(p, match)
             allc.update(c)
             meta = meta or m
     rd = allc["FETCH_SIZE"] * 1024 * 2
+    # vector-memory pipe: TA / TD busy per CU over the kernel's cycles per XCD (GRBM_GUI_ACTIVE sums
+    # the 8 XCDs; 256 CUs each with one TA and one TD)
+    gui = allc.get("GRBM_GUI_ACTIVE", 0) / 8.0
+    pipe = {}
+    if gui > 0:
+        pipe = {"ta_busy_frac": round(allc.get("TA_TA_BUSY_sum", 0) / 256.0 / gui, 3),
+                "td_busy_frac": round(allc.get("TD_TD_BUSY_sum", 0) / 256.0 / gui, 3)}
+    if allc.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
+        pipe["l1_hit_frac"] = round(1.0 - allc.get("TCP_TCC_READ_REQ_sum", 0) / allc["TCP_TOTAL_CACHE_ACCESSES_sum"], 3)
     wr = allc["WRITE_SIZE"] * 1024
     rec = {"kernel": kname, "kernel_class": cls, "rows": rows, "bytes": nbytes,
            "command": "tools/pmc_op.sh (rocprofv3 --pmc, one run per counter group) over tools/prof_op.py, one launch "
@@ -57,6 +66,7 @@ def op_summary(src, tag, match, rows, nbytes):
            "salu_per_row": round(allc.get("SQ_INSTS_SALU", 0) / rows, 1),
            "lds_per_row": round(allc.get("SQ_INSTS_LDS", 0) / rows, 1),
            "wait_frac": round(allc.get("SQ_WAIT_ANY", 0) / max(allc.get("SQ_WAVE_CYCLES", 1), 1), 3),
+           "vmem_rd_per_row": round(allc.get("SQ_INSTS_VMEM_RD", 0) / rows, 1), **pipe,
            "note": "read = FETCH_SIZE x 1024 x 2 (gfx950 half-count correction for 16-B/lane streaming reads), "
                    "write = WRITE_SIZE x 1024"}
     json.dump(rec, open(os.path.join(out, "%s_%s_pmc.json" % (tag, cls)), "w"), indent=1)
