@@ -295,9 +295,9 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     rc = ws_stage_reserve(w, 2 * half, st);
     if (rc) return rc;
     const int R = w->tile_rows;
-    const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the static wave stride
+    const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the work queue (ak_tile.h tile_first_unit)
     if ((rc = ws_unit_fb_reserve(w, ntiles))) return rc;
-    if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
+    if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count, [3] the unit queue
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
@@ -322,6 +322,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     ta.fb_count = w->tile_misc;
     ta.err = w->tile_misc + 1;
     ta.fb2_count = w->tile_misc + 2;
+    ta.next_unit = w->tile_misc + 3;
     ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.rows = R;
@@ -333,7 +334,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     }
     ta.fb2_list = w->fb2;
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 3 * 4, st));
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit

@@ -88,7 +88,7 @@ template <int OPS>
 static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsOut &ofb, const RowsOutFinal &f,
                       hipStream_t st) {
     int rc;
-    if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count
+    if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count, [3] the unit queue
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
@@ -119,12 +119,13 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     ta.err = w->tile_misc + 1;
     ta.fb2_list = w->fb2;
     ta.fb2_count = w->tile_misc + 2;
+    ta.next_unit = w->tile_misc + 3;
     ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.unit_fb = w->unit_fb;
     ta.rows = std::min(w->tile_rows, T_MAXR);
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 3 * 4, st));
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = RT_BLOCK / 64;
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)num_cus() * g_rt_bpc[OPS]);

@@ -68,9 +68,39 @@ struct TileArgs {
     uint32_t *err;        // set if an id fell outside its row's slot (never: bytes + 2 bound)
     uint64_t *unit_fb;    // BPE: per 64-row unit, the mask of its rows sent to the fallback kernels
     uint64_t *passprof;   // optional: device cycles per pass, summed over waves (T_NPASS entries)
+    uint32_t *next_unit;  // the work queue: next unit to take (zeroed before the launch)
     uint64_t ntiles;
     int rows;             // R
 };
+
+#ifndef AK_TILE_DYNAMIC
+#define AK_TILE_DYNAMIC 1
+#endif
+// The next 64-row unit for this wave. Dynamic: lane 0 takes it from the launch's work queue with one
+// agent-scope atomic (a unit is ~0.8 ms of one wave's work at cfg4, so the atomic is free) and the
+// wave leaves once the queue passes ntiles; units vary in cost and so do waves' shares of the
+// SIMDs, which a static stride cannot absorb. Static (AK_TILE_DYNAMIC=0): wave_gid, + nwaves.
+__device__ __forceinline__ uint64_t tile_first_unit(uint32_t *q, uint32_t wave_gid) {
+#if AK_TILE_DYNAMIC
+    (void)wave_gid;
+    uint32_t u = 0;
+    if (w_lane() == 0) u = w_atomic_add32(q, 1u);
+    return (uint64_t)w_bcast(u, 0);
+#else
+    (void)q;
+    return wave_gid;
+#endif
+}
+__device__ __forceinline__ uint64_t tile_next_unit(uint32_t *q, uint64_t t, uint32_t nwaves) {
+#if AK_TILE_DYNAMIC
+    (void)t;
+    (void)nwaves;
+    return tile_first_unit(q, 0);
+#else
+    (void)q;
+    return t + nwaves;
+#endif
+}
 
 // pass profile slots (ak_profile_tile_passes)
 enum { TP_STAGE, TP_D, TP_E, TP_H, TP_P, TP_B, TP_FBC, TP_F, TP_FBE, TP_LOOP, T_NPASS };
@@ -691,7 +721,7 @@ __device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
     pc.init(ta.passprof != nullptr, M.passacc);
     // static stride over units of TILE_UNIT rows (units are near-equal); inside a unit, each tile
     // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
-    for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {
+    for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;

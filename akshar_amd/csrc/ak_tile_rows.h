@@ -334,7 +334,7 @@ __device__ void rows_tiles_wave(const TileArgs &ta, const RowsOut &o, const uint
                                 RowsWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
-    for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {
+    for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;

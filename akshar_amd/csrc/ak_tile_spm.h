@@ -450,7 +450,7 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
     pc.init(ta.passprof != nullptr, M.passacc);
     // static stride over units of TILE_UNIT rows (units are near-equal); inside a unit, each tile
     // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
-    for (uint64_t t = wave_gid; t < ta.ntiles; t += nwaves) {
+    for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;

@@ -179,14 +179,14 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
     std::vector<uint32_t> stage(2 * half), counts(n), fbl(n), fb2(n);
     std::vector<uint64_t> unit_fb(nunits);
-    uint32_t fbn = 0, fb2n = 0, err = 0;
+    uint32_t fbn = 0, fb2n = 0, err = 0, qnext = 0;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = half;
     ta.unit_fb = unit_fb.data();
     ta.ra.row_status = row_status; ta.ra.bpe = m->bdev; ta.ra.single_fast = m->bpe.fast.data();
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
-    ta.fb2_count = &fb2n; ta.err = &err;
+    ta.fb2_count = &fb2n; ta.next_unit = &qnext; ta.err = &err;
     ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
     std::vector<uint16_t> sfast(SFAST_N);
     for (uint32_t i = 0; i < SFAST_N; ++i) sfast[i] = m->bpe.fast[i < 0x80u ? i : i - 0x80u + 0x900u];
@@ -267,13 +267,13 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
     std::vector<uint32_t> stage(2 * half), counts(n), fbl(n), fb2(n);
     std::vector<uint64_t> unit_fb(nunits);
-    uint32_t fbn = 0, fb2n = 0, err = 0;
+    uint32_t fbn = 0, fb2n = 0, err = 0, qnext = 0;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.out = stage.data(); ta.ra.cap = half;
     ta.ra.row_status = row_status; ta.ra.spm = m->sdev; ta.unit_fb = unit_fb.data();
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
-    ta.fb2_count = &fb2n; ta.err = &err;
+    ta.fb2_count = &fb2n; ta.next_unit = &qnext; ta.err = &err;
     ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
     SpmWaveMem *M = new SpmWaveMem();
     EmuWave W;
@@ -345,11 +345,11 @@ static int64_t rows_tiles_run(int matras, const uint8_t *in, const uint64_t *off
     std::vector<uint8_t> snorm(2 * h8), slab(2 * h32);
     std::vector<uint32_t> sseg(2 * h32), sruns(2 * h32), cn(n), cs(n), cr(n), fbl(n), fb2(n);
     std::vector<uint64_t> unit_fb(nunits);
-    uint32_t fbn = 0, fb2n = 0, err = 0;
+    uint32_t fbn = 0, fb2n = 0, err = 0, qnext = 0;
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra.in = in; ta.ra.offs = offs; ta.ra.n = n; ta.ra.row_status = row_status;
-    ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data(); ta.fb2_count = &fb2n; ta.err = &err;
+    ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data(); ta.fb2_count = &fb2n; ta.next_unit = &qnext; ta.err = &err;
     ta.ntiles = nunits; ta.rows = rows; ta.unit_fb = unit_fb.data();
     RowsOut o;
     memset(&o, 0, sizeof(o));
