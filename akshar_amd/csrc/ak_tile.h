@@ -31,7 +31,11 @@ namespace ak {
 
 constexpr int T_BCAP = 768;   // staged bytes per tile (rows past it start the next sub-tile)
 constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
-constexpr uint64_t TILE_UNIT = 64;  // rows per unit of the static wave stride (tiles pack greedily inside one)
+#ifndef AK_TILE_UNIT
+#define AK_TILE_UNIT 64
+#endif
+constexpr uint64_t TILE_UNIT = AK_TILE_UNIT;  // rows per unit of the work queue (tiles pack greedily inside one)
+static_assert(TILE_UNIT <= 64, "a unit's fallback rows are one 64-bit mask");
 constexpr int T_E = T_BCAP + 2 * T_MAXR + 64;
 
 constexpr uint16_t V_FB = 0xFFFC;    // sentinel of a row handed to the fallback kernels (no ids here)
@@ -719,7 +723,7 @@ __device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
                                uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
-    // static stride over units of TILE_UNIT rows (units are near-equal); inside a unit, each tile
+    // units of TILE_UNIT rows from the work queue (tile_first_unit); inside a unit, each tile
     // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
     for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
         pc.mark(TP_LOOP);

@@ -448,7 +448,7 @@ template <int FLAGS>
 __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
-    // static stride over units of TILE_UNIT rows (units are near-equal); inside a unit, each tile
+    // units of TILE_UNIT rows from the work queue (tile_first_unit); inside a unit, each tile
     // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
     for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
         pc.mark(TP_LOOP);
