@@ -18,7 +18,12 @@ namespace ak {
 
 static_assert(T_NPASS == AK_TILE_NPASS, "pass slots: ak_tile.h vs include/akshar.h");
 
-constexpr int TILE_BLOCK = 512;  // 8 waves share the staged property tables; 4 blocks (8 waves/SIMD) per CU
+#ifndef AK_BPE_TILE_BLOCK
+#define AK_BPE_TILE_BLOCK 1024
+#endif
+// 16 waves share the staged property tables; 2 blocks (8 waves/SIMD) per CU (A/B on MI355X with the
+// work queue: 1024-thread blocks +7 % over 4 blocks of 512, 4 M Hinglish rows)
+constexpr int TILE_BLOCK = AK_BPE_TILE_BLOCK;
 constexpr int FB_BLOCK = 256;
 
 template <int FLAGS>

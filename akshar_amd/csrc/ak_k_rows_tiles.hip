@@ -13,7 +13,10 @@
 
 namespace ak {
 
-constexpr int RT_BLOCK = 256;  // 4 waves per block
+#ifndef AK_RT_BLOCK
+#define AK_RT_BLOCK 256
+#endif
+constexpr int RT_BLOCK = AK_RT_BLOCK;  // 4 waves per block
 constexpr int RT_FB_BLOCK = 64;
 
 template <int OPS>

@@ -15,7 +15,10 @@
 
 namespace ak {
 
-constexpr int SPM_TILE_BLOCK = 256;           // 4 waves per block
+#ifndef AK_SPM_TILE_BLOCK
+#define AK_SPM_TILE_BLOCK 256
+#endif
+constexpr int SPM_TILE_BLOCK = AK_SPM_TILE_BLOCK;  // 4 waves per block
 constexpr uint32_t SPM_T_MUL = 2, SPM_T_ADD = 2;  // staging slot of row r: 2 offs[r] + 2 r
 constexpr int SPM_FB_BLOCK = 64;
 
