@@ -3,9 +3,9 @@
 #   the whole GPU suite, the default bench line (cfg4 + cfg5 block + CPU baselines), bench --workload
 #   cfg5 under torchrun (nccl, world 1), a rocprofv3 kernel-trace summary of the bench command, PMC
 #   passes over the cfg4 (10 M-row BPE) and cfg5 (25 M-row SPM) launch shapes, fallback realism.
-#   tools/measure_r03e.sh TAG
+#   tools/measure_r03f.sh TAG
 set -e
-TAG=${1:-r03e}
+TAG=${1:-r03f}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
