@@ -799,7 +799,6 @@ struct SpmDev {
     const uint16_t *cmap;       // page * 128 + (cp & 127) -> code 1..K, 0 = in no piece
     const uint32_t *code_cp;    // code -> cp
     const int32_t *byte_ids;
-    const uint8_t *plen;   // tile path: code points of piece id (unk: 1)
     int32_t root_base;
     uint32_t n_nodes;
     int32_t unk_id;

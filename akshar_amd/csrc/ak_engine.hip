@@ -153,7 +153,6 @@ static int upload_dec(uint8_t *&mem, DecTab &t, const std::vector<uint8_t> &text
 struct ak_spm {
     SpmDev dev;
     int4 *d_trie = nullptr;
-    uint8_t *d_plen = nullptr;
     uint16_t *d_cmap_page = nullptr;
     uint16_t *d_cmap = nullptr;
     uint32_t *d_code_cp = nullptr;
@@ -280,9 +279,6 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->n_nodes = t.n_nodes;
     HIP_TRY(hipMalloc(&m->d_trie, t.n_nodes * sizeof(int4)));
     HIP_TRY(hipMemcpy(m->d_trie, t.trie.data(), t.n_nodes * sizeof(int4), hipMemcpyHostToDevice));
-    if (unk_id >= 0 && (uint32_t)unk_id < n) t.plen[unk_id] = 1;  // an unk node covers one char
-    HIP_TRY(hipMalloc(&m->d_plen, t.plen.size() + 1));
-    HIP_TRY(hipMemcpy(m->d_plen, t.plen.data(), t.plen.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&m->d_cmap_page, t.cmap_page.size() * sizeof(uint16_t)));
     HIP_TRY(hipMemcpy(m->d_cmap_page, t.cmap_page.data(), t.cmap_page.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMalloc(&m->d_cmap, t.cmap.size() * sizeof(uint16_t)));
@@ -292,7 +288,6 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     HIP_TRY(hipMalloc(&m->d_byte_ids, 256 * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(m->d_byte_ids, byte_ids, 256 * sizeof(int32_t), hipMemcpyHostToDevice));
     m->dev.trie = m->d_trie;
-    m->dev.plen = m->d_plen;
     m->dev.cmap_page = m->d_cmap_page;
     m->dev.cmap = m->d_cmap;
     m->dev.code_cp = m->d_code_cp;
@@ -340,7 +335,6 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
 extern "C" void ak_spm_free(ak_spm *m) {
     if (!m) return;
     (void)hipFree(m->d_trie);
-    (void)hipFree(m->d_plen);
     (void)hipFree(m->d_cmap_page);
     (void)hipFree(m->d_cmap);
     (void)hipFree(m->d_code_cp);

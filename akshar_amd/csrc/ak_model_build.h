@@ -143,7 +143,6 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
 
 struct SpmTables {
     std::vector<int> trie;          // 4 ints per node: check, base, value, aux
-    std::vector<uint8_t> plen;      // tile path: code points of each trie piece (the caller sets unk's to 1)
     uint32_t n_nodes = 0;
     int root_base = 0;
     std::vector<uint16_t> cmap_page;  // SPM_CMAP_PAGES entries: page of cp >> 7 (0 = no piece char)
@@ -187,8 +186,7 @@ inline float user_defined_score(size_t bytes) { return (float)((double)((int)byt
 
 inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
                              const uint8_t *types, SpmTables &out) {
-    if (n >= 0xFFFFu) return "65535 or more pieces";  // the tile lattice keeps piece ids in u16
-    out.plen.assign(n, 1);
+    if (n >= (1u << 24)) return "too many pieces";
     float min_score = 3.4e38f;
     struct P { std::vector<uint32_t> cps; int val; int aux; };
     std::vector<P> ps;
@@ -208,8 +206,6 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
         int aux = 0;
         const float sc = kind == 1 ? user_defined_score(s.size()) : scores[i];
         if (kind != 2) memcpy(&aux, &sc, 4);
-        if (cps.size() > 255) return "piece longer than 255 code points";
-        out.plen[i] = (uint8_t)cps.size();
         ps.push_back({cps, (int)i | (kind << 24), aux});
         alpha.insert(alpha.end(), cps.begin(), cps.end());
     }

@@ -44,15 +44,14 @@ constexpr int S_WORDS = (S_BCAP + 32) / 2 >= 256 ? 256 : 128;  // words per tile
 constexpr uint16_t W_CODED = 0x8000;  // W entry: 0x8000 | dense code (a char some piece holds), else the code point
 constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: the trie walk stops there)
 constexpr uint16_t W_END = 0x7FFF;
-constexpr uint16_t BK_NONE = 0xFFFFu;  // back[]: no piece ends here yet
+constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
 
 struct SpmWaveMem {
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
     uint16_t v[S_E];                         // V; after pass W: nxt (u8 per W position)
     uint16_t w[S_W];                         // P (pass D1), then W
     float best[S_W];                         // Viterbi best score per W position (word-local)
-    uint16_t back[S_W];                      // best piece ending here: its id (chars: SpmDev::plen); u16
-                                             // so that 5 blocks of 4 waves fit a CU's LDS
+    uint32_t back[S_W];                      // best piece ending here: id << 8 | chars
     uint8_t wrow[S_WORDS];                   // row of each word
     uint8_t fb[T_MAXR];
     uint8_t mfail[T_MAXR];                   // row has a lattice node within the rounding bound (pass V2)
@@ -127,7 +126,7 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, int p0, 
             if (bk == BK_NONE || cand > M.best[ee]) {
                 if (MARGIN && bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
                 M.best[ee] = cand;
-                M.back[ee] = (uint16_t)id;
+                M.back[ee] = ((uint32_t)id << 8) | (uint32_t)(ee - s);
             } else if (MARGIN) {
                 minm = fminf(minm, M.best[ee] - cand);
             }
@@ -141,7 +140,7 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, int p0, 
             if (bk == BK_NONE || cand > M.best[ee]) {
                 if (MARGIN && bk != BK_NONE) minm = fminf(minm, cand - M.best[ee]);
                 M.best[ee] = cand;
-                M.back[ee] = (uint16_t)m.unk_id;
+                M.back[ee] = ((uint32_t)m.unk_id << 8) | 1u;
             } else if (MARGIN) {
                 minm = fminf(minm, M.best[ee] - cand);
             }
@@ -149,10 +148,10 @@ __device__ __forceinline__ void word_dp(SpmWaveMem &M, const SpmDev &m, int p0, 
     }
 }
 
-// One lattice update: candidate `cand` for W position ee (piece `id`), sentencepiece's
+// One lattice update: candidate `cand` for W position ee (piece `id` of `len` chars), sentencepiece's
 // rule (first arrival wins ties); MARGIN tracks the gap to the stored leader.
 template <bool MARGIN>
-__device__ __forceinline__ void spm_relax(SpmWaveMem &M, int ee, float cand, uint32_t id, float &minm) {
+__device__ __forceinline__ void spm_relax(SpmWaveMem &M, int ee, float cand, uint32_t id, uint32_t len, float &minm) {
     const uint32_t bk = M.back[ee];
     const float bb = M.best[ee];
     const bool none = bk == BK_NONE;
@@ -160,7 +159,7 @@ __device__ __forceinline__ void spm_relax(SpmWaveMem &M, int ee, float cand, uin
     if (MARGIN && !none) minm = fminf(minm, take ? cand - bb : bb - cand);
     if (take) {
         M.best[ee] = cand;
-        M.back[ee] = (uint16_t)id;
+        M.back[ee] = (id << 8) | len;
     }
 }
 
@@ -189,7 +188,7 @@ __device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, in
         const bool hv = ok && value >= 0 && ((value >> 24) & 3) != 2;
         const int ee = k + 1;
         if (hv) {
-            spm_relax<true>(M, ee, __int_as_float(e.w) + till, (uint32_t)(value & 0xFFFFFF), minm);
+            spm_relax<true>(M, ee, __int_as_float(e.w) + till, (uint32_t)(value & 0xFFFFFF), (uint32_t)(ee - s), minm);
             reach = ee > reach ? ee : reach;
             hs = hs || k == s;
         }
@@ -203,7 +202,7 @@ __device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, in
         if (w_ballot(end && !hs)) {  // rare: no piece of exactly the first char -> an unk node
             if (end && !hs) {
                 reach = s + 1 > reach ? s + 1 : reach;
-                spm_relax<true>(M, s + 1, m.unk_score + till, (uint32_t)m.unk_id, minm);
+                spm_relax<true>(M, s + 1, m.unk_score + till, (uint32_t)m.unk_id, 1u, minm);
             }
         }
         const int sn = s + 1;
@@ -239,10 +238,10 @@ __device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &
     uint32_t cnt = 0;
     for (int e = p1; e > p0;) {
         const uint32_t bk = M.back[e];
-        const int d = (int)m.plen[bk];
+        const int d = (int)(bk & 0xFFu);
         const int s = e - d;
         nxt[s] = (uint8_t)d;
-        const int id = (int)bk;
+        const int id = (int)(bk >> 8);
         cnt += id == m.unk_id ? (uint32_t)utf8_len(spm_wcp(m, M.w[s])) : 1u;
         e = s;
     }
@@ -410,7 +409,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             uint64_t d = P;
             for (int s = p0; s < p1;) {
                 const int e = s + (int)nxt[s];
-                const uint32_t id = M.back[e];
+                const uint32_t id = M.back[e] >> 8;
                 if ((int)id == m.unk_id) {  // an unk node is one char: byte fallback
                     const uint32_t cp = spm_wcp(m, M.w[s]);
                     const int cl = utf8_len(cp);

@@ -54,8 +54,6 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->scores.assign(scores, scores + n);
     m->byte_ids.assign(byte_ids, byte_ids + 256);
     m->sdev.trie = (const int4 *)m->spm.trie.data();
-    if (unk_id >= 0 && (size_t)unk_id < m->spm.plen.size()) m->spm.plen[unk_id] = 1;
-    m->sdev.plen = m->spm.plen.data();
     m->sdev.cmap_page = m->spm.cmap_page.data();
     m->sdev.cmap = m->spm.cmap.data();
     m->sdev.code_cp = m->spm.code_cp.data();
