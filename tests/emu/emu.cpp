@@ -165,6 +165,25 @@ thread_local EmuWave *t_wave;
 
 static uint32_t g_last_fb = 0;
 extern "C" uint32_t emu_last_fallback_rows() { return g_last_fb; }
+// waves the tile entries below emulate at once (each its own 64 threads and wave memory), all taking
+// units from the one work queue as on the GPU
+static int g_waves = 1;
+extern "C" void emu_set_waves(int w) { g_waves = w < 1 ? 1 : w; }
+
+// run fn(wave) on g_waves emulated waves of 64 lane threads each
+template <class F>
+static void run_waves(F fn) {
+    std::vector<EmuWave> waves(g_waves);
+    std::vector<std::thread> th;
+    for (int w = 0; w < g_waves; ++w)
+        for (int lane = 0; lane < 64; ++lane)
+            th.emplace_back([&, w, lane] {
+                t_lane = lane;
+                t_wave = &waves[w];
+                fn(w);
+            });
+    for (auto &x : th) x.join();
+}
 
 extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
                                  uint32_t *out, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, int rows) {
@@ -190,17 +209,8 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
     std::vector<uint16_t> sfast(SFAST_N);
     for (uint32_t i = 0; i < SFAST_N; ++i) sfast[i] = m->bpe.fast[i < 0x80u ? i : i - 0x80u + 0x900u];
-    TileWaveMem *M = new TileWaveMem();
-    EmuWave W;
-    std::vector<std::thread> th;
-    for (int lane = 0; lane < 64; ++lane)
-        th.emplace_back([&, lane] {
-            t_lane = lane;
-            t_wave = &W;
-            bpe_tiles_wave<3>(ta, hot_tab, sfast.data(), *M, 0, 1);
-        });
-    for (auto &x : th) x.join();
-    delete M;
+    std::vector<TileWaveMem> M(g_waves);
+    run_waves([&](int w) { bpe_tiles_wave<3>(ta, hot_tab, sfast.data(), M[w], (uint32_t)w, (uint32_t)g_waves); });
     if (err) return -1;
     g_last_fb = fbn;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
@@ -275,17 +285,8 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
     ta.fb2_count = &fb2n; ta.next_unit = &qnext; ta.err = &err;
     ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
-    SpmWaveMem *M = new SpmWaveMem();
-    EmuWave W;
-    std::vector<std::thread> th;
-    for (int lane = 0; lane < 64; ++lane)
-        th.emplace_back([&, lane] {
-            t_lane = lane;
-            t_wave = &W;
-            spm_tiles_wave<3>(ta, hot_tab, scode, *M, 0, 1);
-        });
-    for (auto &x : th) x.join();
-    delete M;
+    std::vector<SpmWaveMem> M(g_waves);
+    run_waves([&](int w) { spm_tiles_wave<3>(ta, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
     if (err) return -1;
     g_last_fb = fbn;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }

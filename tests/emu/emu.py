@@ -28,6 +28,7 @@ def lib():
         L.emu_spm_create.argtypes = [ctypes.c_uint32, P, P, P, P, ctypes.c_int32, P]
         L.emu_free.argtypes = [P]
         L.emu_bpe_tiles.restype = ctypes.c_int64
+        L.emu_set_waves.argtypes = [ctypes.c_int]
         L.emu_bpe_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
         L.emu_spm_tiles.restype = ctypes.c_int64
         L.emu_spm_tiles.argtypes = [P, ctypes.c_int, P, P, ctypes.c_uint64, P, ctypes.c_uint64, P, P, ctypes.c_int]
@@ -83,8 +84,9 @@ def run(op, flags, buf, offs, model=None, matras=False):
     return out[:tot], oo
 
 
-def bpe_tiles(model, buf, offs, flags=3, rows=8):
-    """The tile-cooperative BPE kernel on one emulated wave -> (ids, out_offs, row_status)."""
+def bpe_tiles(model, buf, offs, flags=3, rows=8, waves=1):
+    """The tile-cooperative BPE kernel on `waves` emulated waves sharing the unit queue -> (ids, out_offs,
+    row_status)."""
     buf = pad(buf)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     n = len(offs) - 1
@@ -92,14 +94,17 @@ def bpe_tiles(model, buf, offs, flags=3, rows=8):
     out = np.zeros(cap, dtype=np.uint32)
     oo = np.zeros(n + 1, dtype=np.uint64)
     st = np.zeros(max(n, 1), dtype=np.uint8)
+    lib().emu_set_waves(waves)
     tot = lib().emu_bpe_tiles(model.h, flags, buf.ctypes.data, offs.ctypes.data, n, out.ctypes.data, cap,
                               oo.ctypes.data, st.ctypes.data, rows)
+    lib().emu_set_waves(1)
     assert 0 <= tot <= cap, tot
     return out[:tot], oo, st[:n]
 
 
-def spm_tiles(model, buf, offs, flags=3, rows=4):
-    """The tile-cooperative SentencePiece kernel on one emulated wave -> (ids, out_offs, row_status)."""
+def spm_tiles(model, buf, offs, flags=3, rows=4, waves=1):
+    """The tile-cooperative SentencePiece kernel on `waves` emulated waves sharing the unit queue -> (ids,
+    out_offs, row_status)."""
     buf = pad(buf)
     offs = np.ascontiguousarray(offs, dtype=np.uint64)
     n = len(offs) - 1
@@ -107,8 +112,10 @@ def spm_tiles(model, buf, offs, flags=3, rows=4):
     out = np.zeros(cap, dtype=np.uint32)
     oo = np.zeros(n + 1, dtype=np.uint64)
     st = np.zeros(max(n, 1), dtype=np.uint8)
+    lib().emu_set_waves(waves)
     tot = lib().emu_spm_tiles(model.h, flags, buf.ctypes.data, offs.ctypes.data, n, out.ctypes.data, cap,
                               oo.ctypes.data, st.ctypes.data, rows)
+    lib().emu_set_waves(1)
     assert 0 <= tot <= cap, tot
     return out[:tot], oo, st[:n]
 

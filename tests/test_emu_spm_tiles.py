@@ -79,3 +79,12 @@ def test_margin_rule_keeps_hinglish_on_the_tile_path(em):
     buf, offs = synth.generate(1, 2000, seed=77)
     emu.spm_tiles(em, buf, offs, rows=4)
     assert emu.last_fallback_rows() <= 20  # NFC-decomposed nuktas of the generator (~0.3 %)
+
+
+def test_work_queue_waves_vs_oracle(em, spm_model):
+    """Three emulated waves on one unit queue give the oracle's ids (units finish in any order)."""
+    from akshar_amd import synth
+    buf, offs = synth.generate(1, 400, seed=903)
+    ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=4, waves=3)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)

@@ -75,3 +75,21 @@ def test_mixed_pretoken_lengths(em, bpe_model, rows):
     ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=rows)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
     assert rows_ints(ids, oo) == rows_ints(ref, ro)
+
+
+def test_work_queue_waves_vs_oracle(em, bpe_model):
+    """Three emulated waves take the 64-row units from one work queue (ak_tile.h tile_first_unit) in
+    whatever order their threads interleave; every unit writes its own run, so the ids equal the
+    oracle's, fallback rows (fuzz lines) included."""
+    from akshar_amd import synth
+    b1, o1 = synth.generate(1, 300, seed=901)
+    b2, o2 = synth.generate(2, 100, seed=902)
+    texts = [bytes(b1[o1[i]:o1[i + 1]]) for i in range(300)] + [bytes(b2[o2[i]:o2[i + 1]]) for i in range(100)]
+    order = np.random.default_rng(5).permutation(len(texts))
+    raw = [texts[i] for i in order]
+    offs = np.zeros(len(raw) + 1, dtype=np.uint64)
+    np.cumsum([len(r) for r in raw], out=offs[1:])
+    buf = np.frombuffer(b"".join(raw), dtype=np.uint8).copy()
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8, waves=3)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
