@@ -46,12 +46,16 @@ constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: t
 constexpr uint16_t W_END = 0x7FFF;
 constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
 
+#ifndef AK_SPM_SELECT_RELAX  // the lattice update as selects into a dummy slot (A/B variant)
+#define AK_SPM_SELECT_RELAX 0
+#endif
+
 struct SpmWaveMem {
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
     uint16_t v[S_E];                         // V; after pass W: nxt (u8 per W position)
     uint16_t w[S_W];                         // P (pass D1), then W
-    float best[S_W];                         // Viterbi best score per W position (word-local)
-    uint32_t back[S_W];                      // best piece ending here: id << 8 | chars
+    float best[S_W + AK_SPM_SELECT_RELAX];     // Viterbi best score per W position (word-local)
+    uint32_t back[S_W + AK_SPM_SELECT_RELAX];  // best piece ending here: id << 8 | chars ([S_W]: dummy)
     uint8_t wrow[S_WORDS];                   // row of each word
     uint8_t fb[T_MAXR];
     uint8_t mfail[T_MAXR];                   // row has a lattice node within the rounding bound (pass V2)
@@ -187,11 +191,28 @@ __device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, in
         const int value = e.z;
         const bool hv = ok && value >= 0 && ((value >> 24) & 3) != 2;
         const int ee = k + 1;
+#if AK_SPM_SELECT_RELAX
+        {  // the update as selects: every lane reads and writes a slot (its candidate's, or the dummy)
+            const int es = hv ? ee : S_W;
+            const uint32_t bk = M.back[es];
+            const float bb = M.best[es];
+            const float cand = __int_as_float(e.w) + till;
+            const bool none = bk == BK_NONE;
+            const bool take = none || cand > bb;
+            const float gap = take ? cand - bb : bb - cand;
+            minm = hv && !none ? fminf(minm, gap) : minm;
+            M.best[es] = take ? cand : bb;
+            M.back[es] = take ? (((uint32_t)(value & 0xFFFFFF) << 8) | (uint32_t)(ee - s)) : bk;
+            reach = hv && ee > reach ? ee : reach;
+            hs = hs || (hv && k == s);
+        }
+#else
         if (hv) {
             spm_relax<true>(M, ee, __int_as_float(e.w) + till, (uint32_t)(value & 0xFFFFFF), (uint32_t)(ee - s), minm);
             reach = ee > reach ? ee : reach;
             hs = hs || k == s;
         }
+#endif
         if (ok) {
             node = t;
             nb = e.y;
