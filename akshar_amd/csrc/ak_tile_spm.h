@@ -46,8 +46,8 @@ constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: t
 constexpr uint16_t W_END = 0x7FFF;
 constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
 
-#ifndef AK_SPM_SELECT_RELAX  // the lattice update as selects into a dummy slot (A/B variant)
-#define AK_SPM_SELECT_RELAX 0
+#ifndef AK_SPM_SELECT_RELAX  // the lattice update as selects into a dummy slot: fewer scalar (exec-mask)
+#define AK_SPM_SELECT_RELAX 1  // instructions, +2.8-3.6 % (A/B on MI355X, 4 M rows)
 #endif
 
 struct SpmWaveMem {
