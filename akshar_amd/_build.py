@@ -98,10 +98,13 @@ def build_hip(force=False, jobs=None):
     return out
 
 
-def build_variant(name, defines=(), tu_flags=None):
+def build_variant(name, defines=(), tu_flags=None, only=None):
     """Development aid: the library built with extra -D defines / per-TU flags into
-    akshar_amd/_variants/<name>.so (selected at run time by AK_LIB_VARIANT=<name>)."""
+    akshar_amd/_variants/<name>.so (selected at run time by AK_LIB_VARIANT=<name>). only: the TU
+    names compiled with the defines; every other TU links the default build's object."""
     global TU_FLAGS
+    if only:
+        build_hip()
     objdir = os.path.join(ROOT, "build", "variants", name)
     os.makedirs(objdir, exist_ok=True)
     hipcc = os.path.join(ROCM, "bin", "hipcc")
@@ -110,8 +113,10 @@ def build_variant(name, defines=(), tu_flags=None):
     flags = TU_FLAGS if tu_flags is None else tu_flags
     from concurrent.futures import ThreadPoolExecutor
     srcs = [os.path.join(CSRC, n) for n in sorted(os.listdir(CSRC)) if n.endswith((".hip", ".cpp"))]
-    objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
-    cmds = [common + flags.get(os.path.basename(s), []) + ["-c", "-o", o, s] for s, o in zip(srcs, objs)]
+    objs = [os.path.join(objdir if not only or os.path.basename(s) in only else os.path.join(ROOT, "build", "hip"),
+                         os.path.basename(s) + ".o") for s in srcs]
+    cmds = [common + flags.get(os.path.basename(s), []) + ["-c", "-o", o, s] for s, o in zip(srcs, objs)
+            if not only or os.path.basename(s) in only]
     with ThreadPoolExecutor(min(16, os.cpu_count() or 4)) as ex:
         for f in [ex.submit(_run, c) for c in cmds]:
             f.result()

@@ -22,8 +22,8 @@ AK_ST_FILTER = 4
 AK_ST_ELONG = 8
 AK_ROW_BAD_UTF8 = 1
 AK_ROW_LIMIT = 4
-AK_TILE_PASSES = ("pre", "stage_decode_nfc_map", "elong_ws_pretok", "unused", "pretoken_starts", "merge_or_viterbi",
-                  "fallback_list", "ids_to_slots", "unused2", "loop")
+AK_TILE_PASSES = ("pre", "stage_decode_nfc_map", "elong_ws_pretok", "pretoken_cache", "pretoken_starts", "merge_or_viterbi",
+                  "fallback_list", "ids_to_slots", "pool_merges", "loop")
 AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4, "tiles": 5, "copy": 6, "spm_tiles": 7,
            "row_tiles": 8}
 
@@ -66,6 +66,8 @@ SIGNATURES = {
     "ak_profile_read": (I32, [I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
     "ak_profile_reset": (None, []),
     "ak_profile_tile_passes": (I32, [P, ctypes.POINTER(U64), I32]),
+    "ak_profile_tile_counters": (I32, [P, ctypes.POINTER(U64), I32]),
+    "ak_bpe_cache_info": (I32, [P, ctypes.POINTER(U64)]),
     "ak_ws_fallback_rows": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
     "ak_normalize_cap": (U64, [U64, U64]),
     "ak_segment_cap": (U64, [U64, U64]),
@@ -85,6 +87,8 @@ def lib():
             raise AksharError("HIP engine not built: %s missing (run __graft_entry__.build())" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("AK_LIB_VARIANT") and not hasattr(L, name):
+                continue  # an A/B variant built from an older tree
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -527,6 +527,9 @@ struct BpeDev {
     const uint32_t *added_off;   // n_added + 1 offsets into added_cp
     const uint32_t *added_id;
     uint32_t n_added;
+    // tile path: the pre-token result cache (ak_ptc.h; null = off)
+    const uint32_t *ptc;
+    uint32_t ptc_mask;
 };
 
 constexpr int AK_ADDED_MAXLEN = 16;  // longest added token (code points) the device matcher holds

@@ -18,6 +18,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -126,6 +127,9 @@ struct ak_bpe {
     uint32_t *d_added = nullptr;  // added tokens: code points, offsets, ids (one allocation)
     DecTab dec{};                 // ak_bpe_set_vocab
     uint8_t *d_dec = nullptr;     // text, offsets, kinds (one allocation)
+    uint32_t *d_ptc = nullptr;    // the pre-token result cache (ak_ptc.h), tile path only
+    akb::PtcStats ptc{};
+    uint32_t ptc_slots = 0;
 };
 
 // id -> text tables in one device allocation (DecTab)
@@ -199,7 +203,31 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
     m->dev.bos = bos;
     m->dev.eos = eos;
     m->tile_ok = max_id < 0x7FFCu && monotone;
+    // the tile kernel's pre-token result cache (ak_ptc.h; AK_PTC=0 leaves it off: development aid,
+    // AK_PTC_BITS=b forces 2^b slots: tests of collisions and dropped keys)
+    const char *pe = getenv("AK_PTC");
+    if (m->tile_ok && !(pe && pe[0] == '0')) {
+        const char *pb = getenv("AK_PTC_BITS");
+        const int bits = pb ? std::max(0, std::min(24, atoi(pb))) : -1;
+        std::vector<uint32_t> tab;
+        uint32_t mask = 0;
+        akb::build_bpe_ptc(n_single, single_id, n_merges, merges, bits, tab, mask, m->ptc);
+        HIP_TRY(hipMalloc(&m->d_ptc, tab.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(m->d_ptc, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        m->dev.ptc = m->d_ptc;
+        m->dev.ptc_mask = mask;
+        m->ptc_slots = mask + 1;
+    }
     *out = m;
+    return AK_OK;
+}
+
+extern "C" int ak_bpe_cache_info(const ak_bpe *m, uint64_t info[4]) {
+    if (!m || !info) return fail(AK_ERR_ARG, "ak_bpe_cache_info: null argument");
+    info[0] = m->ptc_slots;
+    info[1] = m->ptc.keys;
+    info[2] = m->ptc.stored;
+    info[3] = m->ptc.multi;
     return AK_OK;
 }
 
@@ -212,6 +240,7 @@ extern "C" void ak_bpe_free(ak_bpe *m) {
     (void)hipFree(m->d_single_id);
     (void)hipFree(m->d_added);
     (void)hipFree(m->d_dec);
+    (void)hipFree(m->d_ptc);
     delete m;
 }
 
@@ -423,6 +452,17 @@ extern "C" int ak_profile_tile_passes(ak_ws *w, uint64_t *cycles, int n) {
     return k;
 }
 
+extern "C" int ak_profile_tile_counters(ak_ws *w, uint64_t *counts, int n) {
+    if (!w || !counts || n < 0) return fail(AK_ERR_ARG, "ak_profile_tile_counters: bad argument");
+    memset(counts, 0, sizeof(uint64_t) * (size_t)n);
+    if (!w->tile_passprof) return 0;
+    const int k = std::min(n, (int)AK_TILE_NCOUNTERS);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(counts, w->tile_passprof + AK_TILE_NPASS, (size_t)k * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemset(w->tile_passprof + AK_TILE_NPASS, 0, AK_TILE_NCOUNTERS * 8));
+    return k;
+}
+
 extern "C" void ak_ws_free(ak_ws *w) {
     if (!w) return;
     (void)hipFree(w->stage);
@@ -430,6 +470,8 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->tile_passprof);
     (void)hipFree(w->fb2);
     (void)hipFree(w->unit_fb);
+    (void)hipFree(w->unit_len);
+    (void)hipFree(w->bpool);
     (void)hipFree(w->counts);
     (void)hipFree(w->slow_list);
     (void)hipFree(w->huge_list);

@@ -60,6 +60,10 @@ struct AkWs {
     uint64_t cap_fb2 = 0;
     uint64_t *unit_fb = nullptr;    // tile BPE: per 64-row unit, the mask of its fallback rows
     uint64_t cap_unit_fb = 0;
+    uint32_t *unit_len = nullptr;   // tile BPE: per unit, its staging run's length (ids + dead entries)
+    uint64_t cap_unit_len = 0;
+    uint4 *bpool = nullptr;         // tile BPE: the waves' merge pools (ak_tile.h pool_flush)
+    uint64_t cap_bpool = 0;         // ... entries
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)

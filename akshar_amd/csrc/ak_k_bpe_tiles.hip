@@ -16,7 +16,7 @@
 
 namespace ak {
 
-static_assert(T_NPASS == AK_TILE_NPASS, "pass slots: ak_tile.h vs include/akshar.h");
+static_assert(T_NPASS == AK_TILE_NPASS && T_NCTR == AK_TILE_NCOUNTERS, "pass slots: ak_tile.h vs include/akshar.h");
 
 #ifndef AK_BPE_TILE_BLOCK
 #define AK_BPE_TILE_BLOCK 1024
@@ -27,7 +27,10 @@ constexpr int TILE_BLOCK = AK_BPE_TILE_BLOCK;
 constexpr int FB_BLOCK = 256;
 
 template <int FLAGS>
-__global__ __launch_bounds__(TILE_BLOCK, 8) void k_bpe_tiles(TileArgs ta) {
+#ifndef AK_BPE_TILE_WPE
+#define AK_BPE_TILE_WPE 8
+#endif
+__global__ __launch_bounds__(TILE_BLOCK, AK_BPE_TILE_WPE) void k_bpe_tiles(TileArgs ta) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t sfast[SFAST_N];
     __shared__ TileWaveMem wm[TILE_BLOCK / 64];
@@ -215,6 +218,84 @@ __global__ __launch_bounds__(256) void k_unit_copy(const T *__restrict__ stage, 
     }
 }
 
+// The tile BPE unit runs -> final positions, dropping the STAGE_DEAD entries pooled merges left
+// (ak_tile.h pool_flush). One wave per unit: a unit without fallback rows streams its run
+// (unit_len[u] entries, UC_B loads per lane in flight) and compacts each 64-entry step by ballot;
+// a unit with fallback rows places the k-th live entry of its run in the non-fallback row whose
+// range of live entries holds k (a binary search over the rows' scanned counts held in lanes) and
+// copies the fallback rows from their slots in the second staging half.
+__global__ __launch_bounds__(256) void k_unit_copy_bpe(const uint32_t *__restrict__ stage, const uint32_t *__restrict__ stage_fb,
+                                                       const uint64_t *__restrict__ offs, const uint64_t *__restrict__ out_offs,
+                                                       const uint64_t *__restrict__ unit_fb, const uint32_t *__restrict__ unit_len,
+                                                       uint64_t n, uint32_t *__restrict__ out, uint64_t cap, uint64_t half) {
+    const int lane = w_lane();
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
+    for (uint64_t u = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < nunits; u += nwaves) {
+        const uint64_t u0 = u * TILE_UNIT;
+        const int nr = (int)(u0 + TILE_UNIT < n ? TILE_UNIT : n - u0);
+        const uint64_t fbm = unit_fb[u];
+        const uint64_t base = offs[u0] + 2 * u0;
+        const uint64_t len = unit_len[u];
+        const uint64_t o0 = out_offs[u0];
+        if (fbm == 0) {
+            uint64_t d = o0;
+            for (uint64_t k0 = 0; k0 < len; k0 += 64 * UC_B) {
+                uint32_t v[UC_B];
+#pragma unroll
+                for (int q = 0; q < UC_B; ++q) {
+                    const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+                    v[q] = k < len && base + k < half ? stage[base + k] : STAGE_DEAD;
+                }
+#pragma unroll
+                for (int q = 0; q < UC_B; ++q) {
+                    const bool keep = v[q] != STAGE_DEAD;
+                    const uint64_t KM = w_ballot(keep);
+                    const uint64_t at = d + w_rank(KM);
+                    if (keep && at < cap) out[at] = v[q];
+                    d += (uint64_t)w_popc(KM);
+                }
+            }
+            continue;
+        }
+        // rare: a unit with fallback rows
+        const uint64_t r = u0 + (uint64_t)lane;
+        const bool in = lane < nr;
+        const uint64_t ro = in ? out_offs[r] : 0ull;
+        const uint64_t c = in ? out_offs[r + 1] - ro : 0ull;
+        const bool fb = in && ((fbm >> lane) & 1ull);
+        uint32_t tot;
+        const uint32_t cum = w_exscan(fb ? 0u : (uint32_t)c, &tot);  // live entries of the run before this row
+        for (int j = 0; j < nr; ++j) {  // fallback rows from their slots
+            if (!((fbm >> j) & 1ull)) continue;
+            const uint64_t cj = w_bcast(c, j), dj = w_bcast(ro, j), rj = u0 + (uint64_t)j;
+            const uint64_t sj = offs[rj] + 2 * rj;
+            for (uint64_t k = (uint64_t)lane; k < cj; k += 64)
+                if (dj + k < cap && sj + k < half) out[dj + k] = stage_fb[sj + k];
+        }
+        uint32_t kseen = 0;  // live entries passed so far
+        for (uint64_t k0 = 0; k0 < len; k0 += 64) {
+            const uint64_t k = k0 + (uint64_t)lane;
+            const uint32_t v = k < len && base + k < half ? stage[base + k] : STAGE_DEAD;
+            const bool keep = v != STAGE_DEAD;
+            const uint64_t KM = w_ballot(keep);
+            const uint32_t idx = kseen + w_rank(KM);
+            // the non-fallback row j with cum[j] <= idx < cum[j] + c[j]: the largest j with cum[j] <= idx
+            // (fallback rows add nothing to cum, so a fallback row never wins a tie with the row after it)
+            int jr = 0;
+            for (int step = 32; step >= 1; step >>= 1) {
+                const int cand = jr + step;
+                const uint32_t cc = w_shfl(cum, cand < nr ? cand : nr - 1);
+                if (cand < nr && cc <= idx) jr = cand;
+            }
+            const uint32_t cj = w_shfl(cum, jr);
+            const uint64_t dj = w_shfl(ro, jr);
+            if (keep && dj + (idx - cj) < cap) out[dj + (idx - cj)] = v;
+            kseen += (uint32_t)w_popc(KM);
+        }
+    }
+}
+
 template <class T>
 int copy_units(const T *stage, const T *stage_fb, uint64_t half, const uint64_t *offs, const uint64_t *out_offs,
                const uint64_t *unit_fb, uint64_t n, T *out, uint64_t cap, uint32_t mul, uint32_t add, hipStream_t st) {
@@ -302,13 +383,20 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     const int R = w->tile_rows;
     const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the work queue (ak_tile.h tile_first_unit)
     if ((rc = ws_unit_fb_reserve(w, ntiles))) return rc;
+    if (w->cap_unit_len < ntiles) {
+        (void)hipFree(w->unit_len);
+        w->unit_len = nullptr;
+        w->cap_unit_len = 0;
+        HIP_TRY(hipMalloc(&w->unit_len, ntiles * 4));
+        w->cap_unit_len = ntiles;
+    }
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count, [3] the unit queue
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
     if (g_prof_passes && !w->tile_passprof) {
-        HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
-        HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
+        HIP_TRY(hipMalloc(&w->tile_passprof, T_NPROF * 8));
+        HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPROF * 8, st));
     }
     if (!g_tile_blocks_per_cu) {
         int b = 0;
@@ -347,6 +435,17 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     if (const char *e = getenv("AK_TILE_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + waves_per_block - 1) / waves_per_block,
                                                        (uint64_t)num_cus() * (uint64_t)bpc);
+    // the waves' merge pools: POOL_CAP entries per wave slot of the grid
+    const uint64_t pool_entries = (uint64_t)grid * waves_per_block * POOL_CAP;
+    if (w->cap_bpool < pool_entries) {
+        (void)hipFree(w->bpool);
+        w->bpool = nullptr;
+        w->cap_bpool = 0;
+        HIP_TRY(hipMalloc(&w->bpool, pool_entries * sizeof(uint4)));
+        w->cap_bpool = pool_entries;
+    }
+    ta.pool = w->bpool;
+    ta.unit_len = w->unit_len;
     AK_PROF(AK_PROF_TILES, false, st);
     k_bpe_tiles<3><<<grid, TILE_BLOCK, 0, st>>>(ta);
     AK_PROF(AK_PROF_TILES, true, st);
@@ -374,8 +473,12 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
     AK_PROF(AK_PROF_COPY, false, st);
-    rc = copy_units<uint32_t>(w->stage, w->stage + half, half, a0.offs, out_offs, w->unit_fb, a0.n,
-                              (uint32_t *)a0.out, a0.cap, 1, 2, st);
+    {
+        const unsigned cgrid = (unsigned)std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)num_cus() * 8);
+        k_unit_copy_bpe<<<cgrid, 256, 0, st>>>(w->stage, w->stage + half, a0.offs, out_offs, w->unit_fb, w->unit_len,
+                                               a0.n, (uint32_t *)a0.out, a0.cap, half);
+        HIP_TRY(hipGetLastError());
+    }
     AK_PROF(AK_PROF_COPY, true, st);
     return rc;
 }

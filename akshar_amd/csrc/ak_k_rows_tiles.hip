@@ -96,8 +96,8 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
     if (g_prof_passes && !w->tile_passprof) {
-        HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
-        HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
+        HIP_TRY(hipMalloc(&w->tile_passprof, T_NPROF * 8));
+        HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPROF * 8, st));
     }
     if (!g_rt_bpc[OPS]) {
         int b = 0;

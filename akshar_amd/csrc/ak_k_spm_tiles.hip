@@ -104,8 +104,8 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
     }
     if (g_prof_passes && !w->tile_passprof) {
-        HIP_TRY(hipMalloc(&w->tile_passprof, T_NPASS * 8));
-        HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPASS * 8, st));
+        HIP_TRY(hipMalloc(&w->tile_passprof, T_NPROF * 8));
+        HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPROF * 8, st));
     }
     if (!g_spm_blocks_per_cu) {
         int b = 0;

@@ -17,6 +17,8 @@
 #include <utility>
 #include <vector>
 
+#include "ak_ptc.h"
+
 namespace akb {
 
 constexpr uint32_t FAST_N = 0x0A00;
@@ -139,6 +141,118 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
     for (size_t i = 0; i < rest.size(); ++i) { t.rest_cp[i] = rest[i].first; t.rest_id[i] = rest[i].second; }
     t.n_rest = (uint32_t)rest.size();
     return "";
+}
+
+// The pre-token result cache (ak_ptc.h): the char-id sequence of every merged token (2..PTC_MAXN
+// symbols: the expansion of its merge's left and right ids down to single-char ids), run through
+// merge_all with the model's ranks (lowest rank, leftmost, as HF BPE); a sequence whose result is
+// ONE id becomes a key. Keys are placed by two-choice cuckoo in token-id order; a key left without
+// a slot after the kick limit is dropped (the tile kernel then merges it as any other pre-token).
+// bits < 0: the table size from the key count (>= 2.5 slots per key); bits >= 0 forces 2^bits
+// slots (tests: tiny tables force collisions and drops).
+struct PtcStats {
+    uint32_t keys = 0;       // single-result sequences found
+    uint32_t stored = 0;     // placed in the table
+    uint32_t multi = 0;      // merged-token sequences whose merge_all is not one id (never stored)
+};
+
+inline void build_bpe_ptc(uint32_t n_single, const uint32_t *single_id, uint32_t n_merges, const uint32_t *merges,
+                          int bits, std::vector<uint32_t> &tab, uint32_t &mask, PtcStats &st) {
+    using namespace akp;
+    st = PtcStats{};
+    uint32_t max_id = 0;
+    for (uint32_t i = 0; i < n_single; ++i) max_id = std::max(max_id, single_id[i]);
+    for (uint64_t i = 0; i < 3ull * n_merges; ++i) max_id = std::max(max_id, merges[i]);
+    // expansion of every id down to single-char ids (empty = unknown / not reachable)
+    std::vector<std::vector<uint16_t>> ex((size_t)max_id + 1);
+    for (uint32_t i = 0; i < n_single; ++i) ex[single_id[i]] = {(uint16_t)single_id[i]};
+    std::vector<uint32_t> made;  // merged token ids, first occurrence
+    for (uint32_t r = 0; r < n_merges; ++r) {
+        const uint32_t a = merges[3 * r], b = merges[3 * r + 1], c = merges[3 * r + 2];
+        if (!ex[c].empty() || ex[a].empty() || ex[b].empty()) continue;
+        if (ex[a].size() + ex[b].size() > (size_t)PTC_MAXN) continue;
+        ex[c] = ex[a];
+        ex[c].insert(ex[c].end(), ex[b].begin(), ex[b].end());
+        made.push_back(c);
+    }
+    // merge ranks: (left << 16 | right) -> (rank << 16 | new id), the lowest rank wins
+    std::vector<std::pair<uint32_t, uint32_t>> pr;
+    pr.reserve(n_merges);
+    for (uint32_t r = 0; r < n_merges; ++r)
+        pr.emplace_back((merges[3 * r] << 16) | merges[3 * r + 1], (r << 16) | (merges[3 * r + 2] & 0xFFFFu));
+    std::stable_sort(pr.begin(), pr.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+    auto rank_of = [&](uint32_t l, uint32_t rgt) -> uint32_t {
+        const uint32_t key = (l << 16) | rgt;
+        auto it = std::lower_bound(pr.begin(), pr.end(), std::make_pair(key, 0u),
+                                   [](const auto &x, const auto &y) { return x.first < y.first; });
+        return it != pr.end() && it->first == key ? it->second : 0xFFFFFFFFu;
+    };
+    struct Key { std::vector<uint16_t> s; uint32_t id; };
+    std::vector<Key> keys;
+    std::sort(made.begin(), made.end());
+    for (uint32_t c : made) {
+        std::vector<uint16_t> w = ex[c];
+        while (w.size() > 1) {  // merge_all: lowest rank, leftmost on ties
+            uint32_t best = 0xFFFFFFFFu;
+            size_t bi = 0;
+            for (size_t i = 0; i + 1 < w.size(); ++i) {
+                const uint32_t v = rank_of(w[i], w[i + 1]);
+                if (v < best) { best = v; bi = i; }
+            }
+            if (best == 0xFFFFFFFFu) break;
+            w[bi] = (uint16_t)(best & 0xFFFFu);
+            w.erase(w.begin() + (ptrdiff_t)bi + 1);
+        }
+        if (w.size() == 1) keys.push_back({ex[c], w[0]});
+        else ++st.multi;
+    }
+    st.keys = (uint32_t)keys.size();
+    if (bits < 0) {
+        bits = 10;
+        while ((1ull << bits) * 2 < 5ull * keys.size()) ++bits;
+    }
+    const uint32_t size = 1u << bits;
+    mask = size - 1;
+    tab.assign((size_t)size * PTC_ENTRY_DWORDS, 0u);
+    auto pack = [](const std::vector<uint16_t> &s, uint32_t q[7]) {
+        for (int k = 0; k < 7; ++k) {
+            const uint32_t lo = 2 * k < (int)s.size() ? s[2 * k] : 0xFFFFu;
+            const uint32_t hi = 2 * k + 1 < (int)s.size() ? s[2 * k + 1] : 0xFFFFu;
+            q[k] = lo | (hi << 16);
+        }
+    };
+    auto hash_of = [&](const std::vector<uint16_t> &s) {
+        uint32_t q[7];
+        pack(s, q);
+        return ptc_hash((uint32_t)s.size(), q[0], q[1], q[2], q[3], q[4], q[5], q[6]);
+    };
+    // cuckoo placement over key indices (-1 = empty)
+    std::vector<int32_t> at(size, -1);
+    for (int32_t k = 0; k < (int32_t)keys.size(); ++k) {
+        int32_t cur = k;
+        uint32_t h = hash_of(keys[cur].s);
+        uint32_t s = ptc_slot1(h, mask);
+        for (int kick = 0; kick < 256 && cur >= 0; ++kick) {
+            std::swap(cur, at[s]);
+            if (cur < 0) break;
+            h = hash_of(keys[cur].s);
+            const uint32_t s1 = ptc_slot1(h, mask), s2 = ptc_slot2(h, mask);
+            s = s1 == s ? s2 : s1;
+        }
+        // cur >= 0 here: a key left without a slot is dropped (a cache, not a dictionary)
+    }
+    for (uint32_t s = 0; s < size; ++s) {
+        if (at[s] < 0) continue;
+        const Key &k = keys[at[s]];
+        uint32_t q[7];
+        pack(k.s, q);
+        uint32_t *e = &tab[(size_t)s * PTC_ENTRY_DWORDS];
+        e[0] = (e[0] & PTC_FLAG) | (k.id & 0xFFFFu) | ((uint32_t)k.s.size() << 16);
+        for (int i = 0; i < 7; ++i) e[1 + i] = q[i];
+        ++st.stored;
+        const uint32_t h = hash_of(k.s);
+        if (ptc_slot1(h, mask) != s) tab[(size_t)ptc_slot1(h, mask) * PTC_ENTRY_DWORDS] |= PTC_FLAG;
+    }
 }
 
 struct SpmTables {

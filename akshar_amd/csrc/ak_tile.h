@@ -23,13 +23,19 @@
 // no ticket: on MI355X every inter-unit hop would be a cross-XCD L2 round trip.
 // Reference semantics: normalize.py:117-148, tokenizer.py:167-193, cli.py:276-299.
 #pragma once
+#include <stddef.h>
+
 #include "ak_dev.h"
+#include "ak_ptc.h"
 #include "ak_rows.h"
 #include "ak_wave.h"
 
 namespace ak {
 
-constexpr int T_BCAP = 768;   // staged bytes per tile (rows past it start the next sub-tile)
+#ifndef AK_T_BCAP
+#define AK_T_BCAP 768
+#endif
+constexpr int T_BCAP = AK_T_BCAP;  // staged bytes per tile (rows past it start the next sub-tile)
 constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
 #ifndef AK_TILE_UNIT
 #define AK_TILE_UNIT 64
@@ -48,7 +54,7 @@ constexpr int WREG = 16;                // pre-tokens up to WREG-1 symbols take 
 // pre-tokens of >= 2 symbols one tile may hold for pass B (their starts share V with the rank rows);
 // a tile with more (never in text: 240 two-symbol pre-tokens in 768 bytes) sends its rows to the
 // fallback kernels
-constexpr int T_SCAP = 240;
+constexpr int T_SCAP = T_BCAP * 5 / 16;
 
 struct TileWaveMem {
     alignas(16) uint8_t bytes[T_BCAP + 32];
@@ -57,9 +63,11 @@ struct TileWaveMem {
     uint8_t fb[T_MAXR];          // row goes to the fallback kernels
     uint16_t rowend[T_MAXR];     // row's end in the staged bytes
     uint32_t rowop[T_MAXR + 1];  // row's first position in the tile's id stream
-    uint64_t passacc[10];        // PassClock accumulators (ak_profile_tile_passes)
+    uint64_t passacc[15];        // PassClock accumulators + counters (ak_profile_tile_passes / _counters)
     uint64_t unext;              // BPE: the unit's staging run: next free position (stage index)
     uint64_t ufbm;               // BPE: the unit's rows (bit r - u0) sent to the fallback kernels
+    uint32_t phead[8];           // BPE: the wave's merge-pool rings (pool_flush): first waiting entry
+    uint32_t pcnt[8];            // ... and entries waiting, per symbol-count class
 };
 
 struct TileArgs {
@@ -71,7 +79,9 @@ struct TileArgs {
     uint32_t *fb2_count;
     uint32_t *err;        // set if an id fell outside its row's slot (never: bytes + 2 bound)
     uint64_t *unit_fb;    // BPE: per 64-row unit, the mask of its rows sent to the fallback kernels
-    uint64_t *passprof;   // optional: device cycles per pass, summed over waves (T_NPASS entries)
+    uint64_t *passprof;   // optional: device cycles per pass summed over waves, then counters (T_NPROF entries)
+    uint4 *pool;          // BPE: the waves' merge pools (POOL_CAP entries per wave slot, ak_tile.h pool_flush)
+    uint32_t *unit_len;   // BPE: per unit, the length of its staging run (ids + STAGE_DEAD entries)
     uint32_t *next_unit;  // the work queue: next unit to take (zeroed before the launch)
     uint64_t ntiles;
     int rows;             // R
@@ -107,18 +117,22 @@ __device__ __forceinline__ uint64_t tile_next_unit(uint32_t *q, uint64_t t, uint
 }
 
 // pass profile slots (ak_profile_tile_passes)
-enum { TP_STAGE, TP_D, TP_E, TP_H, TP_P, TP_B, TP_FBC, TP_F, TP_FBE, TP_LOOP, T_NPASS };
-static_assert(T_NPASS == sizeof(TileWaveMem::passacc) / 8, "TileWaveMem::passacc");
+enum { TP_STAGE, TP_D, TP_E, TP_C, TP_P, TP_B, TP_FBC, TP_F, TP_FBE, TP_LOOP, T_NPASS };
+// event counters after the pass cycles (ak_profile_tile_counters): BPE pre-tokens probed in the
+// pre-token cache and its hits; SentencePiece words looked up in the word cache and its hits
+enum { TC_PROBES, TC_HITS, TC_BBATCH, TC_BROUNDS, TC_BLANES, T_NCTR };
+constexpr int T_NPROF = (int)T_NPASS + (int)T_NCTR;  // u64 slots of the passprof buffer
+static_assert(T_NPROF == sizeof(TileWaveMem::passacc) / 8, "TileWaveMem::passacc");
 
 struct PassClock {  // wave-uniform; the accumulators live in the wave's LDS (no registers held)
-    uint64_t *acc;     // T_NPASS entries (TileWaveMem::passacc)
+    uint64_t *acc;     // T_NPROF entries (TileWaveMem::passacc)
     uint64_t last;
     bool on;
     __device__ __forceinline__ void init(bool enabled, uint64_t *lds_acc) {
         on = enabled;
         acc = lds_acc;
         if (on && w_lane() == 0)
-            for (int i = 0; i < T_NPASS; ++i) acc[i] = 0;
+            for (int i = 0; i < T_NPROF; ++i) acc[i] = 0;
         last = on ? clock64() : 0;
     }
     __device__ __forceinline__ void mark(int k) {
@@ -127,9 +141,12 @@ struct PassClock {  // wave-uniform; the accumulators live in the wave's LDS (no
         if (w_lane() == 0) acc[k] += now - last;
         last = now;
     }
+    __device__ __forceinline__ void count(int k, uint64_t mask) {  // wave-uniform mask of events
+        if (on && w_lane() == 0) acc[T_NPASS + k] += (uint64_t)w_popc(mask);
+    }
     __device__ __forceinline__ void flush(uint64_t *dst) {
         if (!on || w_lane() != 0) return;
-        for (int i = 0; i < T_NPASS; ++i) atomicAdd((unsigned long long *)(dst + i), (unsigned long long)acc[i]);
+        for (int i = 0; i < T_NPROF; ++i) atomicAdd((unsigned long long *)(dst + i), (unsigned long long)acc[i]);
     }
 };
 
@@ -439,9 +456,236 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
     return TileRows{k, nr, S0, a0, vpos};
 }
 
+// The pre-token result cache probe (ak_ptc.h): the stored merge_all id of the pre-token whose n
+// symbols are packed in q (two per dword, 0xFFFF past n), or 0xFFFFFFFF. The whole stored sequence
+// is compared, so a hash collision is a miss.
+__device__ __forceinline__ uint32_t ptc_probe(const BpeDev &m, uint32_t n, const uint32_t q[7]) {
+    const char *cbase = (const char *)m.ptc;
+    const uint32_t h = akp::ptc_hash(n, q[0], q[1], q[2], q[3], q[4], q[5], q[6]);
+    uint32_t off = akp::ptc_slot1(h, m.ptc_mask) << 5;
+    for (int probe = 0; probe < 2; ++probe) {
+        const uint4 e = *(const uint4 *)(cbase + off);
+        bool ok = ((e.x >> 16) & 15u) == n && e.y == q[0] && e.z == q[1] && e.w == q[2];
+        if (ok && n > 6) {
+            const uint4 f = *(const uint4 *)(cbase + off + 16);
+            ok = f.x == q[3] && f.y == q[4] && f.z == q[5] && f.w == q[6];
+        }
+        if (ok) return e.x & 0xFFFFu;
+        if (!(e.x & akp::PTC_FLAG)) break;
+        off = akp::ptc_slot2(h, m.ptc_mask) << 5;
+    }
+    return 0xFFFFFFFFu;
+}
+
+#ifndef AK_KNOCKOUT
+#define AK_KNOCKOUT 0  // timing experiments only (wrong ids): 1 no merges, 2 set-up without rounds
+#endif
+
+// The wave's merge pool (pass A / pool_flush): misses of < WREG symbols from any tile of the wave's
+// units wait in per-wave rings in global memory, one ring per class of symbol count, until 64 of a
+// class are there; those merge as one batch with every lane busy and, the class being narrow, with
+// lanes that need about as many rounds and set-up lookups as each other (a batch runs as many
+// rounds as its longest merge); what is left merges when the wave leaves. A batch reads each
+// miss's symbols back from the unit run where pass F wrote them, merges them in LDS rows, writes
+// the merged ids back in place (merged-away positions become STAGE_DEAD) and subtracts the
+// merged-away count from the row's count (one atomic per lane).
+#ifndef AK_POOL_NCLASS
+#define AK_POOL_NCLASS 1
+#endif
+constexpr int POOL_NCLASS = AK_POOL_NCLASS;    // 8: symbol counts 2, 3, 4, 5, 6, 7, 8-9, 10-15; 4: 2-3, 4-5, 6-8, 9-15
+constexpr uint32_t POOL_RING = 320;            // a class ring holds < 64 waiting + a tile's misses (T_SCAP)
+constexpr uint32_t POOL_CAP = POOL_NCLASS * POOL_RING;  // entries per wave slot
+constexpr uint32_t STAGE_DEAD = 0xFFFFFFFFu;   // stage entry of a merged-away symbol (the copy drops it)
+static_assert(POOL_NCLASS == 1 || POOL_NCLASS == 4 || POOL_NCLASS == 8, "pool classes");
+__device__ __forceinline__ uint32_t pool_class(uint32_t n) {
+    if (POOL_NCLASS == 1) return 0u;
+    if (POOL_NCLASS == 4) return n <= 3u ? 0u : n <= 5u ? 1u : n <= 8u ? 2u : 3u;
+    return n <= 7u ? n - 2u : (n <= 9u ? 6u : 7u);
+}
+
+// loads of data this wave stored earlier in the kernel: served by L2 (a plain load could hit a line
+// this CU's L1 cached before the store); the stores have completed (pool_flush waits for them)
+__device__ __forceinline__ uint4 load_l2(const uint4 *p) {
+#ifdef AK_HOST_EMU
+    return *p;
+#else
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+#endif
+}
+__device__ __forceinline__ uint32_t load_l2(const uint32_t *p) {
+#ifdef AK_HOST_EMU
+    return *p;
+#else
+    return __builtin_nontemporal_load(p);
+#endif
+}
+
+// merge_all rounds over the lanes' LDS rows: sym = the lane's symbols (u16, < WREG), rk16 = its pair
+// values (u16 new ids, 0xFFFF = no merge; new ids increase with rank, checked at load), alive = its
+// live positions. One round = 2 ds_read_b128 + a packed-u16 min tree + the leftmost position of
+// the minimum + two cuckoo lookups for the new neighbours + 5 u16 writes; rounds run until no lane
+// can merge.
+__device__ __forceinline__ void merge_rounds(const BpeDev &m, uint16_t *sym, uint16_t *rk16, uint32_t &alive,
+                                             PassClock &pc) {
+    for (;;) {
+        if (AK_KNOCKOUT == 2) break;
+        uint32_t e[WREG / 2];
+        {
+            const uint4 *r4 = (const uint4 *)rk16;
+            const uint4 x0 = r4[0], x1 = r4[1];
+            e[0] = x0.x; e[1] = x0.y; e[2] = x0.z; e[3] = x0.w; e[4] = x1.x; e[5] = x1.y; e[6] = x1.z; e[7] = x1.w;
+        }
+        // packed-u16 min as a tree (no dependent VOP3P chain)
+        const uint32_t m01 = pk_min_u16(e[0], e[1]), m23 = pk_min_u16(e[2], e[3]);
+        const uint32_t m45 = pk_min_u16(e[4], e[5]), m67 = pk_min_u16(e[6], e[7]);
+        const uint32_t mv = pk_min_u16(pk_min_u16(m01, m23), pk_min_u16(m45, m67));
+        const uint32_t minv = (mv & 0xFFFFu) < (mv >> 16) ? (mv & 0xFFFFu) : (mv >> 16);
+        const bool mg = minv != 0xFFFFu;
+        if (!w_ballot(mg)) break;
+        if (pc.on) {
+            pc.count(TC_BROUNDS, 1);
+            pc.count(TC_BLANES, w_ballot(mg));
+        }
+        if (mg) {
+            // leftmost position of minv, in packed u16 arithmetic (no per-position compare-to-mask /
+            // select): key = (value != minv) * 16 + position, min over all
+            const uint32_t mm = minv * 0x10001u;
+            uint32_t one = 0x00010001u;  // opaque: else the compiler folds min(x, 1) * 16 back into selects
+#ifndef AK_HOST_EMU
+            asm volatile("" : "+v"(one));
+#endif
+            uint32_t kk[WREG / 2];
+#pragma unroll
+            for (int k = 0; k < WREG / 2; ++k)
+                kk[k] = pk_mad_u16(pk_min_u16(e[k] ^ mm, one), 0x00100010u, (uint32_t)(2 * k) | ((uint32_t)(2 * k + 1) << 16));
+            const uint32_t k01 = pk_min_u16(kk[0], kk[1]), k23 = pk_min_u16(kk[2], kk[3]);
+            const uint32_t k45 = pk_min_u16(kk[4], kk[5]), k67 = pk_min_u16(kk[6], kk[7]);
+            const uint32_t kmin = pk_min_u16(pk_min_u16(k01, k23), pk_min_u16(k45, k67));
+            const int bi = (int)(((kmin & 0xFFFFu) < (kmin >> 16) ? kmin : (kmin >> 16)) & 15u);
+            const uint32_t after = alive >> (bi + 1);
+            const int jn = bi + 1 + __builtin_ctz(after);  // the right symbol of the pair
+            const uint32_t below = alive & ((1u << bi) - 1u);
+            const int pl = below ? 31 - __builtin_clz(below) : -1;
+            const uint32_t aj = jn + 1 < 32 ? alive >> (jn + 1) : 0u;
+            const int q = aj ? jn + 1 + __builtin_ctz(aj) : -1;
+            const uint32_t left = pl >= 0 ? sym[pl] : 0u;
+            const uint32_t right = q >= 0 ? sym[q] : 0u;
+            sym[bi] = (uint16_t)minv;
+            alive &= ~(1u << jn);
+            const uint32_t L = pl >= 0 ? merge_lookup_c(m, left, minv) & 0xFFFFu : 0xFFFFu;
+            const uint32_t R = q >= 0 ? merge_lookup_c(m, minv, right) & 0xFFFFu : 0xFFFFu;
+            if (pl >= 0) rk16[pl] = (uint16_t)L;
+            rk16[bi] = (uint16_t)R;
+            rk16[jn] = 0xFFFFu;
+        }
+    }
+}
+
+// One merge batch of the wave's pool: the first cnt (<= 64) entries, lane l the l-th. LDS: the
+// lanes' rank rows and symbol rows (64 x 32 B each) over the tile buffers, free between tiles.
+__device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, uint4 *pool, uint32_t c, uint32_t cnt,
+                                           PassClock &pc) {
+    static_assert(offsetof(TileWaveMem, bytes) == 0 && offsetof(TileWaveMem, w) + sizeof(TileWaveMem::w) >= 2 * 64 * 2 * WREG,
+                  "rank rows + symbol rows fit the tile buffers");
+    const BpeDev &m = ta.ra.bpe;
+    const int lane = w_lane();
+    const bool act = (uint32_t)lane < cnt;
+    uint16_t *rk16 = (uint16_t *)((uint8_t *)&M + lane * (2 * WREG));
+    uint16_t *sym = (uint16_t *)((uint8_t *)&M + 64 * 2 * WREG + lane * (2 * WREG));
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage / count / pool stores have landed
+#endif
+    uint4 *ring = pool + c * POOL_RING;
+    const uint32_t head = w_bcast(M.phead[c], 0);
+    const uint4 e = act ? load_l2(ring + (head + (uint32_t)lane) % POOL_RING) : make_uint4(0, 0, 0, 0);
+    const uint64_t dst = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32);
+    const int n = act ? (int)(e.y >> 16) : 0;
+    const uint32_t row = e.z;
+    uint32_t *sp = (uint32_t *)ta.ra.out + dst;
+    uint32_t p[WREG / 2];  // the symbols as u16 pairs (0xFFFF past n)
+    {
+        const uint4 *s4 = (const uint4 *)sp;  // dword-aligned 16-byte loads (the stage is padded past every run)
+#pragma unroll
+        for (int k = 0; k < WREG / 4; ++k) {
+            const uint4 v = act ? load_l2(s4 + k) : make_uint4(0, 0, 0, 0);
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 4 * k + 2 * h;
+                p[2 * k + h] = (i < n ? x[2 * h] : 0xFFFFu) | ((i + 1 < n ? x[2 * h + 1] : 0xFFFFu) << 16);
+            }
+        }
+    }
+    uint32_t d[WREG / 2];
+#pragma unroll
+    for (int k = 0; k < WREG / 2; ++k) {
+        const int i = 2 * k;
+        const uint32_t a0 = p[k] & 0xFFFFu, a1 = p[k] >> 16, a2 = k + 1 < WREG / 2 ? p[k + 1] & 0xFFFFu : 0xFFFFu;
+        const uint32_t lo = i + 1 < n ? merge_lookup_c(m, a0, a1) & 0xFFFFu : 0xFFFFu;
+        const uint32_t hi = (i + 2 < WREG && i + 2 < n) ? merge_lookup_c(m, a1, a2) & 0xFFFFu : 0xFFFFu;
+        d[k] = lo | (hi << 16);
+    }
+    {  // every lane writes its rows (inactive lanes: no merges): the rounds read them unmasked
+        uint4 *r4 = (uint4 *)rk16;
+        r4[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        r4[1] = make_uint4(d[4], d[5], d[6], d[7]);
+        uint4 *s4 = (uint4 *)sym;
+        s4[0] = make_uint4(p[0], p[1], p[2], p[3]);
+        s4[1] = make_uint4(p[4], p[5], p[6], p[7]);
+    }
+    if (pc.on) pc.count(TC_BBATCH, 1);
+    uint32_t alive = act ? (1u << n) - 1u : 0u;
+    merge_rounds(m, sym, rk16, alive, pc);
+    // the merged row back in place: live symbols stay where they are, merged-away ones become dead
+    {
+        const uint4 *s4 = (const uint4 *)sym;
+#pragma unroll
+        for (int k = 0; k < WREG / 4; ++k) {
+            const uint4 pr = s4[k / 2];
+            const uint32_t w0 = (k & 1) ? pr.z : pr.x, w1 = (k & 1) ? pr.w : pr.y;
+            uint32_t o[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = 4 * k + t;
+                const uint32_t v = ((t < 2 ? w0 : w1) >> (16 * (t & 1))) & 0xFFFFu;
+                o[t] = (alive >> i) & 1u ? v : STAGE_DEAD;
+            }
+            if (4 * k + 3 < n) {
+                ((uint4 *)sp)[k] = make_uint4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 3; ++t)
+                    if (4 * k + t < n) sp[4 * k + t] = o[t];
+            }
+        }
+    }
+    const uint32_t dead = (uint32_t)n - (uint32_t)__builtin_popcount(alive);
+    if (act && dead) atomicSub(ta.counts + row, dead);
+    w_sync();
+    if (lane == 0) {
+        M.phead[c] = (head + cnt) % POOL_RING;
+        M.pcnt[c] -= cnt;
+    }
+    w_sync();
+}
+
+// merge every class ring holding >= minc misses, 64 at a time (minc = 1 at the wave's end: all)
+__device__ __forceinline__ void pool_drain(const TileArgs &ta, TileWaveMem &M, uint4 *pool, uint32_t minc, PassClock &pc) {
+#pragma unroll 1
+    for (uint32_t c = 0; c < (uint32_t)POOL_NCLASS; ++c) {
+        for (;;) {
+            const uint32_t k = w_bcast(M.pcnt[c], 0);
+            if (k < minc || k == 0) break;
+            pool_flush(ta, M, pool, c, k < 64u ? k : 64u, pc);
+        }
+    }
+}
+
 template <int FLAGS>
-__device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *sfast,
-                        TileWaveMem &M, PassClock &pc) {
+__device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *sfast,
+                        TileWaveMem &M, uint4 *pool, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
@@ -566,95 +810,72 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     w_sync();
 
     pc.mark(TP_P);
-    // ---------------- pass B: lane per pre-token, merge_all (lowest rank, leftmost on ties).
-    // Pre-tokens of < WREG symbols: the symbols stay in place in W (merged-away slots become
-    // V_DEAD, an alive-slot bitmask finds neighbours), the pair values live in a per-lane 32-byte
-    // LDS row of u16 new ids (bytes + bottom of V; new ids increase with rank: checked at load, so
-    // the smallest id is the lowest rank). One round = 2 ds_read_b128 + a packed-u16 min + two
-    // cuckoo lookups for the new neighbours + 3 u16 writes. Longer pre-tokens merge in LDS.
+    // ---------------- pass C: lane per listed pre-token: the pre-token result cache (ak_ptc.h) and
+    // the miss list. A hit takes its stored id (its merge_all result) at its start and V_DEAD over
+    // its other symbols (pass F skips those). The misses are listed in order in the staged-bytes
+    // area (dead after D) as st | n << 10, n = 0 for pre-tokens of >= WREG symbols.
+    static_assert(T_E <= 1024 && 2 * T_SCAP <= T_BCAP, "miss list entries st | n << 10 in the staged bytes");
+    static_assert(T_BCAP + 2 * T_MAXR + 1 <= T_E + 16 - 64, "W's dummy slots overlap the id stream");
+    uint16_t *mlist = (uint16_t *)M.bytes;
+    uint32_t nm = 0, nlong = 0;
     {
-        // 64 rank rows fit bytes + the part of V below the kept starts (at most T_SCAP of them)
-        static_assert(64 * 2 * WREG <= (T_BCAP + 32) + 2 * (T_E - T_SCAP), "rank rows overlap the starts");
-        uint16_t *rk16 = (uint16_t *)(M.bytes + lane * (2 * WREG));
+        uint16_t *dummy = (uint16_t *)M.w + (T_E + 16 - 64) + lane;  // past every pre-token (W's pad)
         for (uint32_t wb = 0; wb < nw; wb += 64) {
             const uint32_t j = wb + lane;
             const bool act = j < nw;
             const int st = act ? (int)M.v[T_E - 1 - j] : 0;
-            uint32_t sy[WREG];
+            uint32_t s[WREG];
 #pragma unroll
-            for (int i = 0; i < WREG; ++i) sy[i] = (act && st + i < (int)wlen) ? M.w[st + i] : 0xFFFFu;
+            for (int i = 0; i < WREG; ++i) s[i] = (act && st + i < (int)wlen) ? M.w[st + i] : 0xFFFFu;
             int n = WREG;
 #pragma unroll
-            for (int i = WREG - 1; i >= 1; --i) n = (sy[i] & WSTART) ? i : n;
-            const bool reg = act && n < WREG;
-            int len = n;  // long pre-tokens: measured before any lane writes W back
-            if (act && !reg)
+            for (int i = WREG - 1; i >= 1; --i) n = (s[i] & WSTART) ? i : n;
+            uint32_t res = 0xFFFFFFFFu;
+            if (m.ptc != nullptr) {  // uniform
+                uint32_t q[7];
+#pragma unroll
+                for (int k = 0; k < 7; ++k) {
+                    const uint32_t lo = 2 * k < n ? (s[2 * k] & 0x7FFFu) : 0xFFFFu;
+                    const uint32_t hi = 2 * k + 1 < n ? s[2 * k + 1] : 0xFFFFu;
+                    q[k] = lo | (hi << 16);
+                }
+                if (act && n <= akp::PTC_MAXN) res = ptc_probe(m, (uint32_t)n, q);
+            }
+            const bool hit = res != 0xFFFFFFFFu;
+            if (hit) M.w[st] = (uint16_t)(res | WSTART);
+            for (int i = 1; i < akp::PTC_MAXN; ++i) {
+                const bool wr = hit && i < n;
+                if (!w_ballot(wr)) break;
+                *(wr ? &M.w[st + i] : dummy) = V_DEAD;
+            }
+            const bool miss = act && !hit;
+            const uint64_t MM = w_ballot(miss);
+            if (miss) mlist[nm + w_rank(MM)] = (uint16_t)(st | ((n < WREG ? n : 0) << 10));
+            nm += (uint32_t)w_popc(MM);
+            nlong += (uint32_t)w_popc(w_ballot(miss && n >= WREG));
+            if (pc.on && m.ptc != nullptr) {
+                pc.count(TC_PROBES, w_ballot(act));
+                pc.count(TC_HITS, w_ballot(hit));
+            }
+        }
+        w_sync();
+    }
+
+    pc.mark(TP_C);
+    if (AK_KNOCKOUT == 1) nm = nlong = 0;
+    // ---------------- pass B: pre-tokens of >= WREG symbols (rare) merge here, in LDS (bpe_merge_lds,
+    // one lane each). Every shorter miss goes to the wave's merge pool after pass F (pass A).
+    if (nlong) {
+        for (uint32_t wb = 0; wb < nm; wb += 64) {
+            const uint32_t j = wb + lane;
+            const uint32_t e = j < nm ? mlist[j] : 1u << 10;
+            const bool lng = (e >> 10) == 0;
+            const int st = (int)(e & 1023u);
+            int len = WREG;
+            if (lng)
                 while (st + len < (int)wlen && !(M.w[st + len] & WSTART)) ++len;
-            uint32_t d[WREG / 2];
-#pragma unroll
-            for (int k = 0; k < WREG / 2; ++k) {
-                const int i = 2 * k;
-                const uint32_t lo = (reg && i + 1 < n) ? merge_lookup_c(m, sy[i] & 0x7FFFu, sy[i + 1]) & 0xFFFFu : 0xFFFFu;
-                const uint32_t hi = (i + 2 < WREG && reg && i + 2 < n) ? merge_lookup_c(m, sy[i + 1], sy[(i + 2) % WREG]) & 0xFFFFu : 0xFFFFu;
-                d[k] = lo | (hi << 16);
-            }
-            w_sync();  // every lane has read V and its window before rank rows overwrite bytes / V
-            {  // every lane writes its rank row (all 0xFFFF unless reg): the merge rounds read it unmasked
-                uint4 *r4 = (uint4 *)rk16;
-                r4[0] = make_uint4(d[0], d[1], d[2], d[3]);
-                r4[1] = make_uint4(d[4], d[5], d[6], d[7]);
-            }
-            if (reg) M.w[st] = (uint16_t)(sy[0] & 0x7FFFu);
-            uint32_t alive = reg ? (1u << n) - 1u : 0u;
-            for (;;) {
-                uint32_t e[WREG / 2];
-                {
-                    const uint4 *r4 = (const uint4 *)rk16;
-                    const uint4 x0 = r4[0], x1 = r4[1];
-                    e[0] = x0.x; e[1] = x0.y; e[2] = x0.z; e[3] = x0.w; e[4] = x1.x; e[5] = x1.y; e[6] = x1.z; e[7] = x1.w;
-                }
-                // packed-u16 min as a tree (no dependent VOP3P chain)
-                const uint32_t m01 = pk_min_u16(e[0], e[1]), m23 = pk_min_u16(e[2], e[3]);
-                const uint32_t m45 = pk_min_u16(e[4], e[5]), m67 = pk_min_u16(e[6], e[7]);
-                const uint32_t mv = pk_min_u16(pk_min_u16(m01, m23), pk_min_u16(m45, m67));
-                const uint32_t minv = (mv & 0xFFFFu) < (mv >> 16) ? (mv & 0xFFFFu) : (mv >> 16);
-                const bool mg = minv != 0xFFFFu;
-                if (!w_ballot(mg)) break;
-                if (mg) {
-                    // leftmost position of minv, in packed u16 arithmetic (no per-position
-                    // compare-to-mask / select): key = (value != minv) * 16 + position, min over all
-                    const uint32_t mm = minv * 0x10001u;
-                    uint32_t one = 0x00010001u;  // opaque: else the compiler folds min(x, 1) * 16 back into selects
-#ifndef AK_HOST_EMU
-                    asm volatile("" : "+v"(one));
-#endif
-                    uint32_t kk[WREG / 2];
-#pragma unroll
-                    for (int k = 0; k < WREG / 2; ++k)
-                        kk[k] = pk_mad_u16(pk_min_u16(e[k] ^ mm, one), 0x00100010u, (uint32_t)(2 * k) | ((uint32_t)(2 * k + 1) << 16));
-                    const uint32_t k01 = pk_min_u16(kk[0], kk[1]), k23 = pk_min_u16(kk[2], kk[3]);
-                    const uint32_t k45 = pk_min_u16(kk[4], kk[5]), k67 = pk_min_u16(kk[6], kk[7]);
-                    const uint32_t kmin = pk_min_u16(pk_min_u16(k01, k23), pk_min_u16(k45, k67));
-                    const int bi = (int)(((kmin & 0xFFFFu) < (kmin >> 16) ? kmin : (kmin >> 16)) & 15u);
-                    const uint32_t after = alive >> (bi + 1);
-                    const int jn = bi + 1 + __builtin_ctz(after);  // the right symbol of the pair
-                    const uint32_t below = alive & ((1u << bi) - 1u);
-                    const int pl = below ? 31 - __builtin_clz(below) : -1;
-                    const uint32_t aj = jn + 1 < 32 ? alive >> (jn + 1) : 0u;
-                    const int q = aj ? jn + 1 + __builtin_ctz(aj) : -1;
-                    const uint32_t left = pl >= 0 ? M.w[st + pl] : 0u;
-                    const uint32_t right = q >= 0 ? M.w[st + q] : 0u;
-                    M.w[st + bi] = (uint16_t)minv;
-                    M.w[st + jn] = V_DEAD;
-                    alive &= ~(1u << jn);
-                    const uint32_t L = pl >= 0 ? merge_lookup_c(m, left, minv) & 0xFFFFu : 0xFFFFu;
-                    const uint32_t R = q >= 0 ? merge_lookup_c(m, minv, right) & 0xFFFFu : 0xFFFFu;
-                    if (pl >= 0) rk16[pl] = (uint16_t)L;
-                    rk16[bi] = (uint16_t)R;
-                    rk16[jn] = 0xFFFFu;
-                }
-            }
-            if (act && !reg) {  // long pre-token: merge in LDS
+            w_sync();  // every lane has measured its pre-token before any start bit is cleared
+            if (lng) {
                 M.w[st] &= 0x7FFFu;
                 (void)bpe_merge_lds(m, M.w, st, len);
             }
@@ -677,8 +898,11 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     }
 
     pc.mark(TP_FBC);
-    // ---------------- pass F: ids -> the unit's staging run (back to back after the unit's earlier
-    // tiles); row start positions -> per-row counts
+    // ---------------- pass F: symbols and ids -> the unit's staging run (back to back after the unit's
+    // earlier tiles; a pooled miss's symbols are merged in place later, merged-away ones become
+    // STAGE_DEAD, which the copy drops); row start positions -> per-row counts (pooled merges
+    // subtract theirs); each W position's place in the run (op | row << 12, 0xFFFF = not written)
+    // -> V for pass A
     const uint64_t sbase = M.unext;
     uint32_t *stage = (uint32_t *)a.out + sbase;
     const uint64_t scap = a.cap > sbase ? a.cap - sbase : 0;
@@ -696,6 +920,7 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const uint64_t EM = w_ballot(emit);
         const uint32_t op = pos + w_rank(EM);
         if (isrow) M.rowop[rs + w_rank(RM)] = op;  // read after the loop (counts)
+        if (in) M.v[kk] = emit ? (uint16_t)(op | (row << 12)) : (uint16_t)0xFFFFu;
         if (emit) {
             const uint64_t d = op;
             const uint32_t val = x == V_B ? m.bos : x == V_E ? m.eos : (uint32_t)(x & 0x7FFFu);
@@ -713,31 +938,71 @@ __device__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         ta.counts[r0 + lane] = M.rowop[lane + 1] - M.rowop[lane];
         if (a.row_status) a.row_status[r0 + lane] = 0;
     }
-    w_sync();
     pc.mark(TP_F);
+
+    // ---------------- pass A: the misses of < WREG symbols in rows not sent to the fallback kernels
+    // join the wave's merge pool as {stage index of the first symbol, n << 16, row} in the ring of
+    // their symbol-count class; then every 64 of a class merge as one batch (pool_drain /
+    // pool_flush), so the merge rounds run with all lanes busy and about equally long whatever the
+    // tile.
+    static_assert(POOL_RING >= 63 + T_SCAP, "a class ring holds < 64 waiting + a tile's misses");
+    for (uint32_t wb = 0; wb < nm; wb += 64) {
+        const uint32_t j = wb + lane;
+        const uint32_t e = j < nm ? mlist[j] : 0u;
+        const uint32_t n = e >> 10;
+        const uint32_t at = n ? M.v[e & 1023u] : 0xFFFFu;
+        const bool ok = at != 0xFFFFu;
+        const uint32_t cls = ok ? pool_class(n) : 0xFFu;
+        const uint64_t dst = sbase + (at & 0xFFFu);
+        const uint4 ent = make_uint4((uint32_t)dst, (uint32_t)(dst >> 32) | (n << 16), (uint32_t)(r0 + (at >> 12)), 0u);
+#pragma unroll 1
+        for (uint32_t c = 0; c < (uint32_t)POOL_NCLASS; ++c) {
+            const uint64_t CM = w_ballot(cls == c);
+            if (!CM) continue;
+            const uint32_t head = w_bcast(M.phead[c], 0), k = w_bcast(M.pcnt[c], 0);
+            if (cls == c) pool[c * POOL_RING + (head + k + w_rank(CM)) % POOL_RING] = ent;
+            w_sync();
+            if (lane == 0) M.pcnt[c] = k + (uint32_t)w_popc(CM);
+            w_sync();
+        }
+    }
+    pool_drain(ta, M, pool, 64u, pc);
+    pc.mark(TP_FBE);
     return nr;
 }
 
 template <int FLAGS>
-__device__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *sfast, TileWaveMem &M,
+__device__ __forceinline__ void bpe_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *sfast, TileWaveMem &M,
                                uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
+    uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_CAP;  // this wave's class rings
+    if (w_lane() < POOL_NCLASS) {
+        M.phead[w_lane()] = 0;
+        M.pcnt[w_lane()] = 0;
+    }
+    w_sync();
     // units of TILE_UNIT rows from the work queue (tile_first_unit); inside a unit, each tile
     // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
     for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;
-        if (w_lane() == 0) {  // the unit's staging run starts at its rows' slot base offs[r0] + 2 r0
-            M.unext = ta.ra.offs[r0] + 2 * r0;
+        const uint64_t run0 = ta.ra.offs[r0] + 2 * r0;  // the unit's staging run starts at its rows' slot base
+        if (w_lane() == 0) {
+            M.unext = run0;
             M.ufbm = 0;
         }
         w_sync();
         for (uint64_t r = r0; r < r1;)
-            r += (uint64_t)bpe_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, sfast, M, pc);
-        if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
+            r += (uint64_t)bpe_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, sfast, M, pool, pc);
+        if (w_lane() == 0) {
+            ta.unit_fb[t] = M.ufbm;
+            ta.unit_len[t] = (uint32_t)(M.unext - run0);
+        }
     }
+    pool_drain(ta, M, pool, 1u, pc);  // the rest: every miss merged before the wave leaves
+    pc.mark(TP_FBE);
     pc.flush(ta.passprof);
 }
 

@@ -53,7 +53,7 @@ struct RowsWaveMem {
     uint8_t fb[T_MAXR];
     uint16_t rowend[T_MAXR];
     uint32_t base[4][T_MAXR + 1];  // per row: kept chars / norm bytes / cluster ends / runs before it
-    uint64_t passacc[10];
+    uint64_t passacc[T_NPROF];
     uint64_t un_norm, un_seg, un_runs;  // the unit's staging runs: next free element of each output
     uint64_t ufbm;                      // the unit's rows (bit r - u0) sent to the fallback kernels
 };

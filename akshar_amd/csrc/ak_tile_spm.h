@@ -64,7 +64,7 @@ struct SpmWaveMem {
     uint16_t wfirst[T_MAXR + 1];             // index of each row's first word (+ end)
     uint32_t rowcnt[T_MAXR];
     uint32_t rowfirst[T_MAXR];               // tile-stream position of the row's first id
-    uint64_t passacc[10];
+    uint64_t passacc[T_NPROF];
     uint64_t unext;                          // the unit's staging run: next free position
     uint64_t ufbm;                           // the unit's rows (bit r - u0) sent to the fallback kernels
 };

@@ -87,6 +87,9 @@ inline unsigned long long atomicAdd(unsigned long long *p, unsigned long long v)
 inline uint32_t atomicAdd(uint32_t *p, uint32_t v) {
     return reinterpret_cast<std::atomic<uint32_t> *>(p)->fetch_add(v, std::memory_order_relaxed);
 }
+inline uint32_t atomicSub(uint32_t *p, uint32_t v) {
+    return reinterpret_cast<std::atomic<uint32_t> *>(p)->fetch_sub(v, std::memory_order_relaxed);
+}
 
 #else
 #include <hip/hip_runtime.h>

@@ -294,6 +294,13 @@ class BPE:
         check(_lib.lib().ak_bpe_set_vocab(h, len(toks), tb.ctypes.data, to.ctypes.data, sp.ctypes.data),
               "ak_bpe_set_vocab")
 
+    def cache_info(self):
+        """The pre-token result cache (include/akshar.h ak_bpe_cache_info): slots, keys found, keys
+        stored, merged-token sequences whose merge_all is not one id."""
+        info = (ctypes.c_uint64 * 4)()
+        check(_lib.lib().ak_bpe_cache_info(self.h, info), "ak_bpe_cache_info")
+        return {"slots": info[0], "keys": info[1], "stored": info[2], "multi": info[3]}
+
     @classmethod
     def load(cls, path, dev=None):
         """The device model read by the library itself (ak_bpe_load: tokenizer.json parsed in C++, as
@@ -437,6 +444,18 @@ def profile_tile_passes(dev=None):
         check(k, "ak_profile_tile_passes")
     tot = float(sum(buf)) or 1.0
     return {name: round(buf[i] / tot, 4) for i, name in enumerate(_lib.AK_TILE_PASSES)} if k else {}
+
+
+def profile_tile_counters(dev=None):
+    """Event counters of the instrumented tile launches since the last call (include/akshar.h
+    ak_profile_tile_counters): pre-token cache probes / hits, merge batches / rounds / lane-rounds."""
+    ws = workspace(dev)
+    names = ("ptc_probes", "ptc_hits", "merge_batches", "merge_rounds", "merge_lane_rounds")
+    buf = (ctypes.c_uint64 * len(names))()
+    k = _lib.lib().ak_profile_tile_counters(ws, buf, len(names))
+    if k < 0:
+        check(k, "ak_profile_tile_counters")
+    return {nm: int(buf[i]) for i, nm in enumerate(names[:k])}
 
 
 def fallback_rows(dev=None):

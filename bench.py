@@ -284,15 +284,23 @@ def roofline_of(prof, kern, steps, rows, nbytes, n_ids):
     return r
 
 
-def pass_split(engine, fn, dev):
+def pass_split(engine, fn, dev, counters=None):
     """Per-pass wave-cycle split of the tile kernel from ONE extra, untimed launch with the pass
-    clocks on (they instrument the kernel, so the timed steps run without them)."""
+    clocks on (they instrument the kernel, so the timed steps run without them); `counters` (a dict)
+    receives the same launch's event counters (BPE pre-token cache probes and hits)."""
     engine.profile_enable(True, passes=True)
     engine.profile_tile_passes(dev)  # reset the accumulators
+    engine.profile_tile_counters(dev)
     fn()
     torch.cuda.synchronize()
     passes = engine.profile_tile_passes(dev)
+    ctr = engine.profile_tile_counters(dev)
     engine.profile_enable(False)
+    if counters is not None and ctr.get("ptc_probes"):
+        counters.update({"probes_per_step": ctr["ptc_probes"], "hits_per_step": ctr["ptc_hits"],
+                         "hit_rate": round(ctr["ptc_hits"] / ctr["ptc_probes"], 4),
+                         "source": "the pass-clock step's counters (ak_profile_tile_counters): multi-symbol "
+                                   "pre-tokens probed in the pre-token result cache, and its hits"})
     return passes
 
 
@@ -468,7 +476,8 @@ def main():
     prof = engine.profile_read()
     engine.profile_enable(False)
     fb_rows = engine.fallback_rows(local)
-    passes = pass_split(engine, step, local) if world == 1 else {}  # step() of N > 1 holds a collective
+    ptc = {}
+    passes = pass_split(engine, step, local, ptc) if world == 1 else {}  # step() of N > 1 holds a collective
 
     if dist:
         t = torch.tensor([elapsed, gather_s[0]], dtype=torch.float64, device=cdev)
@@ -497,6 +506,8 @@ def main():
         roofline["tile_pass_cycle_frac"] = passes
         roofline["tile_pass_source"] = "one extra untimed step with the pass clocks on"
     roofline["fallback_rows_per_step"] = fb_rows[0]
+    if ptc:
+        roofline["pretoken_cache"] = ptc
 
     others = e2e = cpu = c5 = None
     if rank == 0 and world == 1 and not cfg5 and not args.no_cfg5:

@@ -103,6 +103,12 @@ int ak_ws_check(ak_ws *ws);
 int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const uint32_t *single_id,
                   uint32_t n_merges, const uint32_t *merges, uint32_t bos, uint32_t eos, ak_bpe **out);
 void ak_bpe_free(ak_bpe *m);
+/* The tile path's pre-token result cache, built by ak_bpe_create (HF BPE's per-word cache,
+ * tokenizer.py:96-97,193, made exact at load: keys are the char-id sequences of merged tokens whose
+ * merge_all is that one id). info[0] table slots (0 = no cache: not a tile-path model, or AK_PTC=0
+ * in the environment), [1] keys found, [2] keys stored, [3] merged-token sequences whose merge_all is
+ * not one id (never stored). */
+int ak_bpe_cache_info(const ak_bpe *m, uint64_t info[4]);
 /* The tokenizer's added tokens (tokenizer.json "added_tokens": <pad> <unk> <s> </s> <mask> for
  * cli.py:283-285), all normalized=false / lstrip=rstrip=single_word=false: HF's AddedVocabulary
  * splits the text it receives on them (leftmost-longest) BEFORE the NFKC normalizer, each match
@@ -208,11 +214,18 @@ int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each
  * pass of the tile-cooperative BPE kernel since the last call, while profiling level 2 is on. Slots:
  * 0 byte staging, 1 decode + NFC check + map/filter, 2 fused elongation + HF NFKC + pre-tokenizer,
- * 3 (unused), 4 pre-token start list, 5 BPE merges, 6 fallback-list append, 7 ids into the unit run +
+ * 3 pre-token cache probes, 4 pre-token start list, 5 BPE merges, 6 fallback-list append, 7 ids into the unit run +
  * counts, 8 (unused), 9 loop overhead.
  * Returns the number of slots written (0 if the tile kernel has not run), or a negative error. */
 #define AK_TILE_NPASS 10
 int ak_profile_tile_passes(ak_ws *ws, uint64_t *cycles, int n);
+/* Event counters of the same instrumented launches (profiling level 2), reset by each call:
+ * [0] BPE pre-tokens probed in the pre-token cache (slot 3 of the pass breakdown), [1] its hits,
+ * [2] merge batches (64 pre-tokens a wave merges at once), [3] merge rounds, [4] lanes merging, summed
+ * over rounds (lane utilisation of the merge loop = [4] / (64 [3])).
+ * Returns the number of counters written (0 if no tile kernel has run), or a negative error. */
+#define AK_TILE_NCOUNTERS 5
+int ak_profile_tile_counters(ak_ws *ws, uint64_t *counts, int n);
 
 /* Decode (tokenizer.py:195-219): rows of ids (u32, id_offs[n+1]) -> UTF-8 text
  * rows (out, out_offs[n+1]; out_offs[n] = required total even when cap is short).

@@ -23,6 +23,8 @@ using namespace ak;
 
 struct EmuModel {
     akb::BpeTables bpe;
+    std::vector<uint32_t> ptc;  // pre-token result cache (ak_ptc.h)
+    akb::PtcStats ptc_stats;
     akb::SpmTables spm;
     BpeDev bdev{};
     SpmDev sdev{};
@@ -44,7 +46,40 @@ extern "C" void *emu_bpe_create(uint32_t n_single, const uint32_t *cp, const uin
     m->bdev.n_single = m->bpe.n_rest;
     m->bdev.bos = bos;
     m->bdev.eos = eos;
+    // the pre-token result cache as ak_bpe_create builds it (emu_bpe_set_ptc rebuilds or drops it)
+    m->bdev.ptc = nullptr;
+    uint32_t mask = 0;
+    akb::build_bpe_ptc(n_single, id, n_merges, merges, -1, m->ptc, mask, m->ptc_stats);
+    m->bdev.ptc = m->ptc.data();
+    m->bdev.ptc_mask = mask;
     return m;
+}
+
+// bits: -2 no cache, -1 sized from the key count, >= 0 forces 2^bits slots; info[4] as ak_bpe_cache_info
+extern "C" void emu_bpe_set_ptc(void *model, int bits, uint32_t n_single, const uint32_t *id, uint32_t n_merges,
+                                const uint32_t *merges, uint64_t *info) {
+    EmuModel *m = (EmuModel *)model;
+    m->ptc.clear();
+    m->bdev.ptc = nullptr;
+    m->bdev.ptc_mask = 0;
+    m->ptc_stats = akb::PtcStats{};
+    if (bits >= -1) {
+        uint32_t mask = 0;
+        akb::build_bpe_ptc(n_single, id, n_merges, merges, bits, m->ptc, mask, m->ptc_stats);
+        m->bdev.ptc = m->ptc.data();
+        m->bdev.ptc_mask = mask;
+    }
+    info[0] = m->bdev.ptc ? (uint64_t)m->bdev.ptc_mask + 1 : 0;
+    info[1] = m->ptc_stats.keys;
+    info[2] = m->ptc_stats.stored;
+    info[3] = m->ptc_stats.multi;
+}
+
+// a raw view of the cache table (tests: cross-check entries against an independent Python build)
+extern "C" uint64_t emu_bpe_ptc_table(void *model, const uint32_t **tab) {
+    EmuModel *m = (EmuModel *)model;
+    *tab = m->ptc.data();
+    return m->ptc.size();
 }
 
 extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t *offs, const float *scores,
@@ -165,6 +200,9 @@ thread_local EmuWave *t_wave;
 
 static uint32_t g_last_fb = 0;
 extern "C" uint32_t emu_last_fallback_rows() { return g_last_fb; }
+// the last tile launch's event counters (ak_tile.h TC_*: pre-token cache probes, hits)
+static uint64_t g_last_ctr[T_NCTR] = {};
+extern "C" void emu_last_counters(uint64_t *out) { for (int i = 0; i < T_NCTR; ++i) out[i] = g_last_ctr[i]; }
 // waves the tile entries below emulate at once (each its own 64 threads and wave memory), all taking
 // units from the one work queue as on the GPU
 static int g_waves = 1;
@@ -210,7 +248,14 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     std::vector<uint16_t> sfast(SFAST_N);
     for (uint32_t i = 0; i < SFAST_N; ++i) sfast[i] = m->bpe.fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     std::vector<TileWaveMem> M(g_waves);
+    std::vector<uint64_t> prof(T_NPROF, 0);
+    ta.passprof = prof.data();  // the pass clocks read 0 here; the counters are real
+    std::vector<uint4> pool((size_t)g_waves * POOL_CAP);
+    std::vector<uint32_t> unit_len(nunits);
+    ta.pool = pool.data();
+    ta.unit_len = unit_len.data();
     run_waves([&](int w) { bpe_tiles_wave<3>(ta, hot_tab, sfast.data(), M[w], (uint32_t)w, (uint32_t)g_waves); });
+    for (int i = 0; i < T_NCTR; ++i) g_last_ctr[i] = prof[T_NPASS + i];
     if (err) return -1;
     g_last_fb = fbn;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
@@ -237,19 +282,26 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
         counts[r] = lim ? 0 : (uint32_t)cnt;
         if (row_status) row_status[r] = (uint8_t)((sc.status & ST_BAD_UTF8) | (lim ? ST_LIMIT : 0));
     }
-    // scan + copy, as the launcher's scan_counts and k_unit_copy: each unit's non-fallback rows
-    // back to back from its run base offs[u0] + 2 u0, fallback rows from their slot in the second half
+    // scan + copy, as the launcher's scan_counts and k_unit_copy_bpe: each unit's run (unit_len
+    // entries) without its STAGE_DEAD entries is its non-fallback rows' ids back to back; fallback
+    // rows from their slot in the second half
     out_offs[0] = 0;
     for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
     for (uint64_t u = 0; u < nunits; ++u) {
         const uint64_t u0 = u * TILE_UNIT;
-        uint64_t p = offs[u0] + 2 * u0;
+        const uint64_t base = offs[u0] + 2 * u0;
+        std::vector<uint32_t> live;
+        for (uint64_t k = 0; k < unit_len[u]; ++k)
+            if (stage[base + k] != STAGE_DEAD) live.push_back(stage[base + k]);
+        uint64_t p = 0;
         for (uint64_t r = u0; r < n && r < u0 + TILE_UNIT; ++r) {
             const bool fb = (unit_fb[u] >> (r - u0)) & 1ull;
-            const uint32_t *src = fb ? stage.data() + half + offs[r] + 2 * r : stage.data() + p;
+            if (!fb && p + counts[r] > live.size()) return -3;
+            const uint32_t *src = fb ? stage.data() + half + offs[r] + 2 * r : live.data() + p;
             for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = src[i];
             if (!fb) p += counts[r];
         }
+        if (p != live.size()) return -4;
     }
     return (int64_t)out_offs[n];
 }

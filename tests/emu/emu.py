@@ -15,7 +15,7 @@ def lib():
     if _L is None:
         so = os.path.join(HERE, "_emu.so")
         srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
-                                                   ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h",
+                                                   ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h", "ak_ptc.h",
                                                     "ak_tile.h", "ak_tile_spm.h", "ak_tile_rows.h", "ak_wave.h")]
         srcs.append(os.path.join(HERE, "..", "..", "include", "akshar.h"))
         if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
@@ -35,6 +35,10 @@ def lib():
         L.emu_rows_tiles.restype = ctypes.c_int64
         L.emu_rows_tiles.argtypes = [ctypes.c_int, ctypes.c_int, P, P, ctypes.c_uint64] + [P] * 8 + [ctypes.c_int]
         L.emu_last_fallback_rows.restype = ctypes.c_uint32
+        L.emu_bpe_set_ptc.argtypes = [P, ctypes.c_int, ctypes.c_uint32, P, ctypes.c_uint32, P, P]
+        L.emu_bpe_ptc_table.restype = ctypes.c_uint64
+        L.emu_bpe_ptc_table.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))]
+        L.emu_last_counters.argtypes = [P]
         L.emu_run.restype = ctypes.c_int64
         L.emu_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_uint64, P, P,
                               ctypes.c_uint64, P]
@@ -51,6 +55,7 @@ def pad(buf):
 class Model:
     def __init__(self, bpe=None, spm=None):
         L = lib()
+        self.bpe = bpe
         if bpe is not None:
             mg = np.ascontiguousarray(bpe.merges, dtype=np.uint32)
             self.h = L.emu_bpe_create(len(bpe.single_cp), bpe.single_cp.ctypes.data, bpe.single_id.ctypes.data,
@@ -60,6 +65,20 @@ class Model:
             self.h = L.emu_spm_create(len(m.pieces), m.piece_bytes.ctypes.data, m.piece_offs.ctypes.data,
                                       m.scores.ctypes.data, m.types.ctypes.data, m.unk_id, m.byte_ids.ctypes.data)
         assert self.h
+
+    def set_ptc(self, bits=-1):
+        """Rebuild the BPE pre-token cache (bits -1: sized from the keys, >= 0: 2^bits slots, None: off);
+        returns ak_bpe_cache_info's fields."""
+        mg = np.ascontiguousarray(self.bpe.merges, dtype=np.uint32)
+        info = (ctypes.c_uint64 * 4)()
+        lib().emu_bpe_set_ptc(self.h, -2 if bits is None else bits, len(self.bpe.single_cp),
+                              self.bpe.single_id.ctypes.data, len(mg), mg.ctypes.data, info)
+        return {"slots": info[0], "keys": info[1], "stored": info[2], "multi": info[3]}
+
+    def ptc_table(self):
+        p = ctypes.POINTER(ctypes.c_uint32)()
+        n = lib().emu_bpe_ptc_table(self.h, ctypes.byref(p))
+        return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -139,6 +158,20 @@ def rows_tiles(ops, buf, offs, matras=False, rows=16):
     assert rc == 0, rc
     return {"norm": (norm[:int(no[-1])], no), "seg": (seg[:int(so[-1])], so),
             "runs": (runs[:int(ro[-1])], labels[:int(ro[-1])], ro)}
+
+
+def last_counters():
+    """(pre-token cache probes, hits) of the last bpe_tiles call."""
+    out = (ctypes.c_uint64 * 8)()
+    lib().emu_last_counters(out)
+    return int(out[0]), int(out[1])
+
+
+def last_counters_all():
+    """The last tile launch's counters (ak_tile.h TC_*)."""
+    out = (ctypes.c_uint64 * 8)()
+    lib().emu_last_counters(out)
+    return [int(x) for x in out]
 
 
 def last_fallback_rows():

@@ -1,0 +1,182 @@
+"""The BPE pre-token result cache (akshar_amd/csrc/ak_ptc.h, ak_model_build.h build_bpe_ptc, ak_tile.h
+pass C) on the emulated tile kernel: the table's contents against an independent Python build from
+the model's vocabulary and merges, and the encode against the oracle with the cache on, off, and
+forced into tiny tables (every key colliding, most keys dropped), with pre-tokens that equal a vocab
+string whose merge_all is NOT that token, and pre-tokens past the cached lengths."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.emu import emu
+
+PTC_MAXN = 14
+
+
+@pytest.fixture(scope="module")
+def em(bpe_model):
+    m = emu.Model(bpe=bpe_model)
+    yield m
+    m.set_ptc(-1)
+
+
+def _merge_all(syms, rank):
+    """HF BPE merge_all on a list of ids (lowest rank, leftmost), independent of the C++ build."""
+    s = list(syms)
+    while len(s) > 1:
+        best = None
+        for i in range(len(s) - 1):
+            r = rank.get((s[i], s[i + 1]))
+            if r is not None and (best is None or r[0] < best[0]):
+                best = (r[0], i, r[1])
+        if best is None:
+            break
+        s[best[1]:best[1] + 2] = [best[2]]
+    return s
+
+
+@pytest.fixture(scope="module")
+def vocab_keys(bpe_model):
+    """{char-id tuple: merge_all result} for every multi-char vocab token of 2..14 chars whose chars
+    are all single-char tokens (the strings a pre-token can spell)."""
+    single = {int(c): int(i) for c, i in zip(bpe_model.single_cp, bpe_model.single_id)}
+    rank = {}
+    for r, (a, b, c) in enumerate(bpe_model.merges.tolist()):
+        rank.setdefault((a, b), (r, c))
+    out = {}
+    for tok, tid in bpe_model.vocab.items():
+        if not 2 <= len(tok) <= PTC_MAXN or any(ord(ch) not in single for ch in tok):
+            continue
+        syms = tuple(single[ord(ch)] for ch in tok)
+        out[syms] = (tid, _merge_all(syms, rank))
+    return out
+
+
+def test_table_matches_independent_build(em, vocab_keys):
+    info = em.set_ptc(-1)
+    tab = em.ptc_table().reshape(-1, 8)
+    assert info["slots"] == len(tab) and info["stored"] <= info["keys"]
+    singles = {k: v for k, v in vocab_keys.items() if len(v[1]) == 1}
+    seen = 0
+    for e in tab:
+        n = (int(e[0]) >> 16) & 15
+        if n == 0:
+            continue
+        seen += 1
+        syms = []
+        for k in range(7):
+            syms += [int(e[1 + k]) & 0xFFFF, int(e[1 + k]) >> 16]
+        assert all(x == 0xFFFF for x in syms[n:])
+        key = tuple(syms[:n])
+        assert key in singles, key
+        assert singles[key][1] == [int(e[0]) & 0xFFFF]
+    assert seen == info["stored"]
+    # every merged-token key with a one-id result is found (the vocab strings the merges make)
+    assert info["keys"] <= len(singles)
+    assert info["stored"] >= 0.99 * info["keys"]
+    assert info["multi"] == sum(1 for v in vocab_keys.values() if len(v[1]) > 1)
+
+
+def _texts(bpe_model, vocab_keys, n=400, seed=7):
+    """Rows mixing cached words, words of 13..16 chars and random Hinglish."""
+    from akshar_amd import synth
+    inv = {int(i): chr(int(c)) for c, i in zip(bpe_model.single_cp, bpe_model.single_id)}
+    cached = ["".join(inv[x] for x in k) for k, v in vocab_keys.items() if len(v[1]) == 1]
+    rng = np.random.default_rng(seed)
+    longw = ["abcdefghijklm", "abcdefghijklmn", "abcdefghijklmno", "abcdefghijklmnop", "namastenamaste",
+             "कर्मण्येवाधिकारस्ते"]
+    buf, offs = synth.generate(1, n // 2, seed=seed)
+    base = [bytes(buf[offs[i]:offs[i + 1]]).decode() for i in range(n // 2)]
+    texts = []
+    for i in range(n):
+        words = list(rng.choice(cached, size=8)) + [str(rng.choice(longw))]
+        rng.shuffle(words)
+        texts.append(" ".join(words) if i % 2 else base[i // 2] + " " + " ".join(words[:4]))
+    return texts
+
+
+@pytest.mark.parametrize("bits", [-1, None, 0, 1, 4])
+def test_encode_vs_oracle(em, bpe_model, vocab_keys, bits):
+    """bits -1: the product table; None: no cache; 0 / 1 / 4: 1 / 2 / 16 slots (every probe collides,
+    almost every key dropped)."""
+    info = em.set_ptc(bits)
+    if bits is not None and bits >= 0:
+        assert info["slots"] == 1 << bits and info["stored"] <= 1 << bits
+    texts = _texts(bpe_model, vocab_keys)
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8)
+    probes, hits = emu.last_counters()
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    if bits is None:
+        assert probes == 0
+    elif bits == -1:
+        assert hits > 0.4 * probes, (probes, hits)
+    em.set_ptc(-1)
+
+
+def test_hit_rate_on_bench_rows(em, bpe_model):
+    """The bench corpus (synthetic Hinglish, seed 1234): most multi-symbol pre-tokens hit."""
+    from akshar_amd import synth
+    em.set_ptc(-1)
+    buf, offs = synth.generate(1, 300, seed=1234)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8)
+    probes, hits = emu.last_counters()
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert np.array_equal(ids, ref)
+    assert 0.55 < hits / probes < 0.7, (probes, hits)
+
+
+def _tiny_model(path):
+    """A 43-token BPE model where two vocab strings are NOT their own merge_all result:
+    "abc" (merges b c -> bc before a b -> ab, and no a bc merge: [a, bc]) and "cab" ([c, ab])."""
+    import json
+    letters = "abcdefghijklmnopqrstuvwxyz"
+    specials = ["<pad>", "<unk>", "<s>", "</s>", "<mask>"]
+    vocab = {t: i for i, t in enumerate(specials)}
+    for ch in letters:
+        vocab[ch] = len(vocab)
+    merges = [("b", "c"), ("a", "b"), ("ab", "c"), ("d", "e"), ("de", "f"), ("x", "y"), ("y", "z"), ("xy", "z"),
+              ("c", "a"), ("bc", "a"), ("ab", "ab"), ("ca", "b")]
+    for a, b in merges:
+        vocab.setdefault(a + b, len(vocab))
+    tmpl = [{"SpecialToken": {"id": "<s>", "type_id": 0}}, {"Sequence": {"id": "A", "type_id": 0}},
+            {"SpecialToken": {"id": "</s>", "type_id": 0}}]
+    j = {"version": "1.0", "truncation": None, "padding": None,
+         "added_tokens": [{"id": i, "content": t, "single_word": False, "lstrip": False, "rstrip": False,
+                           "normalized": False, "special": True} for i, t in enumerate(specials)],
+         "normalizer": {"type": "NFKC"}, "pre_tokenizer": {"type": "Whitespace"},
+         "post_processor": {"type": "TemplateProcessing", "single": tmpl, "pair": tmpl + tmpl,
+                            "special_tokens": {"<s>": {"id": "<s>", "ids": [2], "tokens": ["<s>"]},
+                                               "</s>": {"id": "</s>", "ids": [3], "tokens": ["</s>"]}}},
+         "decoder": None,
+         "model": {"type": "BPE", "dropout": None, "unk_token": None, "continuing_subword_prefix": None,
+                   "end_of_word_suffix": None, "fuse_unk": False, "byte_fallback": False, "ignore_merges": False,
+                   "vocab": vocab, "merges": [[a, b] for a, b in merges]}}
+    path.write_text(json.dumps(j))
+    return str(path)
+
+
+@pytest.mark.parametrize("bits", [-1, 0, 2])
+def test_vocab_string_not_its_own_merge_result(tmp_path, bits):
+    """A pre-token equal to a vocab string whose merge_all is several ids takes the merged result,
+    never the vocab id; cached and uncached words side by side, under every table size."""
+    from akshar_amd.models import BPEModel
+    bm = BPEModel(_tiny_model(tmp_path / "tiny.json"))
+    m = emu.Model(bpe=bm)
+    info = m.set_ptc(bits)
+    assert info["multi"] == 2  # abc, cab
+    v = bm.vocab
+    words = ["abc", "cab", "bca", "abab", "xyz", "def", "de", "ab", "abcabc", "cabcab", "bcabca", "xyzxyz", "q"]
+    rng = np.random.default_rng(3)
+    texts = ["abc", "cab", "ABC cab!"] + [" ".join(rng.choice(words, size=rng.integers(1, 20))) for _ in range(300)]
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(m, buf, offs, rows=8)
+    ref, ro = O.OracleBPE(bm).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    got = [ids[oo[i]:oo[i + 1]].tolist() for i in range(3)]
+    assert got[0] == [2, v["a"], v["bc"], 3]
+    assert got[1] == [2, v["c"], v["ab"], 3]
+    assert got[2] == [2, v["a"], v["bc"], v["c"], v["ab"], 3]
+    probes, hits = emu.last_counters()
+    if bits == -1:
+        assert hits > 0

@@ -15,7 +15,7 @@ from akshar_amd import engine, synth  # noqa: E402
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ops = sys.argv[1:] or ["segment", "normalize", "switches", "analyze", "spm", "bpe"]
 rows = int(os.environ.get("AB_ROWS", "1000000"))
-res = {"variant": os.environ.get("AK_LIB_VARIANT", "default")}
+res = {"variant": os.environ.get("AK_LIB_VARIANT", "default"), "env": os.environ.get("AB_TAG", "")}
 spm = engine.SPM(os.path.join(ROOT, "models", "akshar.model"))
 bpe = engine.BPE(os.path.join(ROOT, "models", "akshar.json"))
 for kind, name in ((0, "deva"), (1, "hing")):

@@ -23,11 +23,16 @@ m.encode_batch(gb, go)
 torch.cuda.synchronize()
 engine.profile_enable(True, passes=True)
 engine.profile_tile_passes()
+has_ctr = hasattr(engine._lib.lib(), "ak_profile_tile_counters")
+if has_ctr:
+    engine.profile_tile_counters()
 engine.profile_reset()
 m.encode_batch(gb, go)
 torch.cuda.synchronize()
 prof = engine.profile_read()
 passes = engine.profile_tile_passes()
+ctr = engine.profile_tile_counters() if has_ctr else {}
 engine.profile_enable(False)
 print(json.dumps({"variant": os.environ.get("AK_LIB_VARIANT", "default"), "op": op, "kind": kind,
-                  "ms": {k: round(v[0], 3) for k, v in prof.items() if v[1]}, "passes": passes}), flush=True)
+                  "env": os.environ.get("AB_TAG", ""), "ms": {k: round(v[0], 3) for k, v in prof.items() if v[1]},
+                  "passes": passes, "counters": ctr}), flush=True)
