@@ -115,7 +115,13 @@ extern "C" int ak_version(void) { return 1; }
 // ------------------------------------------------------------------------------------------
 // models
 
+// model handles carry their kind as the first word, so ak_model_free needs no type string to
+// free the right kind (ak_loader.cpp)
+constexpr uint32_t MODEL_TAG_BPE = 0x31455042u;  // "BPE1"
+constexpr uint32_t MODEL_TAG_SPM = 0x314D5053u;  // "SPM1"
+
 struct ak_bpe {
+    uint32_t tag = MODEL_TAG_BPE;
     BpeDev dev;
     uint64_t *d_tab = nullptr;
     uint32_t *d_ctab = nullptr;
@@ -155,6 +161,7 @@ static int upload_dec(uint8_t *&mem, DecTab &t, const std::vector<uint8_t> &text
 }
 
 struct ak_spm {
+    uint32_t tag = MODEL_TAG_SPM;
     SpmDev dev;
     int4 *d_trie = nullptr;
     uint16_t *d_cmap_page = nullptr;
@@ -165,6 +172,12 @@ struct ak_spm {
     DecTab dec{};
     uint8_t *d_dec = nullptr;
 };
+
+int ak::model_kind(const void *h) {
+    if (!h) return 0;
+    const uint32_t t = *(const uint32_t *)h;
+    return t == MODEL_TAG_BPE ? 1 : t == MODEL_TAG_SPM ? 2 : 0;
+}
 
 extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const uint32_t *single_id,
                              uint32_t n_merges, const uint32_t *merges, uint32_t bos, uint32_t eos,
@@ -233,6 +246,7 @@ extern "C" int ak_bpe_cache_info(const ak_bpe *m, uint64_t info[4]) {
 
 extern "C" void ak_bpe_free(ak_bpe *m) {
     if (!m) return;
+    m->tag = 0;
     (void)hipFree(m->d_tab);
     (void)hipFree(m->d_ctab);
     (void)hipFree(m->d_single_fast);
@@ -363,6 +377,7 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
 
 extern "C" void ak_spm_free(ak_spm *m) {
     if (!m) return;
+    m->tag = 0;
     (void)hipFree(m->d_trie);
     (void)hipFree(m->d_cmap_page);
     (void)hipFree(m->d_cmap);
@@ -659,17 +674,17 @@ int ak::scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st, con
 // ------------------------------------------------------------------------------------------
 // driver
 
-static int g_cus = 0;
+static std::atomic<int> g_cus{0};  // CU count (same part on every device; idempotent store)
 
 int ak::num_cus() {
-    if (!g_cus) {
+    if (!g_cus.load(std::memory_order_relaxed)) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return 256;
         hipDeviceProp_t p;
         if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 256;
-        g_cus = p.multiProcessorCount;
+        g_cus.store(p.multiProcessorCount, std::memory_order_relaxed);
     }
-    return g_cus;
+    return g_cus.load(std::memory_order_relaxed);
 }
 
 static int dispatch(int op, int flags, ak_ws *w, const RowArgs &a, uint64_t *out_offs, hipStream_t st) {

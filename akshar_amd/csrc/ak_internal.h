@@ -2,6 +2,7 @@
 // TUs (ak_k_*.hip, compiled in parallel): workspace layout, error plumbing, the staged row
 // kernels with their slow / huge tiers, and their launcher.
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -17,6 +18,7 @@
 namespace ak {
 
 int set_error(int code, const char *msg);
+int model_kind(const void *h);  // 1 ak_bpe, 2 ak_spm, 0 neither (the handle's first word; ak_engine.hip)
 int set_hip_error(const char *expr, hipError_t e);
 
 #define HIP_TRY(x)                                           \
@@ -88,15 +90,19 @@ int copy_staged(const T *stage, uint64_t stage_cap, const uint64_t *offs, const 
 int num_cus();
 
 // Grid of a fallback-row kernel: as many blocks as stay resident on every CU (its rows run one lane
-// each, sequential and latency-bound, so resident lanes are the lever); the occupancy is cached.
+// each, sequential and latency-bound, so resident lanes are the lever). The occupancy is cached
+// per launcher in an atomic: host threads driving different GPUs may race on it, and every device
+// of the node is the same gfx950 part, so one value serves them all (a benign, idempotent store).
 template <class K>
-unsigned resident_grid(K kernel, int block, int &cache) {
-    if (!cache) {
+unsigned resident_grid(K kernel, int block, std::atomic<int> &cache) {
+    int c = cache.load(std::memory_order_relaxed);
+    if (!c) {
         int b = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, block, 0) != hipSuccess) b = 1;
-        cache = b > 1 ? b : 1;
+        c = b > 1 ? b : 1;
+        cache.store(c, std::memory_order_relaxed);
     }
-    return (unsigned)num_cus() * (unsigned)cache;
+    return (unsigned)num_cus() * (unsigned)c;
 }
 // unit-run staging (tile BPE, row tiles): per-unit fallback masks, and the streaming unit copy
 int ws_unit_fb_reserve(AkWs *w, uint64_t nunits);

@@ -361,7 +361,7 @@ int selftest_wave() {
     return AK_OK;
 }
 
-static int g_tile_blocks_per_cu = 0;
+static std::atomic<int> g_tile_blocks_per_cu{0};  // occupancy (same gfx950 part on every device; idempotent store)
 
 // flags == AK_NORM_DEFAULT only (the dispatcher sends other flags to the row kernels)
 int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t st) {
@@ -398,10 +398,10 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
         HIP_TRY(hipMalloc(&w->tile_passprof, T_NPROF * 8));
         HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPROF * 8, st));
     }
-    if (!g_tile_blocks_per_cu) {
+    if (!g_tile_blocks_per_cu.load(std::memory_order_relaxed)) {
         int b = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_bpe_tiles<3>, TILE_BLOCK, 0));
-        g_tile_blocks_per_cu = std::max(1, b);
+        g_tile_blocks_per_cu.store(std::max(1, b), std::memory_order_relaxed);
     }
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
@@ -431,7 +431,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit
-    int bpc = g_tile_blocks_per_cu;
+    int bpc = g_tile_blocks_per_cu.load(std::memory_order_relaxed);
     if (const char *e = getenv("AK_TILE_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + waves_per_block - 1) / waves_per_block,
                                                        (uint64_t)num_cus() * (uint64_t)bpc);
@@ -456,7 +456,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
-    static int fb_bpc = 0;
+    static std::atomic<int> fb_bpc{0};
     k_tile_fb<3><<<resident_grid(k_tile_fb<3>, FB_BLOCK, fb_bpc), FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;
     ra.counts = w->counts;

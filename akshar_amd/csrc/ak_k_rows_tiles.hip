@@ -137,7 +137,7 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     AK_PROF(AK_PROF_ROW_TILES, true, st);
     HIP_TRY(hipGetLastError());
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
-    static int fb_bpc = 0;
+    static std::atomic<int> fb_bpc{0};
     k_rows_tile_fb<OPS><<<resident_grid(k_rows_tile_fb<OPS>, RT_FB_BLOCK, fb_bpc), RT_FB_BLOCK, 0, st>>>(ta, ofb, w->ctr + CTR_ERR);
     RowArgs ra = ta.ra;
     ra.err = w->ctr + CTR_ERR;

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(SPM_FB_BLOCK) void k_spm_tile_fb(TileArgs ta) {
     }
 }
 
-static int g_spm_blocks_per_cu = 0;
+static std::atomic<int> g_spm_blocks_per_cu{0};  // occupancy (same gfx950 part on every device; idempotent store)
 
 int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t st) {
     if (a0.n == 0) {
@@ -107,10 +107,10 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
         HIP_TRY(hipMalloc(&w->tile_passprof, T_NPROF * 8));
         HIP_TRY(hipMemsetAsync(w->tile_passprof, 0, T_NPROF * 8, st));
     }
-    if (!g_spm_blocks_per_cu) {
+    if (!g_spm_blocks_per_cu.load(std::memory_order_relaxed)) {
         int b = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spm_tiles<3>, SPM_TILE_BLOCK, 0));
-        g_spm_blocks_per_cu = std::max(1, b);
+        g_spm_blocks_per_cu.store(std::max(1, b), std::memory_order_relaxed);
     }
     if (w->cap_fb2 < a0.n) {
         (void)hipFree(w->fb2);
@@ -139,7 +139,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = SPM_TILE_BLOCK / 64;
-    int bpc = g_spm_blocks_per_cu;
+    int bpc = g_spm_blocks_per_cu.load(std::memory_order_relaxed);
     if (const char *e = getenv("AK_SPM_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));  // development aid
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)num_cus() * (uint64_t)bpc);
     AK_PROF(AK_PROF_SPM_TILES, false, st);
@@ -150,7 +150,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
-    static int fb_bpc = 0;
+    static std::atomic<int> fb_bpc{0};
     k_spm_tile_fb<3><<<resident_grid(k_spm_tile_fb<3>, SPM_FB_BLOCK, fb_bpc), SPM_FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;
     ra.counts = w->counts;

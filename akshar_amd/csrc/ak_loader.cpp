@@ -17,7 +17,11 @@
 
 #include "akshar.h"
 
-namespace ak { int set_error(int code, const char *msg); }  // ak_engine.hip: sets ak_last_error()
+namespace ak {
+int set_error(int code, const char *msg);  // ak_engine.hip: sets ak_last_error()
+int model_kind(const void *h);             // ak_engine.hip: 1 ak_bpe, 2 ak_spm, 0 neither
+}  // namespace ak
+static int ak_internal_model_kind(const void *h) { return ak::model_kind(h); }
 static int ak_internal_fail(int code, const char *msg) { return ak::set_error(code, msg); }
 
 namespace {
@@ -205,6 +209,16 @@ struct BpeArrays {
     std::vector<uint64_t> tok_offs{0};
 };
 
+// a token id as the model file states it: a JSON number that is a whole number in [0, 2^24)
+// (anything else would wrap the u32 ids or size a decode table by a garbage value)
+static bool json_id(const JVal *v, uint32_t &out) {
+    if (!v || v->kind != JVal::NUM) return false;
+    const double x = v->num;
+    if (!(x >= 0.0) || x >= 16777216.0 || x != (double)(uint32_t)x) return false;
+    out = (uint32_t)x;
+    return true;
+}
+
 int parse_bpe(const char *path, BpeArrays &A) {
     std::string text;
     if (!read_file(path, text)) return fail(AK_ERR_ARG, std::string("cannot read ") + path);
@@ -235,7 +249,8 @@ int parse_bpe(const char *path, BpeArrays &A) {
     std::map<std::string, uint32_t> vocab;
     std::vector<std::pair<uint32_t, uint32_t>> singles;
     for (const auto &kv : voc->obj) {
-        const uint32_t id = (uint32_t)kv.second.num;
+        uint32_t id = 0;
+        if (!json_id(&kv.second, id)) return fail(AK_ERR_ARG, "tokenizer.json: vocab id of " + kv.first + " is not an integer in [0, 2^24)");
         vocab[kv.first] = id;
         int nch = 0;
         const uint32_t cp = first_cp(kv.first, &nch);
@@ -247,16 +262,18 @@ int parse_bpe(const char *path, BpeArrays &A) {
     if (added && added->kind == JVal::ARR) {
         for (const JVal &a : added->arr) {
             const JVal *c = a.get("content"), *i = a.get("id");
-            if (!c || !i) return fail(AK_ERR_ARG, "tokenizer.json: added token without content / id");
-            vocab.emplace(c->str, (uint32_t)i->num);  // setdefault
+            uint32_t aid = 0;
+            if (!c || c->kind != JVal::STR || !json_id(i, aid))
+                return fail(AK_ERR_ARG, "tokenizer.json: added token without a string content / an integer id in [0, 2^24)");
+            vocab.emplace(c->str, aid);  // setdefault
             for (const char *k : {"single_word", "lstrip", "rstrip", "normalized"}) {
                 const JVal *f = a.get(k);
                 if (f && f->kind == JVal::BOOL && f->b)
                     return fail(AK_ERR_UNSUPPORTED, "added token " + c->str + " with " + k + "=True not supported");
             }
-            added_list.push_back({c->str, (uint32_t)i->num});
+            added_list.push_back({c->str, aid});
             const JVal *sp = a.get("special");
-            if (sp && sp->kind == JVal::BOOL && sp->b) special_ids.push_back((uint32_t)i->num);
+            if (sp && sp->kind == JVal::BOOL && sp->b) special_ids.push_back(aid);
         }
     }
     std::sort(singles.begin(), singles.end());
@@ -290,13 +307,17 @@ int parse_bpe(const char *path, BpeArrays &A) {
     const JVal *s0 = single->arr[0].get("SpecialToken"), *s1 = single->arr[1].get("Sequence"),
                *s2 = single->arr[2].get("SpecialToken");
     if (!s0 || !s1 || !s2 || single->arr[1].get("SpecialToken")) return fail(AK_ERR_UNSUPPORTED, "unsupported template");
+    const JVal *n0 = s0->get("id"), *n2 = s2->get("id");
+    if (!n0 || n0->kind != JVal::STR || !n2 || n2->kind != JVal::STR)
+        return fail(AK_ERR_UNSUPPORTED, "template SpecialToken without a string id");
     const JVal *st = pp->get("special_tokens");
-    const JVal *b0 = st ? st->get(s0->get("id")->str.c_str()) : nullptr;
-    const JVal *b2 = st ? st->get(s2->get("id")->str.c_str()) : nullptr;
+    const JVal *b0 = st ? st->get(n0->str.c_str()) : nullptr;
+    const JVal *b2 = st ? st->get(n2->str.c_str()) : nullptr;
     const JVal *i0 = b0 ? b0->get("ids") : nullptr, *i2 = b2 ? b2->get("ids") : nullptr;
-    if (!i0 || !i2 || i0->arr.empty() || i2->arr.empty()) return fail(AK_ERR_UNSUPPORTED, "template special tokens without ids");
-    A.bos = (uint32_t)i0->arr[0].num;
-    A.eos = (uint32_t)i2->arr[0].num;
+    if (!i0 || !i2 || i0->kind != JVal::ARR || i2->kind != JVal::ARR || i0->arr.empty() || i2->arr.empty())
+        return fail(AK_ERR_UNSUPPORTED, "template special tokens without ids");
+    if (!json_id(&i0->arr[0], A.bos) || !json_id(&i2->arr[0], A.eos))
+        return fail(AK_ERR_ARG, "tokenizer.json: template special token id is not an integer in [0, 2^24)");
     for (auto &a : added_list) {
         uint32_t cnt = 0;
         for (size_t i = 0; i < a.first.size();) {
@@ -468,9 +489,17 @@ extern "C" int ak_model_load(const char *path, const char *model_type, void **ou
     return ak_internal_fail(AK_ERR_ARG, "ak_model_load: model_type must be \"bpe\" or \"sentencepiece\"");
 }
 
+// The handle carries its kind (ak_engine.hip model_kind), so the type string only has to agree:
+// a mismatched or unknown model_type still frees the handle by its own kind and records an error
+// (ak_last_error); a handle that is neither kind is left alone and recorded.
 extern "C" void ak_model_free(void *h, const char *model_type) {
-    if (is_bpe(model_type)) ak_bpe_free((ak_bpe *)h);
-    else if (is_spm(model_type)) ak_spm_free((ak_spm *)h);
+    if (!h) return;
+    const int kind = ak_internal_model_kind(h);
+    if (kind == 1) ak_bpe_free((ak_bpe *)h);
+    else if (kind == 2) ak_spm_free((ak_spm *)h);
+    if (kind == 0) (void)ak_internal_fail(AK_ERR_ARG, "ak_model_free: not a model handle (left alone)");
+    else if (!(kind == 1 ? is_bpe(model_type) : is_spm(model_type)))
+        (void)ak_internal_fail(AK_ERR_ARG, "ak_model_free: model_type does not match the handle (freed by its kind)");
 }
 
 extern "C" int ak_model_info(const char *path, const char *model_type, uint64_t info[8]) {

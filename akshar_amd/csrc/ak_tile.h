@@ -599,8 +599,9 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
 #endif
     uint4 *ring = pool + c * POOL_RING;
     const uint32_t head = w_bcast(M.phead[c], 0);
-    const uint4 e = act ? load_l2(ring + (head + (uint32_t)lane) % POOL_RING) : make_uint4(0, 0, 0, 0);
-    const uint64_t dst = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32);
+    // unconditional loads (no exec-masked regions): an idle lane reads a ring slot and stage[0..16)
+    const uint4 e = load_l2(ring + (head + (uint32_t)lane) % POOL_RING);
+    const uint64_t dst = act ? (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32) : 0ull;
     const int n = act ? (int)(e.y >> 16) : 0;
     const uint32_t row = e.z;
     uint32_t *sp = (uint32_t *)ta.ra.out + dst;
@@ -609,7 +610,7 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
         const uint4 *s4 = (const uint4 *)sp;  // dword-aligned 16-byte loads (the stage is padded past every run)
 #pragma unroll
         for (int k = 0; k < WREG / 4; ++k) {
-            const uint4 v = act ? load_l2(s4 + k) : make_uint4(0, 0, 0, 0);
+            const uint4 v = load_l2(s4 + k);
             const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -623,8 +624,10 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
     for (int k = 0; k < WREG / 2; ++k) {
         const int i = 2 * k;
         const uint32_t a0 = p[k] & 0xFFFFu, a1 = p[k] >> 16, a2 = k + 1 < WREG / 2 ? p[k + 1] & 0xFFFFu : 0xFFFFu;
-        const uint32_t lo = i + 1 < n ? merge_lookup_c(m, a0, a1) & 0xFFFFu : 0xFFFFu;
-        const uint32_t hi = (i + 2 < WREG && i + 2 < n) ? merge_lookup_c(m, a1, a2) & 0xFFFFu : 0xFFFFu;
+        // looked up unconditionally (the table slot of any symbol pair is in range), kept below n
+        const uint32_t l0 = merge_lookup_c(m, a0, a1), l1 = i + 2 < WREG ? merge_lookup_c(m, a1, a2) : 0xFFFFu;
+        const uint32_t lo = i + 1 < n ? l0 & 0xFFFFu : 0xFFFFu;
+        const uint32_t hi = (i + 2 < WREG && i + 2 < n) ? l1 & 0xFFFFu : 0xFFFFu;
         d[k] = lo | (hi << 16);
     }
     {  // every lane writes its rows (inactive lanes: no merges): the rounds read them unmasked
@@ -819,17 +822,39 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
     uint16_t *mlist = (uint16_t *)M.bytes;
     uint32_t nm = 0, nlong = 0;
     {
+        // W's tail past the id stream reads as a pre-token start, so a lane's 16-symbol window needs no
+        // bounds check: the window is read unconditionally as 9 aligned dwords (no exec-masked loads)
+        static_assert(T_BCAP + 2 * T_MAXR + 1 + 18 <= T_E + 16, "W's pad holds a window past the id stream");
+        if (lane < 18) M.w[wlen + lane] = 0xFFFFu;
+        w_sync();
         uint16_t *dummy = (uint16_t *)M.w + (T_E + 16 - 64) + lane;  // past every pre-token (W's pad)
+        const uint32_t *W32 = (const uint32_t *)M.w;
         for (uint32_t wb = 0; wb < nw; wb += 64) {
             const uint32_t j = wb + lane;
             const bool act = j < nw;
             const int st = act ? (int)M.v[T_E - 1 - j] : 0;
+            uint32_t pr[WREG / 2];  // pr[k] = symbols 2k, 2k+1 of the window (low half first)
+            {
+                uint32_t wd[WREG / 2 + 1];
+#pragma unroll
+                for (int k = 0; k <= WREG / 2; ++k) wd[k] = W32[(st >> 1) + k];
+                const uint32_t sh = (uint32_t)(st & 1) * 16u;
+#pragma unroll
+                for (int k = 0; k < WREG / 2; ++k)
+#ifdef AK_HOST_EMU
+                    pr[k] = sh ? (wd[k] >> 16) | (wd[k + 1] << 16) : wd[k];
+#else
+                    pr[k] = __builtin_amdgcn_alignbit(wd[k + 1], wd[k], sh);
+#endif
+            }
+            // n = the first position >= 1 that starts a pre-token (WREG if none in the window)
+            uint32_t sm = 1u << WREG;
+#pragma unroll
+            for (int k = 0; k < WREG / 2; ++k) sm |= ((pr[k] >> 15) & 1u) << (2 * k) | (pr[k] >> 31) << (2 * k + 1);
+            const int n = __builtin_ctz(sm & ~1u);
             uint32_t s[WREG];
 #pragma unroll
-            for (int i = 0; i < WREG; ++i) s[i] = (act && st + i < (int)wlen) ? M.w[st + i] : 0xFFFFu;
-            int n = WREG;
-#pragma unroll
-            for (int i = WREG - 1; i >= 1; --i) n = (s[i] & WSTART) ? i : n;
+            for (int i = 0; i < WREG; ++i) s[i] = (pr[i / 2] >> (16 * (i & 1))) & 0xFFFFu;
             uint32_t res = 0xFFFFFFFFu;
             if (m.ptc != nullptr) {  // uniform
                 uint32_t q[7];

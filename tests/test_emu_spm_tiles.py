@@ -88,3 +88,23 @@ def test_work_queue_waves_vs_oracle(em, spm_model):
     ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=4, waves=3)
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+@pytest.mark.parametrize("scale", [500.0, 2000.0])
+def test_scaled_scores_cross_the_rebase_bound(spm_model, scale):
+    """Scores scaled x500 / x2000 make the carried score of ordinary 40-120-char rows leave
+    [-1e5, 1e5] inside the tile lattice (no test reached the tile rebase; the flat
+    pass V and the V2 redo both rebase there): the tile kernel must rebase exactly as the oracle
+    (the wheel's rule)."""
+    import copy
+    from akshar_amd import synth
+    m = copy.copy(spm_model)
+    m.scores = (np.asarray(spm_model.scores, dtype=np.float32) * np.float32(scale)).astype(np.float32)
+    em = emu.Model(spm=m)
+    buf, offs = synth.generate(1, 300, seed=77)
+    ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=4)
+    ref, ro = O.OracleSPM(m).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    # the rows really cross the bound: a row's summed piece scores is far below -1e5
+    first = ref[ro[0]:ro[1]]
+    assert float(np.sum(m.scores[first])) < -1e5

@@ -96,3 +96,71 @@ def test_library_loaded_models_match(golden, kind):
     ta, tao = a.decode_batch(ids, oo)
     tb, tbo = b.decode_batch(ids, oo)
     assert np.array_equal(ta.cpu().numpy(), tb.cpu().numpy()) and np.array_equal(tao.cpu().numpy(), tbo.cpu().numpy())
+
+
+def _mutated(tmp_path, fn, name="t.json"):
+    j = json.load(open(BPE_PATH, encoding="utf-8"))
+    fn(j)
+    p = tmp_path / name
+    p.write_text(json.dumps(j), encoding="utf-8")
+    return str(p)
+
+
+@pytest.mark.parametrize("case,rc,msg", [
+    ("template_special_without_id", -3, b"SpecialToken without a string id"),
+    ("template_special_numeric_id", -3, b"SpecialToken without a string id"),
+    ("vocab_id_negative", -1, b"not an integer"),
+    ("vocab_id_huge", -1, b"not an integer"),
+    ("vocab_id_fraction", -1, b"not an integer"),
+    ("vocab_id_string", -1, b"not an integer"),
+    ("added_id_missing", -1, b"added token"),
+    ("special_ids_not_numbers", -1, b"template special token id"),
+])
+def test_malformed_bpe_files_fail_with_errors(tmp_path, case, rc, msg):
+    """A malformed tokenizer.json comes back as an error code and message from the C-ABI loader
+    (ADVICE round 3): never a crash, a wrapped id or a decode table sized by a garbage id."""
+    from akshar_amd import _lib
+
+    def mut(j):
+        tmpl = j["post_processor"]["single"]
+        if case == "template_special_without_id":
+            del tmpl[0]["SpecialToken"]["id"]
+        elif case == "template_special_numeric_id":
+            tmpl[2]["SpecialToken"]["id"] = 3
+        elif case == "vocab_id_negative":
+            j["model"]["vocab"]["a"] = -1
+        elif case == "vocab_id_huge":
+            j["model"]["vocab"]["a"] = 4e9
+        elif case == "vocab_id_fraction":
+            j["model"]["vocab"]["a"] = 5.5
+        elif case == "vocab_id_string":
+            j["model"]["vocab"]["a"] = "5"
+        elif case == "added_id_missing":
+            del j["added_tokens"][0]["id"]
+        elif case == "special_ids_not_numbers":
+            j["post_processor"]["special_tokens"]["<s>"]["ids"] = ["2"]
+    got, _ = _info(_mutated(tmp_path, mut), "bpe")
+    assert got == rc
+    assert msg in _lib.lib().ak_last_error()
+
+
+def test_model_free_checks_the_handle_kind():
+    """ak_model_free frees a handle by the kind it carries; a type string that does not match is
+    reported (ak_last_error), a pointer that is not a model handle is left alone and reported."""
+    from akshar_amd import _lib
+    L = _lib.lib()
+    junk = (ctypes.c_uint32 * 4)(7, 7, 7, 7)
+    L.ak_model_free(ctypes.cast(junk, ctypes.c_void_p), b"bpe")
+    assert b"not a model handle" in L.ak_last_error()
+    L.ak_model_free(None, b"bpe")  # null: nothing to do
+
+
+@pytest.mark.gpu
+def test_model_free_by_kind_on_device():
+    """A real handle freed with the other type string is still freed by its own kind, and reported."""
+    from akshar_amd import _lib
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.ak_model_load(BPE_PATH.encode(), b"bpe", ctypes.byref(h)) == 0
+    L.ak_model_free(h, b"sentencepiece")
+    assert b"does not match the handle" in L.ak_last_error()
