@@ -40,6 +40,11 @@ constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
 #ifndef AK_TILE_UNIT
 #define AK_TILE_UNIT 64
 #endif
+#ifndef AK_KNOCKOUT
+// timing experiments only (wrong ids): 1 no merges, 2 set-up without rounds, 8 / 9 / 10 / 11 / 12 /
+// 13 / 14 stop after staging / D1 / D2 / N / S / C / F
+#define AK_KNOCKOUT 0
+#endif
 constexpr uint64_t TILE_UNIT = AK_TILE_UNIT;  // rows per unit of the work queue (tiles pack greedily inside one)
 static_assert(TILE_UNIT <= 64, "a unit's fallback rows are one 64-bit mask");
 constexpr int T_E = T_BCAP + 2 * T_MAXR + 64;
@@ -366,6 +371,7 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
     }
     w_sync();
 
+    if (AK_KNOCKOUT == 8) return TileRows{k, nr, S0, a0, 0u};
     // ---------------- pass D1: per row, 64 bytes per step: the positions of the UTF-8 lead bytes ->
     // P (in W, free until the next pass), each row opened by a mark entry. A row that starts with a
     // continuation byte is invalid UTF-8: fallback (stray continuation bytes inside a row are caught
@@ -391,6 +397,7 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
     }
     w_sync();
 
+    if (AK_KNOCKOUT == 9) return TileRows{k, nr, S0, a0, 0u};
     // ---------------- pass D2: the whole tile's chars, 64 per step: decode (branch-free, dword
     // window), hot word, nfc_trig against the previous char (a mark = row start), then the
     // normalize_text map (lower / allowlist) -> V with <s>/</s> sentinels around each row. If no
@@ -477,9 +484,6 @@ __device__ __forceinline__ uint32_t ptc_probe(const BpeDev &m, uint32_t n, const
     return 0xFFFFFFFFu;
 }
 
-#ifndef AK_KNOCKOUT
-#define AK_KNOCKOUT 0  // timing experiments only (wrong ids): 1 no merges, 2 set-up without rounds
-#endif
 
 // The wave's merge pool (pass A / pool_flush): misses of < WREG symbols from any tile of the wave's
 // units wait in per-wave rings in global memory, one ring per class of symbol count, until 64 of a
@@ -697,6 +701,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
     const TileRows tr = tile_front<T_BCAP>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
+    if (AK_KNOCKOUT == 10) return nr;
 
     pc.mark(TP_D);
     // ---------------- pass N (fused): remove_elongations, HF NFKC, Whitespace pre-tokenizer and
@@ -794,6 +799,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
     w_sync();
 
     pc.mark(TP_E);
+    if (AK_KNOCKOUT == 11) return nr;
     // ---------------- pass S: starts of the pre-tokens with >= 2 symbols (a single symbol has
     // nothing to merge), to the TOP of V (V[T_E-1-k]) so pass B can use bytes + the bottom of V
     // for its rank rows (at most T_SCAP such pre-tokens; more: the tile's rows fall back).
@@ -813,6 +819,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
     w_sync();
 
     pc.mark(TP_P);
+    if (AK_KNOCKOUT == 12) return nr;
     // ---------------- pass C: lane per listed pre-token: the pre-token result cache (ak_ptc.h) and
     // the miss list. A hit takes its stored id (its merge_all result) at its start and V_DEAD over
     // its other symbols (pass F skips those). The misses are listed in order in the staged-bytes
@@ -887,6 +894,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
     }
 
     pc.mark(TP_C);
+    if (AK_KNOCKOUT == 13) return nr;
     if (AK_KNOCKOUT == 1) nm = nlong = 0;
     // ---------------- pass B: pre-tokens of >= WREG symbols (rare) merge here, in LDS (bpe_merge_lds,
     // one lane each). Every shorter miss goes to the wave's merge pool after pass F (pass A).
@@ -964,6 +972,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
         if (a.row_status) a.row_status[r0 + lane] = 0;
     }
     pc.mark(TP_F);
+    if (AK_KNOCKOUT == 14) return nr;
 
     // ---------------- pass A: the misses of < WREG symbols in rows not sent to the fallback kernels
     // join the wave's merge pool as {stage index of the first symbol, n << 16, row} in the ring of

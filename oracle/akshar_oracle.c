@@ -882,3 +882,55 @@ int64_t or_spm_encode(const or_spm *m, int flags, const uint8_t *in, const uint6
     vfree(&s); vfree(&t);
     return (int64_t)pos;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* CPU baseline for bench.py (the encode on the host's cores, no Python in
+ * the loop): `threads` OpenMP threads take chunk_rows-row chunks of the batch from one shared
+ * cursor (wrapping around) and encode them (kind 0 BPE, 1 SentencePiece) into per-thread buffers
+ * they reuse, until `seconds` have passed. Returns the input bytes encoded; *ids_out gets the ids
+ * produced and *elapsed_s the wall time of the parallel region.                              */
+#include <omp.h>
+
+uint64_t or_encode_timed(int kind, const void *m, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
+                         uint64_t chunk_rows, int threads, double seconds, uint64_t *ids_out, double *elapsed_s) {
+    const uint64_t ch = chunk_rows ? (chunk_rows < n ? chunk_rows : n) : n;
+    const uint64_t nchunks = ch ? n / ch : 0;
+    uint64_t bytes = 0, ids = 0, cursor = 0;
+    if (!nchunks) { *ids_out = 0; *elapsed_s = 0.0; return 0; }
+    const double t0 = omp_get_wtime();
+#pragma omp parallel num_threads(threads) reduction(+ : bytes, ids)
+    {
+        vec_t s = {0}, t = {0};
+        uint32_t *out = NULL;
+        size_t out_cap = 0;
+        while (omp_get_wtime() - t0 < seconds) {
+            uint64_t k;
+#pragma omp atomic capture
+            k = cursor++;
+            k %= nchunks;
+            const uint64_t r0 = k * ch, r1 = r0 + ch;
+            size_t pos = 0;
+            for (uint64_t r = r0; r < r1; ++r) {
+                load_row(in, offs, r, &s, NULL);
+                normalize_cps(&s, flags);
+                t.n = 0;
+                if (kind == 0) bpe_encode_cps((const or_bpe *)m, &s, &t);
+                else spm_encode_cps((const or_spm *)m, &s, &t);
+                if (pos + t.n > out_cap) {
+                    out_cap = 2 * (pos + t.n) + 1024;
+                    out = (uint32_t *)realloc(out, out_cap * sizeof(uint32_t));
+                }
+                memcpy(out + pos, t.v, t.n * sizeof(uint32_t));
+                pos += t.n;
+            }
+            bytes += offs[r1] - offs[r0];
+            ids += pos;
+        }
+        free(out);
+        vfree(&s);
+        vfree(&t);
+    }
+    *elapsed_s = omp_get_wtime() - t0;
+    *ids_out = ids;
+    return bytes;
+}

@@ -42,6 +42,9 @@ def lib():
         for name in ("or_bpe_encode", "or_spm_encode"):
             getattr(L, name).restype = I64
             getattr(L, name).argtypes = [P, ctypes.c_int, P, P, U64, P, U64, P, P]
+        L.or_encode_timed.restype = U64
+        L.or_encode_timed.argtypes = [ctypes.c_int, P, ctypes.c_int, P, P, U64, U64, ctypes.c_int, ctypes.c_double,
+                                      ctypes.POINTER(U64), ctypes.POINTER(ctypes.c_double)]
         _LIB = L
     return _LIB
 
@@ -88,6 +91,18 @@ class OracleSPM:
 
     def encode_batch(self, buf, offs, flags=3):
         return _run_ids(lib().or_spm_encode, self.h, flags, buf, offs)
+
+
+def encode_timed(model, buf, offs, threads, seconds, chunk_rows=2000, flags=3):
+    """CPU baseline (bench.py): `model` (OracleBPE / OracleSPM) on `threads` OpenMP threads over
+    chunk_rows-row chunks of (buf, offs) until `seconds` pass -> (bytes, ids, elapsed s)."""
+    kind = 0 if isinstance(model, OracleBPE) else 1
+    ids = U64()
+    el = ctypes.c_double()
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    nb = lib().or_encode_timed(kind, model.h, flags, _p(buf), _p(offs), len(offs) - 1, chunk_rows, threads, seconds,
+                               ctypes.byref(ids), ctypes.byref(el))
+    return int(nb), int(ids.value), float(el.value)
 
 
 def _run_ids(fn, h, flags, buf, offs):
