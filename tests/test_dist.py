@@ -167,3 +167,40 @@ def test_nccl_world1_gather_ids_on_device():
     p.join(timeout=60)
     assert res[0] == "ok", res
     assert p.exitcode == 0 and res[1] > 50000
+
+
+def _edge_worker(rank, world, port, q):
+    """Uneven shards: rank 1 holds no rows at all; rank 2 passes preallocated out buffers."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rows = {0: [[5, 6, 7], [8]], 1: [], 2: [[9, 10], [], [11, 12, 13, 14]]}[rank]
+        ids = torch.tensor([x for r in rows for x in r], dtype=torch.int32)
+        offs = torch.tensor(np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64))
+        out = None
+        if rank == 2:
+            out = (torch.full((20,), -1, dtype=torch.int32), torch.full((10,), -1, dtype=torch.int64))
+        all_ids, all_offs = adist.gather_ids(ids, offs, out=out)
+        q.put((rank, all_ids.tolist(), all_offs.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_gather_uneven_and_empty_shards():
+    """gather_ids with an empty rank and a caller-provided output: every rank gets the whole batch's
+    ids in rank order and offsets rebased across ranks (one size all-gather + exact-size broadcasts)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_edge_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, ids, offs in res:
+        assert ids == [5, 6, 7, 8, 9, 10, 11, 12, 13, 14]
+        assert offs == [0, 3, 4, 6, 6, 10]
