@@ -34,7 +34,7 @@ __global__ __launch_bounds__(TILE_BLOCK, AK_BPE_TILE_WPE) void k_bpe_tiles(TileA
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t sfast[SFAST_N];
     __shared__ TileWaveMem wm[TILE_BLOCK / 64];
-    for (uint32_t i = threadIdx.x; i < HOT_N; i += TILE_BLOCK) hot_tab[i] = hot_of(prop_global(hot_cp(i)));
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += TILE_BLOCK) hot_tab[i] = hot_word(hot_cp(i));
     for (uint32_t i = threadIdx.x; i < SFAST_N; i += TILE_BLOCK)
         sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     __syncthreads();

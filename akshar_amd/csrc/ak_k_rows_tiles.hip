@@ -26,7 +26,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_rows_tiles(TileArgs ta, RowsOut o)
     __shared__ RowsWaveMem wm[RT_BLOCK / 64];
     for (uint32_t i = threadIdx.x; i < HOT_N; i += RT_BLOCK) {
         const uint32_t cp = hot_cp(i);
-        hot_tab[i] = hot_of(prop_global(cp));
+        hot_tab[i] = hot_word(cp);
         sc_tab[i] = seg_class_of(cp);
     }
     __syncthreads();

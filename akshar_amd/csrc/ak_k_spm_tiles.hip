@@ -29,7 +29,7 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     __shared__ SpmWaveMem wm[SPM_TILE_BLOCK / 64];
     for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
         const uint32_t cp = hot_cp(i);
-        hot_tab[i] = hot_of(prop_global(cp));
+        hot_tab[i] = hot_word(cp);
         const uint32_t c = spm_code(ta.ra.spm, cp);
         scode[i] = (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
     }

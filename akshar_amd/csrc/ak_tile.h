@@ -192,6 +192,27 @@ __device__ __forceinline__ uint32_t hot_of(uint2 pr) {
            ((p_ccc_hf(pr) == 0 && !p_second(pr)) ? H_HFST : 0u) | (p_ccc_hf(pr) == 0 ? H_HC0 : 0u) |
            (p_hfspace(pr) ? H_HFSPACE : 0u) | ((uint32_t)p_hfclass(pr) << H_CLS_SHIFT) | (ccc_code(cc) << H_CCC_SHIFT);
 }
+// The precomposed nukta letters U+0958..U+095F, U+09DC, U+09DD, U+09DF are composition exclusions:
+// NFC is always their base + nukta (U+093C / U+09BC), whatever surrounds them (the base is a starter
+// no composite takes as its second, and the nukta follows it directly). Common Hindi input methods
+// produce them, so the tile front end expands them itself instead of sending the row to the
+// fallback kernels: their hot word carries H_EXP, the base in the map field, and no decomposition
+// flag; pass D2 writes base + nukta and checks the next char against the nukta.
+constexpr uint32_t H_EXP = 1u << 25;
+__device__ __forceinline__ uint32_t nukta_base(uint32_t cp) {
+    if (cp - 0x0958u < 8u) {
+        constexpr uint16_t b[8] = {0x0915, 0x0916, 0x0917, 0x091C, 0x0921, 0x0922, 0x092B, 0x092F};
+        return b[cp - 0x0958u];
+    }
+    return cp == 0x09DCu ? 0x09A1u : cp == 0x09DDu ? 0x09A2u : cp == 0x09DFu ? 0x09AFu : 0u;
+}
+__device__ __forceinline__ uint32_t hot_word(uint32_t cp) {
+    const uint32_t b = nukta_base(cp);
+    if (b) return b | H_EXP | (7u << H_CCC_SHIFT);  // the nukta's ccc (7): what a following mark meets
+    return hot_of(prop_global(cp));
+}
+__device__ __forceinline__ uint32_t nukta_of(uint32_t base) { return base < 0x0980u ? 0x093Cu : 0x09BCu; }
+
 // LDS holds the hot words of U+0000..U+017F and U+0900..U+09FF (HOT_N entries, 2.5 KB, so that 8
 // waves per SIMD fit); any other code point builds its word from the global property trie
 constexpr uint32_t HOT_LO = 0x180;
@@ -200,27 +221,53 @@ __device__ __forceinline__ uint32_t hot_cp(uint32_t i) { return i < HOT_LO ? i :
 __device__ __forceinline__ uint32_t hot(const uint32_t *H, uint32_t cp) {
     if (cp < HOT_LO) return H[cp];
     if (cp - 0x900u < 0x100u) return H[cp - 0x900u + HOT_LO];
-    return hot_of(prop_global(cp));
+    return hot_word(cp);
 }
 
 // Exact-or-conservative test that NFC leaves the segment around mark m unchanged, given the char
-// p before it (true = "NFC might change something here": take the full path). Stable chars never
-// trigger by themselves; a non-stable char m triggers if it decomposes, if it is a starter that
-// is not a composition second, if it would be reordered before the previous mark, if it could
-// compose with the previous starter, or if it could be reordered into a decomposable previous
-// starter's trailing marks. HF: the same rule over HF's ccc (p_ccc_hf) and HF-stability.
+// p before it (true = "NFC might change something here": take the full path), except for m
+// composing with p itself, which nfc_pair_cand flags and the caller decides exactly (compose_pair).
+// Stable chars never trigger by themselves; a non-stable char m triggers if it decomposes, if it
+// would be reordered before the previous mark, if it is a mark that could compose with the
+// starter before a previous mark, or if it could be reordered into a decomposable previous
+// starter's trailing marks. At a row start only a decomposition changes anything; a starter after
+// a mark is blocked from every earlier starter and never reordered; a mark right after a
+// non-stable starter composes, if at all, with that starter (the pair clause). HF: the same rule
+// over HF's ccc (p_ccc_hf) and HF-stability.
 template <bool HF>
 __device__ __forceinline__ bool nfc_trig(uint32_t m, uint32_t p) {
-    if (p == H_ROWSTART) return true;
     if (m & H_DECOMP) return true;
+    if (p == H_ROWSTART) return false;
     const uint32_t cm = HF && (m & H_HC0) ? 0u : (m >> H_CCC_SHIFT);
     const bool pst = HF ? (p & H_HFST) != 0 : (p & H_STABLE) != 0;
     if (!pst) {
+        if (cm == 0) return false;
         const uint32_t cpv = HF && (p & H_HC0) ? 0u : (p >> H_CCC_SHIFT);
-        return cm == 0 || cm < cpv || ((m & H_SECOND) && cm > cpv);
+        // a mark after a mark: reordered, or a second that may compose with the starter before p
+        // (p a starter: composing with p itself is the pair clause)
+        return cm < cpv || ((m & H_SECOND) && cpv != 0u && cm > cpv);
     }
-    return (cm == 0 && !(m & H_SECOND)) || ((m & H_SECOND) && (p & H_FIRST)) ||
-           ((p & H_DECOMP) && (p & H_STABLE) && cm < (p >> H_CCC_SHIFT));
+    // (a starter after p never moves, and one after p's trailing mark is blocked from p's base)
+    return (cm == 0 && !(m & H_SECOND)) || ((p & H_DECOMP) && (p & H_STABLE) && cm != 0u && cm < (p >> H_CCC_SHIFT));
+}
+// nfc_trig fires only because m, a composition second, may compose with the starter before the
+// single mark p (m is not reordered before p): the caller checks that starter (the char two back)
+__device__ __forceinline__ bool nfc_l_cand(uint32_t m, uint32_t p) {
+    if ((m & H_DECOMP) || p == H_ROWSTART || (p & H_STABLE) || !(m & H_SECOND)) return false;
+    const uint32_t cm = m >> H_CCC_SHIFT, cpv = p >> H_CCC_SHIFT;
+    return cpv != 0u && cm > cpv;
+}
+// nfc_trig fires only because the mark m would be reordered into the trailing marks of p, a stable
+// decomposable starter: the caller checks p's decomposition
+__device__ __forceinline__ bool nfc_d_cand(uint32_t m, uint32_t p) {
+    if ((m & H_DECOMP) || p == H_ROWSTART || !(p & H_STABLE) || !(p & H_DECOMP)) return false;
+    const uint32_t cm = m >> H_CCC_SHIFT;
+    return cm != 0u && cm < (p >> H_CCC_SHIFT);
+}
+// m may compose with the char p right before it (a primary composite's second after a first):
+// the caller looks the pair up (compose_pair)
+__device__ __forceinline__ bool nfc_pair_cand(uint32_t m, uint32_t p) {
+    return p != H_ROWSTART && (m & H_SECOND) && (p & H_FIRST);
 }
 
 // bytes p .. p+3 of an LDS byte array as one little-endian word (two aligned dword reads and one
@@ -410,7 +457,8 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
     uint16_t *dummy = M.w + (sizeof(M.w) / 2 - 64) + lane;
     uint32_t vpos = 0;
     {
-        uint32_t carry_h = H_ROWSTART, rows = 0;
+        uint32_t carry_h = H_ROWSTART, rows = 0, carry_cp = 0, carry_mv = 0, carry_cmp = 0;
+        uint32_t carry_pcp = 0;  // the char two back at lane 0 (lane 62 of the step before)
         const uint32_t plast = np ? np - 1 : 0;
         for (uint32_t c0 = 0; c0 < np; c0 += 64) {
             const uint32_t c = c0 + lane;
@@ -433,26 +481,92 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             uint32_t hw = H[ci];
             const bool cold = chr && !bad && ci == 0u && cp != 0u;
             if (w_ballot(cold)) {
-                if (cold) hw = hot_of(prop_global(cp));
+                if (cold) hw = hot_word(cp);
             }
             const uint32_t h = chr ? (bad ? 0u : hw) : H_ROWSTART;
-            const uint32_t hprev = w_prev(h, carry_h);  // DPP wave_shr:1, lane 0 takes the carry
-            const bool trig = chr && (bad || (!(h & H_STABLE) && nfc_trig<false>(h, hprev)));
+            // a precomposed nukta letter (H_EXP) is base + nukta: the next char is checked against the
+            // nukta, and the letter itself never needs the full NFC (see hot_word)
+            const bool xp = chr && (h & H_EXP);
+            uint32_t hp = h;
+            if (w_ballot(xp)) {
+                if (xp) hp = H[nukta_of(h & 0xFFFFu) - 0x900u + HOT_LO];
+            }
+            uint32_t hprev = w_prev(hp, carry_h);  // DPP wave_shr:1, lane 0 takes the carry
+            uint32_t mv = chr ? (h & 0xFFFFu) : 0u;
+            // A char that composes with the char right before it (rare: behind a ballot): the pair is
+            // looked up exactly; the tile writes the composite itself (the first char's lane emits the
+            // composite's normalize_text map, the second's nothing) unless the first is itself a
+            // composite of this step's making, or the pair straddles two steps and the composite
+            // would change how many entries the first char emitted: those rows fall back.
+            bool cmp = false, pfb = false;
+            uint32_t cmv = 0, ecp = chr && !bad ? cp : 0u;  // ecp: the char as NFC leaves it (a composite)
+            const bool pcand = chr && !bad && !xp && nfc_pair_cand(h, hprev);
+            if (w_ballot(pcand)) {
+                const uint32_t pcp = w_prev(chr && !bad ? cp : 0u, carry_cp);
+                const uint32_t pmv = w_prev(mv, carry_mv);
+                const uint32_t c = pcand ? compose_pair<NF_UCD>(pcp, cp) : 0u;
+                if (c) {
+                    const uint32_t hc = hot(H, c);
+                    cmv = hc & 0xFFFFu;
+                    cmp = true;
+                    hp = hc;  // the next char meets the composite
+                    if (lane == 0 && (carry_cmp || pmv == 0u || cmv == 0u)) pfb = true;  // cross-step, not 1 -> 1
+                }
+                const bool pcmp = w_prev((uint32_t)cmp, 0u) != 0u;  // (all lanes: a DPP read)
+                if (pcmp && chr && (h & H_SECOND)) pfb = true;  // may chain onto a composite: the full NFC
+                if (pfb) cmp = false;
+                if (cmp) ecp = c;
+                hprev = w_prev(hp, carry_h);
+            }
+            // a second after one mark: exact when the char before the mark is a starter with no trailing
+            // mark of its own (m composes with that starter, unblocked, or NFC leaves the three alone);
+            // rare, behind a ballot
+            const bool lcand = chr && !bad && !xp && !(h & H_STABLE) && nfc_l_cand(h, hprev);
+            bool lok = false;
+            if (w_ballot(lcand)) {
+                const uint32_t pcp = w_prev(ecp, carry_cp);
+                const uint32_t ppcp = w_prev(pcp, carry_pcp);
+                const uint32_t pph = hot(H, ppcp);  // (0 at a row start: NUL's word, a starter)
+                const bool pps = (pph >> H_CCC_SHIFT) == 0u && !(pph & H_EXP);
+                lok = lcand && pps && compose_pair<NF_UCD>(ppcp, cp) == 0u;
+            }
+            // a mark reordered into the previous starter's decomposition: exact when that is base + one
+            // mark (the mark and m swap, base + m do not compose, base + its mark recompose: NFC leaves
+            // p m alone); rare, behind a ballot
+            const bool dcand = chr && !bad && !xp && !(h & H_STABLE) && nfc_d_cand(h, hprev);
+            if (w_ballot(dcand)) {
+                const uint32_t pcp = w_prev(ecp, carry_cp);
+                if (dcand) {
+                    const uint2 pr = prop_global(pcp);
+                    const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
+                    lok = len == 2u && compose_pair<NF_UCD>(AK_UT_DECOMP[idx], cp) == 0u;
+                }
+            }
+            const bool trig = chr && (bad || pfb || (!(h & H_STABLE) && !xp && !lok && nfc_trig<false>(h, hprev)));
             if (w_ballot(trig)) {
                 if (trig) M.fb[row] = 1;
             }
-            const uint32_t mv = chr ? (h & 0xFFFFu) : 0u;
+            // the composing pair: this lane emits nothing; the lane before emits the composite (in the
+            // step before: the entry it wrote is patched)
+            const uint32_t cnext = w_next(cmp ? (cmv | 0x10000u) : 0u);  // lane 63: 0 (patched by the next step)
+            if (cmp) mv = 0u;
+            if (cnext) mv = cnext & 0xFFFFu;
+            if (cmp && lane == 0) M.v[vpos - 1] = (uint16_t)cmv;
             const bool two = mark && row > 0;
-            const uint32_t cnt = mark ? (two ? 2u : 1u) : (mv ? 1u : 0u);
+            const uint32_t cnt = mark ? (two ? 2u : 1u) : (mv ? (xp ? 2u : 1u) : 0u);
             uint32_t tot;
             const uint32_t ex = w_exscan(cnt, &tot);
             uint16_t *d0 = cnt ? &M.v[vpos + ex] : dummy;
-            uint16_t *d1 = two ? &M.v[vpos + ex + 1] : dummy;
+            uint16_t *d1 = (two || xp) ? &M.v[vpos + ex + 1] : dummy;
             *d0 = mark ? (two ? V_E : V_B) : (uint16_t)mv;
-            *d1 = V_B;
+            *d1 = two ? V_B : (uint16_t)nukta_of(mv);
             vpos += tot;
             rows += (uint32_t)w_popc(RMK);
-            carry_h = w_bcast(h, 63);
+            carry_h = w_bcast(hp, 63);
+            carry_pcp = w_bcast(ecp, 62);
+            carry_cp = w_bcast(ecp, 63);
+            carry_mv = w_bcast(mv, 63);
+            carry_cmp = w_bcast((uint32_t)cmp, 63);
         }
         if (k > 0) {
             if (lane == 0) M.v[vpos] = V_E;
@@ -720,7 +834,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
         // lanes that emit nothing, so the common case issues no exec-mask juggling.
         uint16_t *dummy = (uint16_t *)M.bytes;
         const uint32_t h_sp = H[0x20];
-        uint32_t carry_h = H_ROWSTART, carry_word = 0, carry_kword = 0xFFFFFFFFu, rs = 0;
+        uint32_t carry_h = H_ROWSTART, carry_word = 0, carry_kword = 0xFFFFFFFFu, rs = 0, carry_x = 0;
         int carry_cls = HF_S;
         const uint32_t vlast = vlen ? vlen - 1 : 0;
         for (uint32_t base = 0; base < vlen; base += 64) {
@@ -758,9 +872,17 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
             const int cls_l = w_shfl(cls, src);
             const uint32_t hprev = pk ? h_l : carry_h;
             const int cprev = pk ? cls_l : carry_cls;
-            // HF-NFC quick check -> row fallback (rare: behind a ballot)
+            // HF-NFC quick check -> row fallback (rare: behind a ballot); a second right after a first
+            // falls back only if HF's tables compose the pair
             const uint64_t RM = w_ballot(keep && (x == V_B || x == V_FB));
-            const bool trig = keep && !special && !(h & H_HFST) && nfc_trig<true>(h, hprev);
+            const bool hfc = keep && !special && !(h & H_HFST);
+            bool trig = hfc && nfc_trig<true>(h, hprev);
+            const bool hpc = hfc && nfc_pair_cand(h, hprev);
+            if (w_ballot(hpc)) {
+                const uint32_t x_l = w_shfl((uint32_t)x, src);
+                const uint32_t xprev = pk ? x_l : carry_x;
+                if (hpc && compose_pair<NF_HFK>(xprev, x)) trig = true;
+            }
             if (w_ballot(trig)) {
                 if (trig) M.fb[rs + w_rank_incl(RM) - 1] = 1;
             }
@@ -791,6 +913,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
                 const int lk = msb64(KM);
                 carry_h = w_bcast(h, lk);
                 carry_cls = w_bcast(cls, lk);
+                carry_x = w_bcast((uint32_t)x, lk);
             }
             carry_word = w_bcast(word, 63);
             if (K2) carry_kword = w_bcast(word, msb64(K2));

@@ -51,6 +51,11 @@ inline uint32_t w_prev(uint32_t v, uint32_t fill) {
     const uint32_t x = w_shfl(v, t_lane ? t_lane - 1 : 0);
     return t_lane ? x : fill;
 }
+// value of lane + 1; lane 63 gets `fill`
+inline uint32_t w_next(uint32_t v, uint32_t fill = 0u) {
+    const uint32_t x = w_shfl(v, t_lane < 63 ? t_lane + 1 : 63);
+    return t_lane < 63 ? x : fill;
+}
 // exclusive prefix sum over lanes; *total gets the wave sum
 inline uint32_t w_exscan(uint32_t v, uint32_t *total) {
     t_wave->slot[t_lane] = v;
@@ -124,6 +129,10 @@ __device__ __forceinline__ T w_bcast(T v, int src) {
 // ds_bpermute); all 64 lanes must be active
 __device__ __forceinline__ uint32_t w_prev(uint32_t v, uint32_t fill) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138, 0xf, 0xf, false);
+}
+// value of lane + 1, lane 63 gets `fill`: DPP wave_shl:1; all 64 lanes must be active
+__device__ __forceinline__ uint32_t w_next(uint32_t v, uint32_t fill = 0u) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130, 0xf, 0xf, false);
 }
 // inclusive wave64 prefix sum in DPP (row_shr 1/2/4/8 within 16-lane rows, then row_bcast 15/31
 // across rows); all 64 lanes must be active

@@ -9,6 +9,8 @@
  *           with elongations and caps; separators ' ', ', ', '! ', '? '.
  *   kind 2  Mixed-Unicode fuzz lines (combining marks, NFC edge cases, emoji/ZWJ, RI,
  *           Hangul, Bengali, exotic whitespace, GB9c chains) — parity stress only.
+ *   kind 3  kind 1 as common Hindi input methods type it: the nukta consonants precomposed
+ *           (U+0958..U+095F, composition exclusions that NFC decomposes), in 12 % of syllables.
  *
  * Every line is a pure function of (seed, kind, line index), so corpora can be generated in
  * parallel and re-generated identically on the GPU box. Integer arithmetic only.
@@ -63,11 +65,13 @@ static void put_str(sink_t *k, const char *s) {
 
 static const uint32_t NUKTA_BASES[] = {0x0915, 0x0916, 0x0917, 0x091C, 0x0921, 0x0922, 0x092B, 0x092F};
 
-static void deva_syllable(rng_t *r, sink_t *k) {
+static void deva_syllable(rng_t *r, sink_t *k, int precomposed) {
     if (rnd(r, 100) < 10) {
         put_cp(k, 0x0905 + rnd(r, 16));
     } else {
-        if (rnd(r, 100) < 3) {               /* decomposed nukta consonant (NFC keeps it decomposed) */
+        if (precomposed && rnd(r, 100) < 12) {  /* precomposed nukta letter (NFC: base + nukta) */
+            put_cp(k, 0x0958 + rnd(r, 8));
+        } else if (rnd(r, 100) < 3) {        /* decomposed nukta consonant (NFC keeps it decomposed) */
             put_cp(k, NUKTA_BASES[rnd(r, 8)]);
             put_cp(k, 0x093C);
         } else {
@@ -85,9 +89,9 @@ static void deva_syllable(rng_t *r, sink_t *k) {
     }
 }
 
-static void deva_word(rng_t *r, sink_t *k) {
+static void deva_word(rng_t *r, sink_t *k, int precomposed) {
     int n = 1 + (int)rnd(r, 4);
-    for (int i = 0; i < n; ++i) deva_syllable(r, k);
+    for (int i = 0; i < n; ++i) deva_syllable(r, k, precomposed);
 }
 
 static const char *SLANG[] = {
@@ -180,7 +184,7 @@ static void gen_line(uint64_t seed, int kind, uint64_t idx, sink_t *k) {
     int first = 1;
     while (k->cps < target) {
         if (!first) {
-            if (kind == 1) {
+            if (kind == 1 || kind == 3) {
                 uint32_t s = rnd(&r, 100);
                 if (s < 70) put_str(k, " ");
                 else if (s < 85) put_str(k, ", ");
@@ -191,8 +195,8 @@ static void gen_line(uint64_t seed, int kind, uint64_t idx, sink_t *k) {
             }
         }
         first = 0;
-        if (kind == 1 && rnd(&r, 2)) roman_word(&r, k);
-        else deva_word(&r, k);
+        if ((kind == 1 || kind == 3) && rnd(&r, 2)) roman_word(&r, k);
+        else deva_word(&r, k, kind == 3);
     }
     if (kind == 0 && rnd(&r, 100) < 15) put_cp(k, 0x0964);
 }

@@ -11,6 +11,7 @@ import numpy as np
 KIND_DEVANAGARI = 0
 KIND_HINGLISH = 1
 KIND_FUZZ = 2
+KIND_HINGLISH_NUKTA = 3  # kind 1 with precomposed nukta letters (U+0958..U+095F), as IMEs type them
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None

@@ -230,7 +230,7 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     static uint2 fast[FAST_N];
     static uint32_t hot_tab[HOT_N];
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
-    for (uint32_t i = 0; i < HOT_N; ++i) hot_tab[i] = hot_of(prop_global(hot_cp(i)));
+    for (uint32_t i = 0; i < HOT_N; ++i) hot_tab[i] = hot_word(hot_cp(i));
     if (n == 0) { out_offs[0] = 0; return 0; }
     const uint64_t half = offs[n] + 2 * n + 64;
     const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
@@ -320,7 +320,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
     for (uint32_t i = 0; i < HOT_N; ++i) {
         const uint32_t cp = hot_cp(i);
-        hot_tab[i] = hot_of(prop_global(cp));
+        hot_tab[i] = hot_word(cp);
         const uint32_t c = spm_code(m->sdev, cp);
         scode[i] = (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
     }
@@ -390,7 +390,7 @@ static int64_t rows_tiles_run(int matras, const uint8_t *in, const uint64_t *off
     static uint32_t hot_tab[HOT_N];
     static uint16_t sc_tab[HOT_N];
     for (uint32_t i = 0; i < FAST_N; ++i) fast[i] = prop_global(i);
-    for (uint32_t i = 0; i < HOT_N; ++i) { hot_tab[i] = hot_of(prop_global(hot_cp(i))); sc_tab[i] = seg_class_of(hot_cp(i)); }
+    for (uint32_t i = 0; i < HOT_N; ++i) { hot_tab[i] = hot_word(hot_cp(i)); sc_tab[i] = seg_class_of(hot_cp(i)); }
     const uint64_t nb = n ? offs[n] : 0;
     // as the launcher: first half = the tile kernel's unit runs, second half = fallback rows' slots
     const uint64_t h8 = RT_NORM_MUL * nb + RT_NORM_ADD * n + 64, h32 = nb + n + 64;

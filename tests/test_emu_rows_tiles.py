@@ -19,7 +19,7 @@ def test_golden_fused(golden, matras, key):
     assert [r["text"] for r, g in zip(short, rows_runs(*res["runs"])) if g != r["sw"]] == []
 
 
-@pytest.mark.parametrize("kind", [0, 1, 2])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("ops", [1, 2, 4, 7])
 def test_synthetic_vs_oracle(kind, ops):
     from akshar_amd import synth

@@ -108,3 +108,14 @@ def test_scaled_scores_cross_the_rebase_bound(spm_model, scale):
     # the rows really cross the bound: a row's summed piece scores is far below -1e5
     first = ref[ro[0]:ro[1]]
     assert float(np.sum(m.scores[first])) < -1e5
+
+
+def test_precomposed_nukta_letters(em, spm_model):
+    """IME-typed Hindi (synthetic kind 3: precomposed nukta letters) through the SentencePiece tile
+    kernel: no fallback rows, ids equal the oracle's."""
+    from akshar_amd import synth
+    buf, offs = synth.generate(synth.KIND_HINGLISH_NUKTA, 300, seed=22)
+    ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=4)
+    assert emu.last_fallback_rows() == 0
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)

@@ -93,3 +93,59 @@ def test_work_queue_waves_vs_oracle(em, bpe_model):
     ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8, waves=3)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_precomposed_nukta_letters_stay_in_the_tile(em, bpe_model):
+    """The precomposed nukta letters (U+0958..U+095F, U+09DC/DD/DF: NFC = base + nukta) are
+    expanded by the tile front end itself: IME-typed Hindi (synthetic kind 3) sends no row to
+    the fallback kernels, and the ids equal the oracle's, also with the letters at row starts,
+    after a virama, doubled, followed by a nukta or by a mark of ccc < 7 (U+0334, which NFC reorders
+    before the nukta: that row still falls back), and in Bengali."""
+    from akshar_amd import synth
+    buf, offs = synth.generate(synth.KIND_HINGLISH_NUKTA, 400, seed=21)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=8)
+    assert emu.last_fallback_rows() == 0
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    texts = ["क़लम", "ज़िंदगी फ़िल्म", "क्ख़", "ड़ढ़", "क़़", "ग̴़", "য়াড়ি ঢ়", "xक़", "क़", "ज़्य़",
+             "फ़॑", "ख़ ख़ ख़ ख़", "ज़ज़ज़ज़", "क़़ँ", "ऩ ऱ ऴ"]
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=4)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)
+
+
+# (text, what the row tests) as code points: NFC leaves NFC_SAME alone and changes every NFC_CHANGES row
+NFC_SAME = ["x\u0316\u0301",       # second after one mark, nothing to compose with two back
+            "q\u0327\u0301 y",     # the same after a starter that is a first of other pairs
+            "\u0130\u093c",        # a mark of lower ccc after U+0130 (I + U+0307): swaps, recomposes
+            "\u0130\u093c\u0952",  # ... then a mark of higher ccc
+            "\u0130\u09cd", "\u0130\u09be",  # a starter second after U+0130, or a virama
+            "\u0931\u09be",        # a starter second after a decomposable starter with a trailing mark
+            "\u09cb\u0301",        # a mark after a stable composite
+            "\u0929\u0951\u0301"]  # two marks after a decomposable starter
+NFC_CHANGES = ["a\u0316\u0301",      # second after one mark, composes with the starter two back
+               "\u0130\u0328",        # I + U+0328 compose once the marks swap
+               "\u0130\u093c\u0328",  # ... behind a mark of lower ccc
+               "\u01d6\u0323",        # base + two marks: the conservative clause
+               "e\u0302\u0301",       # a chain of compositions
+               "\u0950\u093c\u0334"]  # a reorder
+NFC_IN_TILE = ["\u0928\u093c", "\u09c7\u09be", "A\u030a", "ka\u0301"]  # a composing pair: in-tile
+
+
+def test_nfc_clauses_are_exact(em, bpe_model):
+    """The in-tile NFC checks (ak_tile.h nfc_trig and the exact pair / two-back / decomposition
+    clauses of pass D2) send a row to the fallback kernels only where NFC changes it, for each clause:
+    a composition second after one mark (composes with the starter two back or not), a mark that NFC
+    moves into the previous starter's base + mark decomposition (U+0130 = I + U+0307), a starter
+    second after a decomposable starter, a second after an in-tile composite (falls back: it may chain);
+    a composing pair is composed in the tile. The ids equal the oracle's either way."""
+    import unicodedata
+    assert all(unicodedata.normalize("NFC", t) == t for t in NFC_SAME)
+    assert all(unicodedata.normalize("NFC", t) != t for t in NFC_CHANGES + NFC_IN_TILE)
+    for texts, fb in ((NFC_SAME, 0), (NFC_CHANGES, len(NFC_CHANGES)), (NFC_IN_TILE, 0)):
+        buf, offs = O.pack(texts)
+        ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=4)
+        assert emu.last_fallback_rows() == fb
+        ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+        assert rows_ints(ids, oo) == rows_ints(ref, ro)

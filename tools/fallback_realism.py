@@ -5,7 +5,8 @@ and what that costs: for each input set, BPE and SentencePiece encode and the fu
 
 Sets (each replicated to --rows rows so the launch is full-size): the reference's data/corpus.txt
 lines (from tests/golden/cli_golden.json.gz, as the CLI read them), the golden fuzz / alphabet /
-adversarial / NFKC sets, and the synthetic Hinglish bench rows. Prints one JSON line.
+adversarial / NFKC sets, the synthetic Hinglish bench rows and the same with precomposed nukta
+letters (U+0958..095F as IME-typed Hindi has them: synth kind 3). Prints one JSON line.
   python tools/fallback_realism.py [--rows 1000000]
 """
 import argparse
@@ -62,9 +63,10 @@ def main():
     spm = engine.SPM(os.path.join(ROOT, "models", "akshar.model"))
     out = {"rows": args.rows, "sets": {}}
     inputs = {name: (texts * (args.rows // len(texts) + 1))[:args.rows] for name, texts in sets().items()}
-    for name, texts in list(inputs.items()) + [("synthetic_hinglish", None)]:
-        if texts is None:
-            buf, offs = synth.generate(synth.KIND_HINGLISH, args.rows, seed=1234)
+    synthetic = [("synthetic_hinglish", synth.KIND_HINGLISH), ("synthetic_hindi_nukta", synth.KIND_HINGLISH_NUKTA)]
+    for name, texts in list(inputs.items()) + synthetic:
+        if isinstance(texts, int):
+            buf, offs = synth.generate(texts, args.rows, seed=1234)
             pad = np.zeros(len(buf) + 32, np.uint8)
             pad[:len(buf)] = buf
             gb, go = engine.to_device(pad, offs.astype(np.int64))
@@ -77,6 +79,9 @@ def main():
         for k in ("bpe", "spm", "analyze"):
             res[k]["fallback_rate"] = round(res[k]["fallback_rows"] / args.rows, 5)
         out["sets"][name] = res
+        if name == "synthetic_hindi_nukta":  # precomposed nukta letters vs the bench corpus, same size
+            h = out["sets"]["synthetic_hinglish"]
+            res["rate_vs_hinglish"] = {k: round(res[k]["mb_s"] / h[k]["mb_s"], 3) for k in ("bpe", "spm", "analyze")}
         print(name, json.dumps(res), file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 
