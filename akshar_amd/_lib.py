@@ -68,6 +68,7 @@ SIGNATURES = {
     "ak_profile_tile_passes": (I32, [P, ctypes.POINTER(U64), I32]),
     "ak_profile_tile_counters": (I32, [P, ctypes.POINTER(U64), I32]),
     "ak_bpe_cache_info": (I32, [P, ctypes.POINTER(U64)]),
+    "ak_spm_cache_info": (I32, [P, ctypes.POINTER(U64)]),
     "ak_ws_fallback_rows": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
     "ak_normalize_cap": (U64, [U64, U64]),
     "ak_segment_cap": (U64, [U64, U64]),

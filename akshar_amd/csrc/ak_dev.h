@@ -808,6 +808,8 @@ struct SpmDev {
     float unk_score;       // min_score - 10
     float abs_score_max;   // largest |score| a lattice node can add (pieces, unk): the tile path's rounding bound
     uint16_t ws_code;      // tile path W entry of U+2581 (0x8000 | code, or the code point if no piece holds it)
+    const uint32_t *wc;    // tile path: the word cache (ak_swc.h; null = off)
+    uint32_t wc_mask;
 };
 
 // word chars are stored as 0x80000000 | code for chars some piece holds, the plain code point

@@ -171,6 +171,9 @@ struct ak_spm {
     uint32_t n_nodes = 0;
     DecTab dec{};
     uint8_t *d_dec = nullptr;
+    uint32_t *d_wc = nullptr;     // the word cache (ak_swc.h), tile path only
+    akb::SwcStats wc{};
+    uint32_t wc_slots = 0;
 };
 
 int ak::model_kind(const void *h) {
@@ -241,6 +244,15 @@ extern "C" int ak_bpe_cache_info(const ak_bpe *m, uint64_t info[4]) {
     info[1] = m->ptc.keys;
     info[2] = m->ptc.stored;
     info[3] = m->ptc.multi;
+    return AK_OK;
+}
+
+extern "C" int ak_spm_cache_info(const ak_spm *m, uint64_t info[4]) {
+    if (!m || !info) return fail(AK_ERR_ARG, "ak_spm_cache_info: null argument");
+    info[0] = m->wc_slots;
+    info[1] = m->wc.words;
+    info[2] = m->wc.stored;
+    info[3] = m->wc.skipped;
     return AK_OK;
 }
 
@@ -341,6 +353,21 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.unk_score = t.min_score - 10.0f;
     m->dev.abs_score_max = t.abs_score_max;
     m->dev.ws_code = t.ws_code;
+    // the tile kernel's word cache (ak_swc.h; AK_SWC=0 leaves it off: development aid, AK_SWC_BITS=b
+    // forces 2^b slots: tests of collisions and dropped words)
+    const char *we = getenv("AK_SWC");
+    if (!(we && we[0] == '0')) {
+        const char *wb = getenv("AK_SWC_BITS");
+        const int bits = wb ? std::max(0, std::min(24, atoi(wb))) : -1;
+        std::vector<uint32_t> tab;
+        uint32_t mask = 0;
+        akb::build_spm_wcache(t, m->dev.unk_score, unk_id, n, piece_bytes, piece_offs, types, bits, tab, mask, m->wc);
+        HIP_TRY(hipMalloc(&m->d_wc, tab.size() * sizeof(uint32_t)));
+        HIP_TRY(hipMemcpy(m->d_wc, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        m->dev.wc = m->d_wc;
+        m->dev.wc_mask = mask;
+        m->wc_slots = mask + 1;
+    }
     {   // DecodeIds tables: pieces with U+2581 -> ' ', kinds, byte values of <0xXX>
         std::vector<uint8_t> text, kind(n), bv(n, 0);
         std::vector<uint32_t> off(n + 1, 0);
@@ -384,6 +411,7 @@ extern "C" void ak_spm_free(ak_spm *m) {
     (void)hipFree(m->d_code_cp);
     (void)hipFree(m->d_byte_ids);
     (void)hipFree(m->d_dec);
+    (void)hipFree(m->d_wc);
     delete m;
 }
 

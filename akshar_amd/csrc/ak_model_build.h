@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "ak_ptc.h"
+#include "ak_swc.h"
 
 namespace akb {
 
@@ -430,6 +431,156 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
     const uint16_t wc = wpg ? out.cmap[(size_t)wpg * 128 + (0x2581u & 127u)] : 0;
     out.ws_code = wc ? (uint16_t)(0x8000u | wc) : (uint16_t)0x2581u;
     return "";
+}
+
+// The SentencePiece word cache (ak_swc.h). spm_word_solve is the host restatement of the tile
+// path's base-0 word lattice (ak_tile_spm.h word_dp<true>: the same float adds in the same order,
+// first arrival wins ties, the same rebase, the same margin bookkeeping) over the W codes w[0..n):
+// the pieces along the best path (back[] entries, first piece first) and the smallest winning
+// margin. False when the path holds an unknown char or more than SWC_MAXP pieces (not cached).
+inline bool spm_word_solve(const SpmTables &t, float unk_score, int unk_id, const std::vector<uint16_t> &w,
+                           std::vector<uint32_t> &pieces, float &minm) {
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    const int L = (int)w.size();
+    std::vector<float> best(L + 1, 0.0f);
+    std::vector<uint32_t> back(L + 1, NONE);
+    minm = 3.0e38f;
+    auto relax = [&](int ee, float cand, uint32_t id, uint32_t len) {
+        const uint32_t bk = back[ee];
+        if (bk == NONE || cand > best[ee]) {
+            if (bk != NONE) minm = std::fmin(minm, cand - best[ee]);
+            best[ee] = cand;
+            back[ee] = (id << 8) | len;
+        } else {
+            minm = std::fmin(minm, best[ee] - cand);
+        }
+    };
+    int reach = 0;
+    for (int s = 0; s < L; ++s) {
+        float till = s == 0 ? 0.0f : best[s];
+        if (till < -100000.0f || till > 100000.0f) {
+            for (int q = s + 1; q <= reach; ++q)
+                if (back[q] != NONE) best[q] -= till;
+            till = 0.0f;
+        }
+        bool has_single = false;
+        int node = 0, nb = t.root_base;
+        for (int k = s; k < L; ++k) {
+            const uint32_t v = w[k];
+            if (!(v & 0x8000u)) break;
+            const int tt = nb + (int)(v & 0x7FFFu);
+            if (tt < 0 || (uint32_t)tt >= t.n_nodes) break;
+            const int *e = &t.trie[4 * (size_t)tt];
+            if (e[0] != node) break;
+            node = tt;
+            nb = e[1];
+            const int value = e[2];
+            if (value < 0 || ((value >> 24) & 3) == 2) continue;
+            float sc;
+            memcpy(&sc, &e[3], 4);
+            const float cand = sc + till;
+            const int ee = k + 1;
+            reach = std::max(reach, ee);
+            relax(ee, cand, (uint32_t)(value & 0xFFFFFF), (uint32_t)(ee - s));
+            if (k == s) has_single = true;
+        }
+        if (!has_single) {
+            reach = std::max(reach, s + 1);
+            relax(s + 1, unk_score + till, (uint32_t)unk_id, 1u);
+        }
+    }
+    pieces.clear();
+    for (int e = L; e > 0;) {
+        const uint32_t bk = back[e];
+        if ((int)(bk >> 8) == unk_id || pieces.size() >= (size_t)aks::SWC_MAXP) return false;
+        pieces.insert(pieces.begin(), bk);
+        e -= (int)(bk & 0xFFu);
+    }
+    return true;
+}
+
+struct SwcStats {
+    uint32_t words = 0;    // "▁"-initial piece strings of 2..SWC_MAXN codes
+    uint32_t stored = 0;   // placed in the table
+    uint32_t skipped = 0;  // solution with an unknown char or more than SWC_MAXP pieces (never stored)
+};
+
+// bits < 0: the table size from the word count (>= 2.5 slots per word); bits >= 0 forces 2^bits
+// slots (tests: tiny tables force collisions and drops)
+inline void build_spm_wcache(const SpmTables &t, float unk_score, int unk_id, uint32_t n, const uint8_t *piece_bytes,
+                             const uint64_t *piece_offs, const uint8_t *types, int bits, std::vector<uint32_t> &tab,
+                             uint32_t &mask, SwcStats &st) {
+    using namespace aks;
+    st = SwcStats{};
+    struct Key { std::vector<uint16_t> w; std::vector<uint32_t> pieces; float minm; };
+    std::vector<Key> keys;
+    std::vector<uint32_t> cps;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (types[i] != 1 && types[i] != 4 && types[i] != 5) continue;
+        const uint64_t a = piece_offs[i], b = piece_offs[i + 1];
+        if (b < a + 4 || memcmp(piece_bytes + a, "\xe2\x96\x81", 3) != 0) continue;
+        if (utf8_decode_piece(std::string((const char *)piece_bytes + a, (size_t)(b - a)), cps)) continue;
+        if (cps.size() < 2 || cps.size() > (size_t)SWC_MAXN) continue;
+        std::vector<uint16_t> w;
+        for (uint32_t cp : cps) {
+            const uint16_t pg = cp < 0x110000u ? t.cmap_page[cp >> 7] : 0;
+            const uint16_t c = pg ? t.cmap[(size_t)pg * 128 + (cp & 127u)] : 0;
+            if (!c) break;
+            w.push_back((uint16_t)(0x8000u | c));
+        }
+        if (w.size() != cps.size()) continue;
+        ++st.words;
+        Key k{w, {}, 0.0f};
+        if (spm_word_solve(t, unk_score, unk_id, w, k.pieces, k.minm)) keys.push_back(std::move(k));
+        else ++st.skipped;
+    }
+    if (bits < 0) {
+        bits = 10;
+        while ((1ull << bits) * 2 < 5ull * keys.size()) ++bits;
+    }
+    const uint32_t size = 1u << bits;
+    mask = size - 1;
+    tab.assign((size_t)size * SWC_ENTRY_DWORDS, 0u);
+    auto pack = [](const std::vector<uint16_t> &w, uint32_t q[8]) {
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t lo = 2 * k < (int)w.size() ? w[2 * k] : 0u;
+            const uint32_t hi = 2 * k + 1 < (int)w.size() ? w[2 * k + 1] : 0u;
+            q[k] = lo | (hi << 16);
+        }
+    };
+    auto hash_of = [&](const std::vector<uint16_t> &w) {
+        uint32_t q[8];
+        pack(w, q);
+        return swc_hash((uint32_t)w.size(), q);
+    };
+    std::vector<int32_t> at(size, -1);
+    for (int32_t k = 0; k < (int32_t)keys.size(); ++k) {
+        int32_t cur = k;
+        uint32_t h = hash_of(keys[cur].w);
+        uint32_t s = swc_slot1(h, mask);
+        for (int kick = 0; kick < 256 && cur >= 0; ++kick) {
+            std::swap(cur, at[s]);
+            if (cur < 0) break;
+            h = hash_of(keys[cur].w);
+            const uint32_t s1 = swc_slot1(h, mask), s2 = swc_slot2(h, mask);
+            s = s1 == s ? s2 : s1;
+        }
+        // cur >= 0 here: a word left without a slot is dropped (a cache, not a dictionary)
+    }
+    for (uint32_t s = 0; s < size; ++s) {
+        if (at[s] < 0) continue;
+        const Key &k = keys[at[s]];
+        const uint32_t h = hash_of(k.w);
+        uint32_t *e = &tab[(size_t)s * SWC_ENTRY_DWORDS];
+        e[0] = (e[0] & SWC_FLAG) | swc_head(h, (uint32_t)k.w.size()) | ((uint32_t)k.pieces.size() << 17);
+        memcpy(&e[1], &k.minm, 4);
+        for (size_t i = 0; i < k.pieces.size(); ++i) e[2 + i] = k.pieces[i];
+        uint32_t q[8];
+        pack(k.w, q);
+        for (int i = 0; i < 8; ++i) e[8 + i] = q[i];
+        ++st.stored;
+        if (swc_slot1(h, mask) != s) tab[(size_t)swc_slot1(h, mask) * SWC_ENTRY_DWORDS] |= SWC_FLAG;
+    }
 }
 
 }  // namespace akb

@@ -29,6 +29,7 @@
 // tau = (L + 3) M 2^-22 for a word of L chars is sufficient.
 // Reference semantics: normalize.py:117-148, tokenizer.py:190-191, cli.py:232-248.
 #pragma once
+#include "ak_swc.h"
 #include "ak_tile.h"
 
 namespace ak {
@@ -57,6 +58,7 @@ struct SpmWaveMem {
     float best[S_W + AK_SPM_SELECT_RELAX];     // Viterbi best score per W position (word-local)
     uint32_t back[S_W + AK_SPM_SELECT_RELAX];  // best piece ending here: id << 8 | chars ([S_W]: dummy)
     uint8_t wrow[S_WORDS];                   // row of each word
+    uint8_t wmiss[S_WORDS];                  // words the word cache did not hold (pass V)
     uint8_t fb[T_MAXR];
     uint8_t mfail[T_MAXR];                   // row has a lattice node within the rounding bound (pass V2)
     uint16_t rowend[T_MAXR];
@@ -269,6 +271,39 @@ __device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &
     return cnt;
 }
 
+// The word cache probe (ak_swc.h) for the n W codes packed in q (two per dword, 0 past n): the
+// entry's dwords 0-3 (head, margin, pieces 0-1) in hd and its address, or null. The whole stored
+// code sequence is compared, so a hash collision is a miss.
+__device__ __forceinline__ const uint4 *swc_probe(const SpmDev &m, uint32_t n, const uint32_t q[8], uint4 &hd) {
+    const uint32_t h = aks::swc_hash(n, q);
+    const uint32_t head = aks::swc_head(h, n);
+    uint32_t s = aks::swc_slot1(h, m.wc_mask);
+    for (int probe = 0; probe < 2; ++probe) {
+        const uint4 *e = (const uint4 *)(m.wc + (size_t)s * aks::SWC_ENTRY_DWORDS);
+        const uint4 a = e[0];
+        if ((a.x & aks::SWC_HEAD_MASK) == head) {
+            const uint4 c0 = e[2], c1 = e[3];
+            if (c0.x == q[0] && c0.y == q[1] && c0.z == q[2] && c0.w == q[3] && c1.x == q[4] && c1.y == q[5] &&
+                c1.z == q[6] && c1.w == q[7]) {
+                hd = a;
+                return e;
+            }
+        }
+        if (!(a.x & aks::SWC_FLAG)) break;
+        s = aks::swc_slot2(h, m.wc_mask);
+    }
+    return nullptr;
+}
+
+// The rounding-bound test of a word solved from base 0 (header comment): false = the row redoes
+// its words from the carried base. M = (chars from the row start to the word end + 1) x the
+// largest |score|, at most 1e5 + that score.
+__device__ __forceinline__ bool spm_margin_ok(const SpmWaveMem &M, const SpmDev &m, int row, int p0, int p1, float minm) {
+    const float Mb = fminf((float)(p1 - (int)M.rowpos[row] + 1) * m.abs_score_max, SPM_REBASE + m.abs_score_max) + 1.0f;
+    const float tau = (float)(p1 - p0 + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
+    return minm > tau;
+}
+
 template <int FLAGS>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
                         SpmWaveMem &M, PassClock &pc) {
@@ -341,14 +376,68 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     w_sync();
     pc.mark(TP_E);
 
-    // ---------------- pass V: lane per word, Viterbi from base 0 with the running margin check
-    // (word_dp); a row with a close call is redone exactly below (pass V2)
+    // ---------------- pass V: lane per word. First the word cache (ak_swc.h): a hit writes its stored
+    // pieces and applies the margin test to its stored margin; the words it misses are listed and
+    // then solved 64 at a time, lane per word, by the Viterbi from base 0 with the running margin
+    // (word_dp_flat). A row with a close call is redone exactly below (pass V2).
     uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
     for (uint32_t i = (uint32_t)lane; i < wlen; i += 64) M.back[i] = BK_NONE;  // word_dp_flat's entry state
     w_sync();
+    uint32_t nmiss = 0;
     for (uint32_t jb = 0; jb < nw; jb += 64) {
         const uint32_t j = jb + (uint32_t)lane;
         const bool act = j < nw;
+        const int row = act ? (int)wrow[j] : 0;
+        const int p0 = act ? (int)starts[j] : 0;
+        const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
+        bool hit = false;
+        if (m.wc) {
+            const int n = p1 - p0;
+            bool cand = act && n >= 2 && n <= aks::SWC_MAXN;
+            uint32_t q[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i0 = p0 + 2 * k, i1 = i0 + 1;
+                const uint32_t lo = cand && 2 * k < n ? (uint32_t)M.w[i0] : 0u;
+                const uint32_t hi = cand && 2 * k + 1 < n ? (uint32_t)M.w[i1] : 0u;
+                cand = cand && (2 * k >= n || (lo & W_CODED)) && (2 * k + 1 >= n || (hi & W_CODED));
+                q[k] = lo | (hi << 16);
+            }
+            uint4 hd = make_uint4(0, 0, 0, 0);
+            const uint4 *e = nullptr;
+            if (cand) e = swc_probe(m, (uint32_t)n, q, hd);
+            hit = e != nullptr;
+            pc.count(TC_PROBES, w_ballot(cand));
+            pc.count(TC_HITS, w_ballot(hit));
+            if (hit) {
+                const uint32_t np = (hd.x >> 17) & 7u;
+                uint4 more = make_uint4(0, 0, 0, 0);
+                if (np > 2) more = e[1];
+                int s = p0;
+#pragma unroll
+                for (int i = 0; i < aks::SWC_MAXP; ++i) {
+                    const uint32_t pe = i == 0 ? hd.z : i == 1 ? hd.w : i == 2 ? more.x : i == 3 ? more.y : i == 4 ? more.z : more.w;
+                    if ((uint32_t)i < np) {
+                        const int len = (int)(pe & 0xFFu);
+                        nxt[s] = (uint8_t)len;
+                        M.back[s + len] = pe;
+                        s += len;
+                    }
+                }
+                wcnt[j] = (uint16_t)np;
+                if (!spm_margin_ok(M, m, row, p0, p1, __uint_as_float(hd.y))) M.mfail[row] = 1;
+            }
+        }
+        const bool miss = act && !hit;
+        const uint64_t MM = w_ballot(miss);
+        if (miss) M.wmiss[nmiss + w_rank(MM)] = (uint8_t)j;
+        nmiss += (uint32_t)w_popc(MM);
+    }
+    w_sync();
+    for (uint32_t ib = 0; ib < nmiss; ib += 64) {
+        const uint32_t i = ib + (uint32_t)lane;
+        const bool act = i < nmiss;
+        const uint32_t j = act ? (uint32_t)M.wmiss[i] : 0u;
         const int row = act ? (int)wrow[j] : 0;
         const int p0 = act ? (int)starts[j] : 0;
         const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
@@ -359,11 +448,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const float minm = word_dp_flat(M, m, p0, p1);
 #endif
         if (act) {
-            // rounding bound of this word (header comment): M = (chars from the row start to the word
-            // end + 1) x the largest |score|, at most 1e5 + that score
-            const float Mb = fminf((float)(p1 - (int)M.rowpos[row] + 1) * m.abs_score_max, SPM_REBASE + m.abs_score_max) + 1.0f;
-            const float tau = (float)(p1 - p0 + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
-            if (!(minm > tau)) M.mfail[row] = 1;
+            if (!spm_margin_ok(M, m, row, p0, p1, minm)) M.mfail[row] = 1;
             wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
         }
     }

@@ -363,6 +363,13 @@ class SPM:
                                            m.byte_ids.ctypes.data, ctypes.byref(h)), "ak_spm_create")
         self.h = h
 
+    def cache_info(self):
+        """The word cache (include/akshar.h ak_spm_cache_info): slots, "▁" words found, words
+        stored, words whose solution holds an unknown char or more than 6 pieces."""
+        info = (ctypes.c_uint64 * 4)()
+        check(_lib.lib().ak_spm_cache_info(self.h, info), "ak_spm_cache_info")
+        return {"slots": info[0], "words": info[1], "stored": info[2], "skipped": info[3]}
+
     @classmethod
     def load(cls, path, dev=None):
         """The device model read by the library itself (ak_spm_load: the protobuf parsed in C++)."""

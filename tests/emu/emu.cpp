@@ -30,6 +30,10 @@ struct EmuModel {
     SpmDev sdev{};
     std::vector<float> scores;
     std::vector<int32_t> byte_ids;
+    std::vector<uint32_t> wc;   // the SPM word cache (ak_swc.h)
+    akb::SwcStats wc_stats;
+    std::vector<uint8_t> piece_bytes, types;
+    std::vector<uint64_t> piece_offs;
 };
 
 extern "C" void *emu_bpe_create(uint32_t n_single, const uint32_t *cp, const uint32_t *id, uint32_t n_merges,
@@ -99,7 +103,42 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->sdev.unk_score = m->spm.min_score - 10.0f;
     m->sdev.abs_score_max = m->spm.abs_score_max;
     m->sdev.ws_code = m->spm.ws_code;
+    m->piece_bytes.assign(bytes, bytes + offs[n]);
+    m->piece_offs.assign(offs, offs + n + 1);
+    m->types.assign(types, types + n);
+    // the word cache as ak_spm_create builds it (emu_spm_set_wc rebuilds or drops it)
+    uint32_t mask = 0;
+    akb::build_spm_wcache(m->spm, m->sdev.unk_score, unk_id, n, bytes, offs, types, -1, m->wc, mask, m->wc_stats);
+    m->sdev.wc = m->wc.data();
+    m->sdev.wc_mask = mask;
     return m;
+}
+
+extern "C" uint64_t emu_spm_wc_table(void *model, const uint32_t **tab) {
+    EmuModel *m = (EmuModel *)model;
+    *tab = m->wc.data();
+    return m->wc.size();
+}
+
+// bits: -2 no cache, -1 sized from the word count, >= 0 forces 2^bits slots; info[4] as ak_spm_cache_info
+extern "C" void emu_spm_set_wc(void *model, int bits, uint64_t *info) {
+    EmuModel *m = (EmuModel *)model;
+    m->wc.clear();
+    m->sdev.wc = nullptr;
+    m->sdev.wc_mask = 0;
+    m->wc_stats = akb::SwcStats{};
+    if (bits >= -1) {
+        uint32_t mask = 0;
+        const uint32_t n = (uint32_t)m->types.size();
+        akb::build_spm_wcache(m->spm, m->sdev.unk_score, m->sdev.unk_id, n, m->piece_bytes.data(), m->piece_offs.data(),
+                              m->types.data(), bits, m->wc, mask, m->wc_stats);
+        m->sdev.wc = m->wc.data();
+        m->sdev.wc_mask = mask;
+    }
+    info[0] = m->sdev.wc ? (uint64_t)m->sdev.wc_mask + 1 : 0;
+    info[1] = m->wc_stats.words;
+    info[2] = m->wc_stats.stored;
+    info[3] = m->wc_stats.skipped;
 }
 
 extern "C" void emu_free(void *m) { delete (EmuModel *)m; }
@@ -337,8 +376,11 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     ta.counts = counts.data(); ta.fb_list = fbl.data(); ta.fb_count = &fbn; ta.fb2_list = fb2.data();
     ta.fb2_count = &fb2n; ta.next_unit = &qnext; ta.err = &err;
     ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
+    std::vector<uint64_t> prof(T_NPROF, 0);
+    ta.passprof = prof.data();  // the pass clocks read 0 here; the counters are real
     std::vector<SpmWaveMem> M(g_waves);
     run_waves([&](int w) { spm_tiles_wave<3>(ta, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
+    for (int i = 0; i < T_NCTR; ++i) g_last_ctr[i] = prof[T_NPASS + i];
     if (err) return -1;
     g_last_fb = fbn;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }

@@ -15,7 +15,7 @@ def lib():
     if _L is None:
         so = os.path.join(HERE, "_emu.so")
         srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
-                                                   ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h", "ak_ptc.h",
+                                                   ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h", "ak_ptc.h", "ak_swc.h",
                                                     "ak_tile.h", "ak_tile_spm.h", "ak_tile_rows.h", "ak_wave.h")]
         srcs.append(os.path.join(HERE, "..", "..", "include", "akshar.h"))
         if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
@@ -39,6 +39,9 @@ def lib():
         L.emu_bpe_ptc_table.restype = ctypes.c_uint64
         L.emu_bpe_ptc_table.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))]
         L.emu_last_counters.argtypes = [P]
+        L.emu_spm_set_wc.argtypes = [P, ctypes.c_int, P]
+        L.emu_spm_wc_table.restype = ctypes.c_uint64
+        L.emu_spm_wc_table.argtypes = [P, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))]
         L.emu_run.restype = ctypes.c_int64
         L.emu_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_uint64, P, P,
                               ctypes.c_uint64, P]
@@ -74,6 +77,18 @@ class Model:
         lib().emu_bpe_set_ptc(self.h, -2 if bits is None else bits, len(self.bpe.single_cp),
                               self.bpe.single_id.ctypes.data, len(mg), mg.ctypes.data, info)
         return {"slots": info[0], "keys": info[1], "stored": info[2], "multi": info[3]}
+
+    def set_wc(self, bits=-1):
+        """Rebuild the SPM word cache (bits -1: sized from the words, >= 0: 2^bits slots, None: off);
+        returns ak_spm_cache_info's fields."""
+        info = (ctypes.c_uint64 * 4)()
+        lib().emu_spm_set_wc(self.h, -2 if bits is None else bits, info)
+        return {"slots": info[0], "words": info[1], "stored": info[2], "skipped": info[3]}
+
+    def wc_table(self):
+        p = ctypes.POINTER(ctypes.c_uint32)()
+        n = lib().emu_spm_wc_table(self.h, ctypes.byref(p))
+        return np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
 
     def ptc_table(self):
         p = ctypes.POINTER(ctypes.c_uint32)()
@@ -161,7 +176,7 @@ def rows_tiles(ops, buf, offs, matras=False, rows=16):
 
 
 def last_counters():
-    """(pre-token cache probes, hits) of the last bpe_tiles call."""
+    """(cache probes, hits) of the last bpe_tiles (pre-token cache) or spm_tiles (word cache) call."""
     out = (ctypes.c_uint64 * 8)()
     lib().emu_last_counters(out)
     return int(out[0]), int(out[1])
