@@ -11,6 +11,10 @@ if os.environ.get("AK_LIB_VARIANT"):  # development aid: A/B a prebuilt variant 
     LIB_PATH = os.path.join(_HERE, "_variants", os.environ["AK_LIB_VARIANT"] + ".so")
 
 AK_OK = 0
+AK_ERR_ARG = -1
+AK_ERR_HIP = -2
+AK_ERR_UNSUPPORTED = -3
+AK_ERR_NOMEM = -4
 AK_NORM_LOWER = 1
 AK_NORM_CLEAN = 2
 AK_RAW = -1
@@ -62,6 +66,8 @@ SIGNATURES = {
     "ak_analyze": (I32, [P, I32, I32, P, P, U64, P, U64, P, P, U64, P, P, P, U64, P, P, P]),
     "ak_bpe_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
     "ak_spm_encode": (I32, [P, P, I32, P, P, U64, P, U64, P, P, P]),
+    "ak_bpe_encode_host": (I32, [P, P, I32, P, U64, P, U64, ctypes.POINTER(U64), P]),
+    "ak_spm_encode_host": (I32, [P, P, I32, P, U64, P, U64, ctypes.POINTER(U64), P]),
     "ak_profile_enable": (I32, [I32]),
     "ak_profile_read": (I32, [I32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
     "ak_profile_reset": (None, []),

@@ -524,6 +524,8 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->huge_mem);
     (void)hipFree(w->stage8);
     (void)hipFree(w->acounts);
+    (void)hipFree(w->dev1);
+    (void)hipHostFree(w->pin);
     delete w;
 }
 
@@ -842,6 +844,102 @@ extern "C" int ak_analyze(ak_ws *w, int flags, int matras, const uint8_t *in, co
     }
     AnalyzeOut o{norm, norm_cap, norm_offs, clusters, cl_cap, cl_offs, runs, labels, run_cap, run_offs};
     return launch_analyze(flags, w, a, o, (hipStream_t)stream);
+}
+
+int ak::ws_total_bytes(AkWs *w, const uint64_t *offs, uint64_t n, hipStream_t st, uint64_t *nbytes) {
+    if (w->host_nbytes != ~0ull) {
+        *nbytes = w->host_nbytes;
+        return AK_OK;
+    }
+    HIP_TRY(hipMemcpyAsync(nbytes, offs + n, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return AK_OK;
+}
+
+// the workspace's error words (ak_ws_check) next to the call's results, for the one read-back
+__global__ void k_err_words(const uint32_t *ctr, const uint32_t *misc, uint32_t *dst) {
+    dst[0] = ctr[CTR_ERR];
+    dst[1] = misc ? misc[1] : 0u;
+}
+
+// ak_*_encode_host: one row through pinned host staging. Device staging layout (16-byte aligned):
+// [offs 2 x u64 | bytes, padded | out_offs 2 x u64 | error words | ids dcap x u32]; the first two
+// travel host->device in one copy, the last three device->host in one copy.
+template <class Enc>
+static int encode_host(ak_ws *w, const uint8_t *text, uint64_t len, int32_t *ids, uint64_t cap, uint64_t *n_ids,
+                       uint64_t dcap, hipStream_t st, const char *who, Enc enc) {
+    if (!w || !n_ids || (len && !text) || (cap && !ids)) return fail(AK_ERR_ARG, who);
+    *n_ids = 0;
+    const uint64_t bpad = ((len + 15) / 16) * 16 + 16;
+    const uint64_t o_bytes = 16, o_oo = 16 + bpad, o_err = o_oo + 16, o_ids = o_err + 16;
+    const uint64_t total = o_ids + dcap * 4;
+    if (w->cap_pin < total) {
+        (void)hipHostFree(w->pin);
+        w->pin = nullptr;
+        w->cap_pin = 0;
+        const uint64_t c = std::max<uint64_t>(total, 64 * 1024);
+        HIP_TRY(hipHostMalloc(&w->pin, c, hipHostMallocDefault));
+        w->cap_pin = c;
+    }
+    if (w->cap_dev1 < total) {
+        (void)hipFree(w->dev1);  // every earlier call synchronized before returning
+        w->dev1 = nullptr;
+        w->cap_dev1 = 0;
+        const uint64_t c = std::max<uint64_t>(total, 64 * 1024);
+        HIP_TRY(hipMalloc(&w->dev1, c));
+        w->cap_dev1 = c;
+    }
+    uint64_t *po = (uint64_t *)w->pin;
+    po[0] = 0;
+    po[1] = len;
+    if (len) memcpy(w->pin + o_bytes, text, len);
+    memset(w->pin + o_bytes + len, 0, bpad - len);
+    HIP_TRY(hipMemcpyAsync(w->dev1, w->pin, o_oo, hipMemcpyHostToDevice, st));
+    w->host_nbytes = len;
+    w->host_maxlen = len;
+    const int rc = enc(w->dev1 + o_bytes, (const uint64_t *)w->dev1, (uint32_t *)(w->dev1 + o_ids), dcap,
+                       (uint64_t *)(w->dev1 + o_oo));
+    w->host_nbytes = ~0ull;
+    w->host_maxlen = ~0ull;
+    if (rc) return rc;
+    k_err_words<<<1, 1, 0, st>>>(w->ctr, w->tile_misc, (uint32_t *)(w->dev1 + o_err));
+    HIP_TRY(hipGetLastError());
+    // small rows: count, error words and every id slot in one copy; large ones: the count first
+    const bool one = dcap * 4 <= 256 * 1024;
+    HIP_TRY(hipMemcpyAsync(w->pin + o_oo, w->dev1 + o_oo, one ? total - o_oo : 32, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const uint64_t n = ((const uint64_t *)(w->pin + o_oo))[1];
+    const uint32_t *err = (const uint32_t *)(w->pin + o_err);
+    if (err[0]) return fail(AK_ERR_HIP, "internal: a row overflowed its staging slot or the huge tier (engine bug)");
+    if (err[1]) return fail(AK_ERR_HIP, "tile staging slot overflow (a row produced more ids than bytes + 2)");
+    if (n > dcap) return fail(AK_ERR_HIP, "internal: more ids than the encode bound (engine bug)");
+    *n_ids = n;
+    if (n > cap) return fail(AK_ERR_NOMEM, "encode_host: ids buffer too small (*n_ids holds the count)");
+    if (!one && n) {
+        HIP_TRY(hipMemcpyAsync(w->pin + o_ids, w->dev1 + o_ids, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (n) memcpy(ids, w->pin + o_ids, n * 4);
+    return AK_OK;
+}
+
+extern "C" int ak_bpe_encode_host(const ak_bpe *m, ak_ws *w, int flags, const uint8_t *text, uint64_t len, int32_t *ids,
+                                  uint64_t cap, uint64_t *n_ids, void *stream) {
+    if (!m) return fail(AK_ERR_ARG, "ak_bpe_encode_host: null model");
+    return encode_host(w, text, len, ids, cap, n_ids, len + 2 + 16, (hipStream_t)stream, "ak_bpe_encode_host: null argument",
+                       [&](const uint8_t *in, const uint64_t *offs, uint32_t *out, uint64_t c, uint64_t *oo) {
+                           return ak_bpe_encode(m, w, flags, in, offs, 1, out, c, oo, nullptr, stream);
+                       });
+}
+
+extern "C" int ak_spm_encode_host(const ak_spm *m, ak_ws *w, int flags, const uint8_t *text, uint64_t len, int32_t *ids,
+                                  uint64_t cap, uint64_t *n_ids, void *stream) {
+    if (!m) return fail(AK_ERR_ARG, "ak_spm_encode_host: null model");
+    return encode_host(w, text, len, ids, cap, n_ids, 3 * len + 4 + 16, (hipStream_t)stream,
+                       "ak_spm_encode_host: null argument",
+                       [&](const uint8_t *in, const uint64_t *offs, uint32_t *out, uint64_t c, uint64_t *oo) {
+                           return ak_spm_encode(m, w, flags, in, offs, 1, out, c, oo, nullptr, stream);
+                       });
 }
 
 extern "C" uint64_t ak_normalize_cap(uint64_t n, uint64_t total_bytes) { return 3 * total_bytes + 16 + 0 * n; }

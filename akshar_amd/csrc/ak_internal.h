@@ -69,7 +69,20 @@ struct AkWs {
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)
+    // host-staged single calls (ak_*_encode_host): what the host already knows about the launch's
+    // rows, so the launchers skip their read-backs (ws_total_bytes; the huge tier when every row
+    // fits the slow tier), and the staging buffers (pinned host, device)
+    uint64_t host_nbytes = ~0ull;   // total bytes of the rows (~0: unknown, read offs[n] back)
+    uint64_t host_maxlen = ~0ull;   // longest row (~0: unknown)
+    uint8_t *pin = nullptr;         // pinned host staging
+    uint64_t cap_pin = 0;
+    uint8_t *dev1 = nullptr;        // device staging of one call: offsets, bytes, ids, offsets out
+    uint64_t cap_dev1 = 0;
 };
+
+// total bytes of a launch's rows (offs[n]): known to the host for a host-staged call, else one
+// 8-byte read-back
+int ws_total_bytes(AkWs *w, const uint64_t *offs, uint64_t n, hipStream_t st, uint64_t *nbytes);
 
 // built-in kernel timing (include/akshar.h ak_profile_*): HIP events around every launch
 extern bool g_prof_on;
@@ -228,6 +241,9 @@ int huge_check(AkWs *w, hipStream_t st);
 
 template <class Launch>
 inline int run_huge_tier(AkWs *w, const uint64_t *offs, hipStream_t st, Launch launch) {
+    // a host-staged call whose rows all fit the slow tier's regions never reaches the huge tier
+    // (huge_prepare sizes a region of 3 x the longest row + 64 entries for any row)
+    if (w->host_maxlen != ~0ull && 3 * w->host_maxlen + 64 <= SLOW_CAP) return AK_OK;
     Tier t;
     unsigned blocks = 0;
     int rc = huge_prepare(w, offs, st, &t, &blocks);
@@ -246,8 +262,7 @@ inline int launch_rows_staged(AkWs *w, RowArgs a, uint64_t *out_offs, hipStream_
     int rc = ws_reserve(w, a.n);
     if (rc) return rc;
     uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging area
-    HIP_TRY(hipMemcpyAsync(&nbytes, a.offs + a.n, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = ws_total_bytes(w, a.offs, a.n, st, &nbytes))) return rc;
     const uint64_t need = (uint64_t)mul * nbytes + (uint64_t)add * a.n + 64;
     if (OP != OP_NORMALIZE) {
         rc = ws_stage_reserve(w, need, st);

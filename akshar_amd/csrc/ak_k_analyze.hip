@@ -97,10 +97,10 @@ __global__ __launch_bounds__(64) void k_analyze_tier(RowArgs a, AnalyzeArgs x, T
 template <int FLAGS>
 static int launch(AkWs *w, RowArgs a, const AnalyzeOut &o, hipStream_t st) {
     uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging areas
-    HIP_TRY(hipMemcpyAsync(&nbytes, a.offs + a.n, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    int rc = ws_total_bytes(w, a.offs, a.n, st, &nbytes);
+    if (rc) return rc;
     const uint64_t need = (uint64_t)AN_MUL * nbytes + (uint64_t)AN_ADD * a.n + 64;
-    int rc = ws_stage_reserve(w, 2 * need, st);
+    rc = ws_stage_reserve(w, 2 * need, st);
     if (rc) return rc;
     rc = ws_stage8_reserve(w, 2 * need, st);
     if (rc) return rc;

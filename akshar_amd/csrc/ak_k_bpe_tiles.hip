@@ -374,8 +374,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     if (rc) return rc;
     // staging slot of row r starts at offs[r] + 2 r: size offs[n] + 2 n (one 8-byte read-back)
     uint64_t nbytes = 0;
-    HIP_TRY(hipMemcpyAsync(&nbytes, a0.offs + a0.n, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = ws_total_bytes(w, a0.offs, a0.n, st, &nbytes))) return rc;
     // two halves: the tile kernel's unit runs, then the fallback rows' slots
     const uint64_t half = nbytes + 2 * a0.n + 64;
     rc = ws_stage_reserve(w, 2 * half, st);

@@ -183,8 +183,7 @@ int launch_rows_tiles(int ops, AkWs *w, const RowArgs &a0, int matras, const Row
     int rc = ws_reserve(w, a0.n);
     if (rc) return rc;
     uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging areas
-    HIP_TRY(hipMemcpyAsync(&nbytes, a0.offs + a0.n, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = ws_total_bytes(w, a0.offs, a0.n, st, &nbytes))) return rc;
     const uint64_t need8 = RT_NORM_MUL * nbytes + RT_NORM_ADD * a0.n + 64;   // normalized bytes
     const uint64_t need32 = RT_SEG_MUL * nbytes + RT_SEG_ADD * a0.n + 64;    // cluster / run ends, labels
     const bool sg = (ops & RT_SEG) != 0, sw = (ops & RT_SW) != 0, nm = (ops & RT_NORM) != 0;

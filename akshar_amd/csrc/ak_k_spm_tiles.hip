@@ -90,8 +90,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     int rc = ws_reserve(w, a0.n);
     if (rc) return rc;
     uint64_t nbytes = 0;  // one 8-byte read-back sizes the staging area
-    HIP_TRY(hipMemcpyAsync(&nbytes, a0.offs + a0.n, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if ((rc = ws_total_bytes(w, a0.offs, a0.n, st, &nbytes))) return rc;
     // two halves: the tile kernel's unit runs, then the fallback rows' slots
     const uint64_t half = SPM_T_MUL * nbytes + SPM_T_ADD * a0.n + 64;
     rc = ws_stage_reserve(w, 2 * half, st);

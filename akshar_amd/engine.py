@@ -139,6 +139,17 @@ def decode_lists(model, rows, dev=None):
     return [b[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(n)]
 
 
+def _encode_host(fn, name, h, dev, raw, flags, cap):
+    """One host string -> numpy int32 ids through ak_*_encode_host (pinned staging, one copy each
+    way, one synchronize)."""
+    ws = workspace(dev.index)
+    check(_lib.lib().ak_ws_set_tiling(ws, TILE_PATH, tile_rows()), "ak_ws_set_tiling")
+    out = np.empty(max(cap, 1), dtype=np.int32)
+    n = ctypes.c_uint64()
+    check(fn(h, ws, flags, raw, len(raw), out.ctypes.data, cap, ctypes.byref(n), _stream(dev)), name)
+    return out[:n.value]
+
+
 def _run(fn_call, n, cap, make_out, dev, ws, out=None, out_offs=None):
     """Run a capacity-bounded op, re-running once with the exact size if needed. Every row is exact
     at any length (include/akshar.h "Row lengths"); ak_ws_check turns an internal overflow into an
@@ -320,6 +331,11 @@ class BPE:
         HF Tokenizer.decode per row (tokenizer.py:219), on the device."""
         return _decode(_lib.lib().ak_bpe_decode, self.h, ids, id_offs)
 
+    def encode_host(self, raw, flags=3):
+        """One UTF-8 string (bytes) -> numpy int32 ids (ak_bpe_encode_host: the per-call path)."""
+        return _encode_host(_lib.lib().ak_bpe_encode_host, "ak_bpe_encode_host", self.h, self.dev, raw, flags,
+                            len(raw) + 18)
+
     def __del__(self):
         h = getattr(self, "h", None)
         if h and _lib is not None:  # at interpreter exit the module may already be torn down
@@ -362,6 +378,11 @@ class SPM:
                                            m.scores.ctypes.data, m.types.ctypes.data, m.unk_id,
                                            m.byte_ids.ctypes.data, ctypes.byref(h)), "ak_spm_create")
         self.h = h
+
+    def encode_host(self, raw, flags=3):
+        """One UTF-8 string (bytes) -> numpy int32 ids (ak_spm_encode_host: the per-call path)."""
+        return _encode_host(_lib.lib().ak_spm_encode_host, "ak_spm_encode_host", self.h, self.dev, raw, flags,
+                            3 * len(raw) + 20)
 
     def cache_info(self):
         """The word cache (include/akshar.h ak_spm_cache_info): slots, "▁" words found, words

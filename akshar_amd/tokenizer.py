@@ -104,8 +104,9 @@ class aksharTokenizer:
                 gb, go = engine.to_device(buf, offs)
                 ids, oo = self.encode_packed(gb, go, nbytes=len(raw))
                 return [int(x) for x in longrows.stitch_bpe(ids.cpu().numpy(), oo.cpu().numpy())]
-        # SentencePiece: always one row (its lattice carries a float score across the whole row)
-        return self.encode_batch([text])[0]
+        # SentencePiece: always one row (its lattice carries a float score across the whole row).
+        # One string: the host-staged single call (pinned staging, one copy each way, one sync)
+        return self.model.encode_host(text.encode("utf-8", "surrogatepass"), self._flags).tolist()
 
     def decode(self, ids: List[int]) -> str:
         """tokenizer.py:195-219, on the device (ak_bpe_decode / ak_spm_decode)."""
@@ -152,7 +153,7 @@ class aksharTokenizer:
                 if pieces is not None:  # clusters of the exact pieces (longrows.py), concatenated
                     norms = self.preprocess_batch(pieces)
                     return [t for n, e in zip(norms, segment_batch(norms)) for t in _split(n, e)]
-            elif self.model_type == "bpe":
+            else:
                 return self._tokens_for(self.encode(text))
         return self.tokenize_batch([text], return_metadata)[0]
 

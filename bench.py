@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-others", action="store_true", help="skip the config 2/3/5 side measurements")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end host->host rates")
+    ap.add_argument("--no-single", action="store_true", help="skip the per-call latency block")
     return ap.parse_args()
 
 
@@ -237,6 +238,39 @@ def end_to_end(dev, model, host_buf, host_offs, kind):
             "list_mb_s": round(lb / 1e6 / dt_l, 2), "list_tokens_per_s": round(sum(len(r) for r in res) / dt_l, 1),
             "list": "aksharTokenizer.encode_batch(list of %d str) -> list[list[int]] (UTF-8 packing, H2D, encode, D2H, "
                     "Python int lists), %.1f ms" % (n_list, dt_l * 1e3)}
+
+
+# ------------------------------------------------------------------------------------------ per-call latency
+def single_call(dev, calls=1000):
+    """Per-call latency of the drop-in class on one 143-byte line: encode(str)
+    on both models (ak_*_encode_host: pinned staging, one copy each way, one synchronize) and
+    tokenize(str), each `calls` calls after a warmup; the batch-of-one path (encode_batch([str]):
+    device packing, read-backs) beside it. Wall-clock microseconds per call, mean and median."""
+    from akshar_amd import synth
+    from akshar_amd.tokenizer import aksharTokenizer
+    line = next(t for t in synth.lines(synth.KIND_HINGLISH, 20000, seed=SEED + 5) if len(t.encode()) >= 143)
+    raw = line.encode()[:143]
+    while True:  # cut on a char boundary
+        try:
+            line = raw.decode()
+            break
+        except UnicodeDecodeError:
+            raw = raw[:-1]
+    out = {"line_bytes": len(line.encode()), "calls": calls}
+    for kind, mp, mt in (("bpe", "akshar.json", "bpe"), ("spm", "akshar.model", "sentencepiece")):
+        tk = aksharTokenizer(model_path=os.path.join(ROOT, "models", mp), model_type=mt)
+        for name, fn in (("encode", lambda: tk.encode(line)), ("tokenize", lambda: tk.tokenize(line)),
+                         ("encode_batch_of_one", lambda: tk.encode_batch([line])[0])):
+            for _ in range(50):
+                fn()
+            ts = []
+            for _ in range(calls):
+                t = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t)
+            ts = np.asarray(ts) * 1e6
+            out["%s_%s_us" % (kind, name)] = {"mean": round(float(ts.mean()), 1), "median": round(float(np.median(ts)), 1)}
+    return out
 
 
 # ------------------------------------------------------------------------------------------ PMC traffic
@@ -509,7 +543,7 @@ def main():
     if ptc:
         roofline["pretoken_cache"] = ptc
 
-    others = e2e = cpu = c5 = None
+    others = e2e = cpu = c5 = single = None
     if rank == 0 and world == 1 and not cfg5 and not args.no_cfg5:
         log(rank, "cfg5 launch block")
         c5 = cfg5_block(args, local)
@@ -519,6 +553,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         log(rank, "end to end")
         e2e = end_to_end(local, model, buf, offs, kind)
+    if rank == 0 and world == 1 and not args.no_single:
+        log(rank, "per-call latency")
+        single = single_call(local)
     if rank == 0 and world == 1 and not args.no_cpu:
         log(rank, "timed region done (%.1f ms/step); CPU baseline" % ms_step)
         cpu = cpu_baseline(args, buf, offs, kind)
@@ -546,6 +583,8 @@ def main():
             line["shard_byte_imbalance"] = round(byte_imbalance, 5)
         if e2e:
             line["end_to_end"] = e2e
+        if single:
+            line["single_call_us"] = single
         if c5:
             line["cfg5"] = c5
         if others:

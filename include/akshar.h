@@ -193,6 +193,19 @@ int ak_bpe_encode(const ak_bpe *m, ak_ws *ws, int flags, const uint8_t *in, cons
 int ak_spm_encode(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *in, const uint64_t *offs, uint64_t n,
                   uint32_t *ids, uint64_t cap, uint64_t *out_offs, uint8_t *row_status, void *stream);
 
+/* One string from host memory to host ids: aksharTokenizer.encode(text) as a non-Python caller binds
+ * it (tokenizer.py:167-193; the FFI stub in INTEGRATION.md), for per-call latency. text: len UTF-8
+ * bytes (host); ids: cap host int32 slots. The row goes through pinned staging in one
+ * host->device copy, the same kernels as ak_bpe_encode / ak_spm_encode on `stream`, and one
+ * device->host copy of count, error words and ids, with one stream synchronize (no read-backs in
+ * between: the workspace knows the row's length). *n_ids = the id count; if it exceeds cap, nothing
+ * is copied and the call returns AK_ERR_NOMEM (call again with a larger buffer). Synchronous: the
+ * ids are in `ids` on return. */
+int ak_bpe_encode_host(const ak_bpe *m, ak_ws *ws, int flags, const uint8_t *text, uint64_t len, int32_t *ids,
+                       uint64_t cap, uint64_t *n_ids, void *stream);
+int ak_spm_encode_host(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *text, uint64_t len, int32_t *ids,
+                       uint64_t cap, uint64_t *n_ids, void *stream);
+
 /* Built-in kernel timing: when enabled, every batch call records HIP events around each of its
  * kernel launches on the caller's stream; ak_profile_read synchronizes the pending events and
  * returns the accumulated device time and launch count of one kernel class. */

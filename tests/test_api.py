@@ -169,3 +169,39 @@ def test_long_rows_through_the_public_api(golden):
         assert spm.encode(r["text"]) == r["spm"]
         assert bpe.preprocess(r["text"]) == r["norm"]
         assert [len(s) for s in akshar_amd.segment_akshars(r["text"])] == r["ak_raw"]
+
+
+@gpu
+def test_single_call_host_path(golden):
+    """encode(str) / tokenize(str) run ak_*_encode_host (pinned staging, one copy each way, one
+    synchronize): the same ids as the batch path and the reference's answers, for every golden row,
+    with each constructor flag variant, an empty string, and a row long enough for the two-step
+    read-back (count first); a too-small ids buffer reports the count with AK_ERR_NOMEM."""
+    import ctypes
+    import numpy as np
+    from akshar_amd import _lib, engine
+    bpe = aksharTokenizer(model_path=BPE_PATH, model_type="bpe")
+    spm = aksharTokenizer(model_path=SPM_PATH, model_type="sentencepiece")
+    for r in golden:
+        assert spm.encode(r["text"]) == r["spm"]
+        assert bpe.encode(r["text"]) == r["bpe"]
+    for r in golden[:200]:
+        assert spm.tokenize(r["text"]) == r["spm_tok"]
+        assert bpe.tokenize(r["text"]) == r["bpe_tok"]
+    texts = [r["text"] for r in golden[:300]]
+    for nr, ch in ((False, True), (True, False), (False, False)):
+        for mp, mt in ((SPM_PATH, "sentencepiece"), (BPE_PATH, "bpe")):
+            tk = aksharTokenizer(model_path=mp, model_type=mt, normalize_roman=nr, clean_hinglish=ch)
+            assert [tk.encode(t) for t in texts] == tk.encode_batch(texts), (mt, nr, ch)
+    assert spm.encode("") == spm.encode_batch([""])[0] and bpe.encode("") == bpe.encode_batch([""])[0]
+    long = " ".join(r["text"] for r in golden if r["set"] == "corpus") * 8
+    assert len(long.encode()) > 300_000
+    assert spm.encode(long) == spm.encode_batch([long])[0]
+    raw = golden[0]["text"].encode()
+    want = spm.model.encode_host(raw)
+    out = np.zeros(1, np.int32)
+    n = ctypes.c_uint64()
+    ws = engine.workspace(spm.model.dev.index)
+    rc = _lib.lib().ak_spm_encode_host(spm.model.h, ws, 3, raw, len(raw), out.ctypes.data, 0 if len(want) else 1,
+                                       ctypes.byref(n), engine._stream(spm.model.dev))
+    assert n.value == len(want) and rc == (_lib.AK_ERR_NOMEM if len(want) else 0)
