@@ -63,7 +63,7 @@ def _deps(src, seen=None):
 # per-TU code-generation flags. ak_k_bpe_tiles.hip: without machine LICM the tile kernel keeps its
 # per-lane constants and addresses in-loop (rematerialised) and fits the 64 VGPRs of 8 waves/SIMD
 # with no scratch spills (with it: 20 VGPRs spilled to scratch in every tile's prologue). The SPM
-# and row-tile kernels measured faster WITH machine LICM (A/B on MI355X, tools/ab_run.sh: cfg3
+# and row-tile kernels measured faster WITH machine LICM (A/B on MI355X, tools/gpu_iter.sh AB_VARIANTS: cfg3
 # fused analyze 66.8 vs 60.9 GB/s), so only the BPE TU takes the flag.
 TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"]}
 

@@ -1,4 +1,4 @@
-"""Summarise a tools/profile_round.sh output directory into profiles/<tag>_*.
+"""Summarise a tools/measure.sh trace / pmc output directory into profiles/<tag>_*.
 
   python tools/pmc_summary.py gpurun_out/v4/prof r01_v4
 
@@ -92,7 +92,7 @@ def main(src, tag):
     wr = allc["WRITE_SIZE"] * 1024
     rec = {"kernel": "k_bpe_tiles<3>",
            "command": "rocprofv3 --pmc <counters> -- python3 tools/prof_op.py bpe 10000000 1 1 (one cfg4-size launch, "
-                      "10 M synthetic Hinglish rows); separate passes per counter group (tools/profile_round.sh)",
+                      "10 M synthetic Hinglish rows); separate passes per counter group (tools/measure.sh, tools/pmc_op.sh)",
            "rows": 10000000, "counters": allc, **meta,
            "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
            "note": "read = FETCH_SIZE x 1024 x 2 (gfx950 half-count correction for 16-B/lane streaming reads), "
