@@ -98,11 +98,13 @@ def build_hip(force=False, jobs=None):
     return out
 
 
-def build_variant(name, defines=(), tu_flags=None, only=None):
+def build_variant(name, defines=(), tu_flags=None, only=None, csrc=None):
     """Development aid: the library built with extra -D defines / per-TU flags into
     akshar_amd/_variants/<name>.so (selected at run time by AK_LIB_VARIANT=<name>). only: the TU
-    names compiled with the defines; every other TU links the default build's object."""
+    names compiled with the defines; every other TU links the default build's object. csrc: another
+    source directory (an earlier commit's csrc/, for an A/B on one box)."""
     global TU_FLAGS
+    CSRC = csrc or globals()["CSRC"]
     if only:
         build_hip()
     objdir = os.path.join(ROOT, "build", "variants", name)

@@ -457,9 +457,11 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
     uint16_t *dummy = M.w + (sizeof(M.w) / 2 - 64) + lane;
     uint32_t vpos = 0;
     {
-        uint32_t carry_h = H_ROWSTART, rows = 0, carry_cp = 0, carry_mv = 0, carry_cmp = 0;
-        uint32_t carry_pcp = 0;  // the char two back at lane 0 (lane 62 of the step before)
+        uint32_t carry_h = H_ROWSTART, rows = 0;
+        uint32_t carry_cmp = 0;  // bit 1 / bit 0: lane 63 / 62 of the step before wrote a composite
         const uint32_t plast = np ? np - 1 : 0;
+        // the hot words a precomposed nukta letter's successor meets (its nukta's)
+        const uint32_t hn_deva = H[0x093Cu - 0x900u + HOT_LO], hn_beng = H[0x09BCu - 0x900u + HOT_LO];
         for (uint32_t c0 = 0; c0 < np; c0 += 64) {
             const uint32_t c = c0 + lane;
             const bool in = c < np;
@@ -487,71 +489,85 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             // a precomposed nukta letter (H_EXP) is base + nukta: the next char is checked against the
             // nukta, and the letter itself never needs the full NFC (see hot_word)
             const bool xp = chr && (h & H_EXP);
-            uint32_t hp = h;
-            if (w_ballot(xp)) {
-                if (xp) hp = H[nukta_of(h & 0xFFFFu) - 0x900u + HOT_LO];
-            }
+            uint32_t hp = xp ? ((h & 0xFFFFu) < 0x0980u ? hn_deva : hn_beng) : h;
             uint32_t hprev = w_prev(hp, carry_h);  // DPP wave_shr:1, lane 0 takes the carry
             uint32_t mv = chr ? (h & 0xFFFFu) : 0u;
-            // A char that composes with the char right before it (rare: behind a ballot): the pair is
-            // looked up exactly; the tile writes the composite itself (the first char's lane emits the
-            // composite's normalize_text map, the second's nothing) unless the first is itself a
-            // composite of this step's making, or the pair straddles two steps and the composite
-            // would change how many entries the first char emitted: those rows fall back.
-            bool cmp = false, pfb = false;
-            uint32_t cmv = 0, ecp = chr && !bad ? cp : 0u;  // ecp: the char as NFC leaves it (a composite)
-            const bool pcand = chr && !bad && !xp && nfc_pair_cand(h, hprev);
-            if (w_ballot(pcand)) {
-                const uint32_t pcp = w_prev(chr && !bad ? cp : 0u, carry_cp);
-                const uint32_t pmv = w_prev(mv, carry_mv);
-                const uint32_t c = pcand ? compose_pair<NF_UCD>(pcp, cp) : 0u;
-                if (c) {
-                    const uint32_t hc = hot(H, c);
+            // The exact clauses (rare: ONE ballot for all three): a char that composes with the char
+            // right before it (nfc_pair_cand), a second after one mark (nfc_l_cand), a mark moved into
+            // the previous starter's base + mark decomposition (nfc_d_cand).
+            bool pfb = false, lok = false;
+            const bool ok = chr && !bad && !xp;
+            const bool anyc = ok && (nfc_pair_cand(h, hprev) ||
+                                     (!(h & H_STABLE) && (nfc_l_cand(h, hprev) || nfc_d_cand(h, hprev))));
+            uint32_t cmp_hi = 0;
+            if (w_ballot(anyc)) {
+                // lane 0's previous two chars sit in the step before: re-read from LDS (the rows' chars
+                // there are of row `rows - 1`; 0 for a row mark, as for a row start)
+                auto cp_at = [&](uint32_t ci2) -> uint32_t {
+                    const uint32_t e2 = P[ci2];
+                    if (e2 & 0x8000u) return 0u;
+                    const int p2 = (int)(e2 & 0x7FFFu);
+                    const uint32_t x = decode_word(lds_word(M.bytes, p2), p2, (int)M.rowend[rows > 0 ? rows - 1 : 0]);
+                    return x == 0xFFFFFFFFu ? 0u : x;
+                };
+                const uint32_t xcp1 = c0 >= 1 ? cp_at(c0 - 1) : 0u, xcp2 = c0 >= 2 ? cp_at(c0 - 2) : 0u;
+                // A char that composes with the char right before it: the pair is looked up exactly;
+                // the tile writes the composite itself (the first char's lane emits the composite's
+                // normalize_text map, the second's nothing) unless the first is itself a composite of
+                // this step's making, or the pair straddles two steps and the composite would change
+                // how many entries the first char emitted: those rows fall back.
+                uint32_t ecp = ok ? cp : 0u;  // the char as NFC leaves it (a composite)
+                const bool pcand = ok && nfc_pair_cand(h, hprev);
+                const uint32_t pcp0 = w_prev(ecp, xcp1);
+                const uint32_t pmv = w_prev(mv, hot(H, xcp1) & 0xFFFFu);
+                const uint32_t cc = pcand ? compose_pair<NF_UCD>(pcp0, cp) : 0u;
+                bool cmp = false;
+                uint32_t cmv = 0;
+                if (cc) {
+                    const uint32_t hc = hot(H, cc);
                     cmv = hc & 0xFFFFu;
                     cmp = true;
                     hp = hc;  // the next char meets the composite
-                    if (lane == 0 && (carry_cmp || pmv == 0u || cmv == 0u)) pfb = true;  // cross-step, not 1 -> 1
+                    if (lane == 0 && ((carry_cmp & 2u) || pmv == 0u || cmv == 0u)) pfb = true;  // cross-step, not 1 -> 1
                 }
                 const bool pcmp = w_prev((uint32_t)cmp, 0u) != 0u;  // (all lanes: a DPP read)
                 if (pcmp && chr && (h & H_SECOND)) pfb = true;  // may chain onto a composite: the full NFC
                 if (pfb) cmp = false;
-                if (cmp) ecp = c;
+                if (cmp) ecp = cc;
                 hprev = w_prev(hp, carry_h);
-            }
-            // a second after one mark: exact when the char before the mark is a starter with no trailing
-            // mark of its own (m composes with that starter, unblocked, or NFC leaves the three alone);
-            // rare, behind a ballot
-            const bool lcand = chr && !bad && !xp && !(h & H_STABLE) && nfc_l_cand(h, hprev);
-            bool lok = false;
-            if (w_ballot(lcand)) {
-                const uint32_t pcp = w_prev(ecp, carry_cp);
-                const uint32_t ppcp = w_prev(pcp, carry_pcp);
-                const uint32_t pph = hot(H, ppcp);  // (0 at a row start: NUL's word, a starter)
-                const bool pps = (pph >> H_CCC_SHIFT) == 0u && !(pph & H_EXP);
-                lok = lcand && pps && compose_pair<NF_UCD>(ppcp, cp) == 0u;
-            }
-            // a mark reordered into the previous starter's decomposition: exact when that is base + one
-            // mark (the mark and m swap, base + m do not compose, base + its mark recompose: NFC leaves
-            // p m alone); rare, behind a ballot
-            const bool dcand = chr && !bad && !xp && !(h & H_STABLE) && nfc_d_cand(h, hprev);
-            if (w_ballot(dcand)) {
-                const uint32_t pcp = w_prev(ecp, carry_cp);
+                // a second after one mark: exact when the char before the mark is a starter with no
+                // trailing mark of its own (m composes with that starter, unblocked, or NFC leaves the
+                // three alone)
+                const uint32_t pcp = w_prev(ecp, xcp1);
+                const uint32_t ppcp = w_prev(pcp, xcp2);
+                const bool lcand = ok && !(h & H_STABLE) && nfc_l_cand(h, hprev);
+                if (lcand) {
+                    const uint32_t pph = hot(H, ppcp);  // (0 at a row start: NUL's word, a starter)
+                    lok = (pph >> H_CCC_SHIFT) == 0u && !(pph & H_EXP) && compose_pair<NF_UCD>(ppcp, cp) == 0u;
+                }
+                // a mark reordered into the previous starter's decomposition: exact when that is base +
+                // one mark (the mark and m swap, base + m do not compose, base + its mark recompose:
+                // NFC leaves p m alone)
+                const bool dcand = ok && !(h & H_STABLE) && nfc_d_cand(h, hprev);
                 if (dcand) {
                     const uint2 pr = prop_global(pcp);
                     const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
                     lok = len == 2u && compose_pair<NF_UCD>(AK_UT_DECOMP[idx], cp) == 0u;
                 }
+                // a composite written by the step before is not what LDS holds there: no proof
+                if ((lane == 0 && carry_cmp) || (lane == 1 && (carry_cmp & 2u))) lok = false;
+                // the composing pair: this lane emits nothing; the lane before emits the composite (in
+                // the step before: the entry it wrote is patched)
+                const uint32_t cnext = w_next(cmp ? (cmv | 0x10000u) : 0u);  // lane 63: 0 (patched by the next step)
+                if (cmp) mv = 0u;
+                if (cnext) mv = cnext & 0xFFFFu;
+                if (cmp && lane == 0) M.v[vpos - 1] = (uint16_t)cmv;
+                cmp_hi = (uint32_t)(w_ballot(cmp) >> 62);
             }
             const bool trig = chr && (bad || pfb || (!(h & H_STABLE) && !xp && !lok && nfc_trig<false>(h, hprev)));
             if (w_ballot(trig)) {
                 if (trig) M.fb[row] = 1;
             }
-            // the composing pair: this lane emits nothing; the lane before emits the composite (in the
-            // step before: the entry it wrote is patched)
-            const uint32_t cnext = w_next(cmp ? (cmv | 0x10000u) : 0u);  // lane 63: 0 (patched by the next step)
-            if (cmp) mv = 0u;
-            if (cnext) mv = cnext & 0xFFFFu;
-            if (cmp && lane == 0) M.v[vpos - 1] = (uint16_t)cmv;
             const bool two = mark && row > 0;
             const uint32_t cnt = mark ? (two ? 2u : 1u) : (mv ? (xp ? 2u : 1u) : 0u);
             uint32_t tot;
@@ -563,10 +579,7 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             vpos += tot;
             rows += (uint32_t)w_popc(RMK);
             carry_h = w_bcast(hp, 63);
-            carry_pcp = w_bcast(ecp, 62);
-            carry_cp = w_bcast(ecp, 63);
-            carry_mv = w_bcast(mv, 63);
-            carry_cmp = w_bcast((uint32_t)cmp, 63);
+            carry_cmp = cmp_hi;
         }
         if (k > 0) {
             if (lane == 0) M.v[vpos] = V_E;

@@ -434,6 +434,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         nmiss += (uint32_t)w_popc(MM);
     }
     w_sync();
+    pc.mark(TP_C);
     for (uint32_t ib = 0; ib < nmiss; ib += 64) {
         const uint32_t i = ib + (uint32_t)lane;
         const bool act = i < nmiss;

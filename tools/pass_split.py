@@ -1,6 +1,6 @@
 """Development aid: per-pass wave-cycle split of the tile kernels (profiling level 2) for the
 library selected by AK_LIB_VARIANT, on synthetic rows. Prints one JSON line.
-  python tools/pass_split.py [op: spm|bpe] [rows] [kind]"""
+  python tools/pass_split.py [op: spm|bpe|analyze] [rows] [kind]"""
 import json
 import os
 import sys
@@ -18,7 +18,14 @@ buf, offs = synth.generate(kind, rows, seed=1241)
 pad = np.zeros(len(buf) + 32, np.uint8)
 pad[:len(buf)] = buf
 gb, go = engine.to_device(pad, offs.astype(np.int64))
-m = engine.SPM("models/akshar.model") if op == "spm" else engine.BPE("models/akshar.json")
+if op == "analyze":
+    class _A:
+        @staticmethod
+        def encode_batch(b, o):
+            return engine.analyze_batch(b, o)
+    m = _A()
+else:
+    m = engine.SPM("models/akshar.model") if op == "spm" else engine.BPE("models/akshar.json")
 m.encode_batch(gb, go)
 torch.cuda.synchronize()
 engine.profile_enable(True, passes=True)
