@@ -353,10 +353,11 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.unk_score = t.min_score - 10.0f;
     m->dev.abs_score_max = t.abs_score_max;
     m->dev.ws_code = t.ws_code;
-    // the tile kernel's word cache (ak_swc.h; AK_SWC=0 leaves it off: development aid, AK_SWC_BITS=b
-    // forces 2^b slots: tests of collisions and dropped words)
+    // the tile kernel's word cache (ak_swc.h): off unless AK_SWC=1 (measured slower on MI355X: the
+    // lattice runs lane per word in rounds of 64, and a tile's words fit one round, so hits do not
+    // shorten it while every word pays the probe). AK_SWC_BITS=b forces 2^b slots.
     const char *we = getenv("AK_SWC");
-    if (!(we && we[0] == '0')) {
+    if (we && we[0] == '1') {
         const char *wb = getenv("AK_SWC_BITS");
         const int bits = wb ? std::max(0, std::min(24, atoi(wb))) : -1;
         std::vector<uint32_t> tab;

@@ -218,6 +218,10 @@ __device__ __forceinline__ uint32_t nukta_of(uint32_t base) { return base < 0x09
 constexpr uint32_t HOT_LO = 0x180;
 constexpr uint32_t HOT_N = HOT_LO + 0x100;
 __device__ __forceinline__ uint32_t hot_cp(uint32_t i) { return i < HOT_LO ? i : i - HOT_LO + 0x900u; }
+// index of cp's word in the LDS hot table, HOT_N if it has none there
+__device__ __forceinline__ uint32_t hot_index(uint32_t cp) {
+    return cp < HOT_LO ? cp : (cp - 0x900u < 0x100u ? cp - 0x900u + HOT_LO : HOT_N);
+}
 __device__ __forceinline__ uint32_t hot(const uint32_t *H, uint32_t cp) {
     if (cp < HOT_LO) return H[cp];
     if (cp - 0x900u < 0x100u) return H[cp - 0x900u + HOT_LO];
@@ -386,6 +390,100 @@ struct TileRows {
     uint32_t vlen;  // entries of V
 };
 
+// Pass D2's exact NFC clauses (rare: the caller's ONE ballot) for the lanes of one step: a char
+// that composes with the char right before it (nfc_pair_cand), a second after one mark (nfc_l_cand),
+// a mark moved into the previous starter's base + mark decomposition (nfc_d_cand). Out of line
+// (AK_D2_NOINLINE) or inlined; every lane of the wave calls it.
+#ifndef AK_D2_NOINLINE
+#define AK_D2_NOINLINE 0
+#endif
+#if AK_D2_NOINLINE && !defined(AK_HOST_EMU)
+#define AK_D2_INLINE __noinline__
+#else
+#define AK_D2_INLINE __forceinline__
+#endif
+struct D2Exact {
+    uint32_t hp, hprev, mv, cmp_hi;
+    bool pfb, lok;
+};
+template <class MemT>
+__device__ AK_D2_INLINE D2Exact d2_exact(MemT &M, const uint16_t *P, const uint32_t *H, uint32_t c0, uint32_t rows,
+                                         uint32_t vpos, uint32_t carry_h, uint32_t carry_cmp, uint32_t h, uint32_t cp,
+                                         bool ok, bool chr, uint32_t hp, uint32_t hprev, uint32_t mv) {
+    const int lane = w_lane();
+    bool pfb = false, lok = false;
+    // lane 0's previous two chars sit in the step before: re-read from LDS (the rows' chars
+    // there are of row `rows - 1`; 0 for a row mark, as for a row start)
+    auto cp_at = [&](uint32_t ci2) -> uint32_t {
+        const uint32_t e2 = P[ci2];
+        if (e2 & 0x8000u) return 0u;
+        const int p2 = (int)(e2 & 0x7FFFu);
+        const uint32_t x = decode_word(lds_word(M.bytes, p2), p2, (int)M.rowend[rows > 0 ? rows - 1 : 0]);
+        return x == 0xFFFFFFFFu ? 0u : x;
+    };
+    const uint32_t xcp1 = c0 >= 1 ? cp_at(c0 - 1) : 0u, xcp2 = c0 >= 2 ? cp_at(c0 - 2) : 0u;
+    // A char that composes with the char right before it: the pair is looked up exactly;
+    // the tile writes the composite itself (the first char's lane emits the composite's
+    // normalize_text map, the second's nothing) unless the first is itself a composite of
+    // this step's making, or the pair straddles two steps and the composite would change
+    // how many entries the first char emitted: those rows fall back.
+    uint32_t ecp = ok ? cp : 0u;  // the char as NFC leaves it (a composite)
+    const bool pcand = ok && nfc_pair_cand(h, hprev);
+    const uint32_t pcp0 = w_prev(ecp, xcp1);  // (all lanes: a DPP read)
+    const uint32_t cc = pcand ? compose_pair<NF_UCD>(pcp0, cp) : 0u;
+    const uint32_t cci = hot_index(cc);
+    bool cmp = cc != 0u;
+    uint32_t hc = H[cci < HOT_N ? cci : 0u];
+    if (w_ballot(cmp && cci >= HOT_N)) {  // a composite outside the LDS table (Latin Extended)
+        if (cmp && cci >= HOT_N) hc = hot_word(cc);
+    }
+    const uint32_t cmv = hc & 0xFFFFu;
+    if (cmp && lane == 0) {  // the first char is the step before's last: its entry is patched
+        const uint32_t xi = hot_index(xcp1);
+        const uint32_t pmv = H[xi < HOT_N ? xi : 0u] & 0xFFFFu;
+        if ((carry_cmp & 2u) || xi >= HOT_N || pmv == 0u || cmv == 0u) pfb = true;  // not 1 -> 1
+    }
+    const bool pcmp = w_prev((uint32_t)cmp, 0u) != 0u;  // (all lanes: a DPP read)
+    if (pcmp && chr && (h & H_SECOND)) pfb = true;  // may chain onto a composite: the full NFC
+    if (pfb) cmp = false;
+    if (cmp) {
+        ecp = cc;
+        hp = hc;  // the next char meets the composite
+    }
+    hprev = w_prev(hp, carry_h);
+    // A second after one mark: exact when the char before the mark is a starter with no
+    // trailing mark of its own (m composes with that starter, unblocked, or NFC leaves the
+    // three alone). A mark moved into the previous starter's decomposition: exact when that
+    // is base + one mark (the mark and m swap, base + m do not compose, base + its mark
+    // recompose: NFC leaves p m alone). One lookup either way.
+    const uint32_t pcp = w_prev(ecp, xcp1);
+    const uint32_t ppcp = w_prev(pcp, xcp2);
+    const bool lcand = ok && !(h & H_STABLE) && nfc_l_cand(h, hprev);
+    const bool dcand = ok && !(h & H_STABLE) && nfc_d_cand(h, hprev);
+    uint32_t first = 0u;
+    bool cand2 = false;
+    if (lcand) {
+        const uint32_t pi = hot_index(ppcp);
+        const uint32_t pph = H[pi < HOT_N ? pi : 0u];  // (0 at a row start: NUL's word, a starter)
+        cand2 = pi < HOT_N && (pph >> H_CCC_SHIFT) == 0u && !(pph & H_EXP);
+        first = ppcp;
+    } else if (dcand) {
+        const uint2 pr = prop_global(pcp);
+        cand2 = ((pr.y >> 16) & 7u) == 2u;
+        first = cand2 ? AK_UT_DECOMP[pr.y >> 19] : 0u;
+    }
+    lok = cand2 && compose_pair<NF_UCD>(first, cp) == 0u;
+    // a composite written by the step before is not what LDS holds there: no proof
+    if ((lane == 0 && carry_cmp) || (lane == 1 && (carry_cmp & 2u))) lok = false;
+    // the composing pair: this lane emits nothing; the lane before emits the composite
+    const uint32_t cnext = w_next(cmp ? (cmv | 0x10000u) : 0u);  // lane 63: 0 (patched by the next step)
+    if (cmp) mv = 0u;
+    if (cnext) mv = cnext & 0xFFFFu;
+    if (cmp && lane == 0) M.v[vpos - 1] = (uint16_t)cmv;
+    const uint32_t cmp_hi = (uint32_t)(w_ballot(cmp) >> 62);
+    return D2Exact{hp, hprev, mv, cmp_hi, pfb, lok};
+}
+
 // Shared front end of the tile kernels (BPE, SentencePiece):
 //   stage: 16-byte coalesced loads of the tile's bytes into LDS;
 //   D1: per row, 64 bytes per step: the positions of the UTF-8 lead bytes -> P (in M.w);
@@ -497,72 +595,17 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             // the previous starter's base + mark decomposition (nfc_d_cand).
             bool pfb = false, lok = false;
             const bool ok = chr && !bad && !xp;
-            const bool anyc = ok && (nfc_pair_cand(h, hprev) ||
+            const bool anyc = AK_KNOCKOUT != 15 && ok && (nfc_pair_cand(h, hprev) ||
                                      (!(h & H_STABLE) && (nfc_l_cand(h, hprev) || nfc_d_cand(h, hprev))));
             uint32_t cmp_hi = 0;
             if (w_ballot(anyc)) {
-                // lane 0's previous two chars sit in the step before: re-read from LDS (the rows' chars
-                // there are of row `rows - 1`; 0 for a row mark, as for a row start)
-                auto cp_at = [&](uint32_t ci2) -> uint32_t {
-                    const uint32_t e2 = P[ci2];
-                    if (e2 & 0x8000u) return 0u;
-                    const int p2 = (int)(e2 & 0x7FFFu);
-                    const uint32_t x = decode_word(lds_word(M.bytes, p2), p2, (int)M.rowend[rows > 0 ? rows - 1 : 0]);
-                    return x == 0xFFFFFFFFu ? 0u : x;
-                };
-                const uint32_t xcp1 = c0 >= 1 ? cp_at(c0 - 1) : 0u, xcp2 = c0 >= 2 ? cp_at(c0 - 2) : 0u;
-                // A char that composes with the char right before it: the pair is looked up exactly;
-                // the tile writes the composite itself (the first char's lane emits the composite's
-                // normalize_text map, the second's nothing) unless the first is itself a composite of
-                // this step's making, or the pair straddles two steps and the composite would change
-                // how many entries the first char emitted: those rows fall back.
-                uint32_t ecp = ok ? cp : 0u;  // the char as NFC leaves it (a composite)
-                const bool pcand = ok && nfc_pair_cand(h, hprev);
-                const uint32_t pcp0 = w_prev(ecp, xcp1);
-                const uint32_t pmv = w_prev(mv, hot(H, xcp1) & 0xFFFFu);
-                const uint32_t cc = pcand ? compose_pair<NF_UCD>(pcp0, cp) : 0u;
-                bool cmp = false;
-                uint32_t cmv = 0;
-                if (cc) {
-                    const uint32_t hc = hot(H, cc);
-                    cmv = hc & 0xFFFFu;
-                    cmp = true;
-                    hp = hc;  // the next char meets the composite
-                    if (lane == 0 && ((carry_cmp & 2u) || pmv == 0u || cmv == 0u)) pfb = true;  // cross-step, not 1 -> 1
-                }
-                const bool pcmp = w_prev((uint32_t)cmp, 0u) != 0u;  // (all lanes: a DPP read)
-                if (pcmp && chr && (h & H_SECOND)) pfb = true;  // may chain onto a composite: the full NFC
-                if (pfb) cmp = false;
-                if (cmp) ecp = cc;
-                hprev = w_prev(hp, carry_h);
-                // a second after one mark: exact when the char before the mark is a starter with no
-                // trailing mark of its own (m composes with that starter, unblocked, or NFC leaves the
-                // three alone)
-                const uint32_t pcp = w_prev(ecp, xcp1);
-                const uint32_t ppcp = w_prev(pcp, xcp2);
-                const bool lcand = ok && !(h & H_STABLE) && nfc_l_cand(h, hprev);
-                if (lcand) {
-                    const uint32_t pph = hot(H, ppcp);  // (0 at a row start: NUL's word, a starter)
-                    lok = (pph >> H_CCC_SHIFT) == 0u && !(pph & H_EXP) && compose_pair<NF_UCD>(ppcp, cp) == 0u;
-                }
-                // a mark reordered into the previous starter's decomposition: exact when that is base +
-                // one mark (the mark and m swap, base + m do not compose, base + its mark recompose:
-                // NFC leaves p m alone)
-                const bool dcand = ok && !(h & H_STABLE) && nfc_d_cand(h, hprev);
-                if (dcand) {
-                    const uint2 pr = prop_global(pcp);
-                    const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
-                    lok = len == 2u && compose_pair<NF_UCD>(AK_UT_DECOMP[idx], cp) == 0u;
-                }
-                // a composite written by the step before is not what LDS holds there: no proof
-                if ((lane == 0 && carry_cmp) || (lane == 1 && (carry_cmp & 2u))) lok = false;
-                // the composing pair: this lane emits nothing; the lane before emits the composite (in
-                // the step before: the entry it wrote is patched)
-                const uint32_t cnext = w_next(cmp ? (cmv | 0x10000u) : 0u);  // lane 63: 0 (patched by the next step)
-                if (cmp) mv = 0u;
-                if (cnext) mv = cnext & 0xFFFFu;
-                if (cmp && lane == 0) M.v[vpos - 1] = (uint16_t)cmv;
-                cmp_hi = (uint32_t)(w_ballot(cmp) >> 62);
+                const D2Exact r = d2_exact(M, P, H, c0, rows, vpos, carry_h, carry_cmp, h, cp, ok, chr, hp, hprev, mv);
+                hp = r.hp;
+                hprev = r.hprev;
+                mv = r.mv;
+                pfb = r.pfb;
+                lok = r.lok;
+                cmp_hi = r.cmp_hi;
             }
             const bool trig = chr && (bad || pfb || (!(h & H_STABLE) && !xp && !lok && nfc_trig<false>(h, hprev)));
             if (w_ballot(trig)) {
@@ -847,7 +890,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
         // lanes that emit nothing, so the common case issues no exec-mask juggling.
         uint16_t *dummy = (uint16_t *)M.bytes;
         const uint32_t h_sp = H[0x20];
-        uint32_t carry_h = H_ROWSTART, carry_word = 0, carry_kword = 0xFFFFFFFFu, rs = 0, carry_x = 0;
+        uint32_t carry_h = H_ROWSTART, carry_word = 0, carry_kword = 0xFFFFFFFFu, rs = 0;
         int carry_cls = HF_S;
         const uint32_t vlast = vlen ? vlen - 1 : 0;
         for (uint32_t base = 0; base < vlen; base += 64) {
@@ -885,16 +928,17 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
             const int cls_l = w_shfl(cls, src);
             const uint32_t hprev = pk ? h_l : carry_h;
             const int cprev = pk ? cls_l : carry_cls;
-            // HF-NFC quick check -> row fallback (rare: behind a ballot); a second right after a first
-            // falls back only if HF's tables compose the pair
+            // HF-NFC quick check -> row fallback (rare: behind a ballot). Pass D2 composed every
+            // adjacent pair of the source, so a composition second right after a first here met it
+            // through normalize_text's filter (a dropped char between): the row falls back only if
+            // HF's tables compose the pair (the previous kept char is its word's map field: a char of
+            // normalize_text's output maps to itself).
             const uint64_t RM = w_ballot(keep && (x == V_B || x == V_FB));
             const bool hfc = keep && !special && !(h & H_HFST);
             bool trig = hfc && nfc_trig<true>(h, hprev);
             const bool hpc = hfc && nfc_pair_cand(h, hprev);
             if (w_ballot(hpc)) {
-                const uint32_t x_l = w_shfl((uint32_t)x, src);
-                const uint32_t xprev = pk ? x_l : carry_x;
-                if (hpc && compose_pair<NF_HFK>(xprev, x)) trig = true;
+                if (hpc && compose_pair<NF_HFK>(hprev & 0xFFFFu, x)) trig = true;
             }
             if (w_ballot(trig)) {
                 if (trig) M.fb[rs + w_rank_incl(RM) - 1] = 1;
@@ -926,7 +970,6 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
                 const int lk = msb64(KM);
                 carry_h = w_bcast(h, lk);
                 carry_cls = w_bcast(cls, lk);
-                carry_x = w_bcast((uint32_t)x, lk);
             }
             carry_word = w_bcast(word, 63);
             if (K2) carry_kword = w_bcast(word, msb64(K2));

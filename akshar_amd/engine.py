@@ -190,7 +190,8 @@ def normalize_batch(buf, offs, flags=3, row_status=None, path=None):
     _tiling(ws, path)
     nbytes = int(offs[-1].item()) if n else 0
     filtered = flags & AK_ST_FILTER if flags & AK_NORM_STAGES else flags & AK_NORM_CLEAN
-    cap = nbytes + 64 if filtered else int(_lib.lib().ak_normalize_cap(n, nbytes))
+    # filtered text: NFC of the allowlist expands only the precomposed nukta letters (3 -> 6 bytes)
+    cap = 2 * nbytes + 64 if filtered else int(_lib.lib().ak_normalize_cap(n, nbytes))
 
     def call(out, c, oo):
         check(_lib.lib().ak_normalize(ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
@@ -248,7 +249,7 @@ def analyze_batch(buf, offs, flags=3, matras=False, row_status=None, path=None):
     _tiling(ws, path)
     nbytes = int(offs[-1].item()) if n else 0
     L = _lib.lib()
-    caps = [nbytes + 64 if flags & AK_NORM_CLEAN else int(L.ak_normalize_cap(n, nbytes)),
+    caps = [2 * nbytes + 64 if flags & AK_NORM_CLEAN else int(L.ak_normalize_cap(n, nbytes)),
             int(L.ak_segment_cap(n, nbytes)), int(L.ak_segment_cap(n, nbytes))]
     oo = [torch.empty(n + 1, dtype=torch.int64, device=dev) for _ in range(3)]
     for _ in range(2):

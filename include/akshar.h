@@ -127,11 +127,12 @@ int ak_bpe_set_added(ak_bpe *m, uint32_t n, const uint32_t *cps, const uint32_t 
 int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint64_t *piece_offs, const float *scores,
                   const uint8_t *types, int32_t unk_id, const int32_t *byte_ids, ak_spm **out);
 void ak_spm_free(ak_spm *m);
-/* The tile path's word cache, built by ak_spm_create: the base-0 lattice solution (pieces and the
- * smallest winning margin) of every "▁"-initial piece string, solved at load; a hit is accepted
- * under the same rounding-bound test as a solved word. info[0] table slots (0 = no cache: AK_SWC=0
- * in the environment), [1] words found, [2] words stored, [3] words whose solution holds an unknown
- * char or more than 6 pieces (never stored). */
+/* The tile path's word cache, built by ak_spm_create when AK_SWC=1 is in the environment (off by
+ * default: measured slower): the base-0 lattice solution (pieces and the smallest
+ * winning margin) of every "▁"-initial piece string, solved at load; a hit is accepted under the
+ * same rounding-bound test as a solved word. info[0] table slots (0 = no cache), [1] words found,
+ * [2] words stored, [3] words whose solution holds an unknown char or more than 6 pieces (never
+ * stored). */
 int ak_spm_cache_info(const ak_spm *m, uint64_t info[4]);
 
 /* Model files read inside the library (host code, no GPU needed to parse): a caller over the

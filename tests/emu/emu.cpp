@@ -106,11 +106,9 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->piece_bytes.assign(bytes, bytes + offs[n]);
     m->piece_offs.assign(offs, offs + n + 1);
     m->types.assign(types, types + n);
-    // the word cache as ak_spm_create builds it (emu_spm_set_wc rebuilds or drops it)
-    uint32_t mask = 0;
-    akb::build_spm_wcache(m->spm, m->sdev.unk_score, unk_id, n, bytes, offs, types, -1, m->wc, mask, m->wc_stats);
-    m->sdev.wc = m->wc.data();
-    m->sdev.wc_mask = mask;
+    // no word cache, as ak_spm_create by default (emu_spm_set_wc builds one)
+    m->sdev.wc = nullptr;
+    m->sdev.wc_mask = 0;
     return m;
 }
 

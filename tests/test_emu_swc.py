@@ -18,8 +18,8 @@ SWC_MAXN = 16
 @pytest.fixture(scope="module")
 def em(spm_model):
     m = emu.Model(spm=spm_model)
-    yield m
     m.set_wc(-1)
+    yield m
 
 
 def _pieces(spm_model):
@@ -146,6 +146,7 @@ def test_ties_on_cached_words_redo_from_the_carried_base(spm_model):
     m, tied = _tied_model(spm_model)
     assert len(tied) >= 100
     em = emu.Model(spm=m)
+    em.set_wc(-1)
     rng = np.random.default_rng(5)
     texts = [" ".join(rng.choice(tied, size=rng.integers(1, 14))) for _ in range(300)]
     buf, offs = O.pack(texts)
@@ -163,6 +164,7 @@ def test_cached_words_across_the_rebase_bound(spm_model, scale):
     m = copy.copy(spm_model)
     m.scores = (np.asarray(spm_model.scores, dtype=np.float32) * np.float32(scale)).astype(np.float32)
     em = emu.Model(spm=m)
+    em.set_wc(-1)
     buf, offs = O.pack(_texts(m, n=200, seed=11))
     ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=4)
     probes, hits = emu.last_counters()

@@ -477,3 +477,20 @@ def test_device_decode_edge_cases(eng, bpe_model, spm_model):
     bpe = eng.BPE(bpe_model)
     brows = [[], [2, 3], [2, 100, 3, 200, 4], [10 ** 6, 100], [100 + i for i in range(200)]]
     assert eng.decode_lists(bpe, brows) == [decode_ref.bpe_decode(bpe_model, r) for r in brows]
+
+
+@pytest.mark.parametrize("bits", [None, "2"])
+def test_spm_word_cache_on_device(eng, spm_model, monkeypatch, bits):
+    """The opt-in SentencePiece word cache (AK_SWC=1; AK_SWC_BITS=2: a 4-slot table, every probe
+    colliding) gives the ids of the default build on 200 k synthetic rows."""
+    buf, offs = _synth(1, 200_000, 31)
+    gb, go = _to_dev(eng, buf, offs)
+    ref_ids, ref_oo = eng.SPM(spm_model).encode_batch(gb, go)
+    monkeypatch.setenv("AK_SWC", "1")
+    if bits:
+        monkeypatch.setenv("AK_SWC_BITS", bits)
+    m = eng.SPM(spm_model)
+    info = m.cache_info()
+    assert info["slots"] > 0 and info["stored"] > 0
+    ids, oo = m.encode_batch(gb, go)
+    assert torch.equal(oo, ref_oo) and torch.equal(ids, ref_ids)
