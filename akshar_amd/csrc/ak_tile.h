@@ -590,25 +590,27 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             uint32_t hp = xp ? ((h & 0xFFFFu) < 0x0980u ? hn_deva : hn_beng) : h;
             uint32_t hprev = w_prev(hp, carry_h);  // DPP wave_shr:1, lane 0 takes the carry
             uint32_t mv = chr ? (h & 0xFFFFu) : 0u;
-            // The exact clauses (rare: ONE ballot for all three): a char that composes with the char
-            // right before it (nfc_pair_cand), a second after one mark (nfc_l_cand), a mark moved into
-            // the previous starter's base + mark decomposition (nfc_d_cand).
-            bool pfb = false, lok = false;
+            // NFC proof (rare work behind ONE ballot): nfc_trig on the non-stable chars, and the pair
+            // candidates (a second right after a first). Where either holds, or the char is bad, the
+            // exact clauses (d2_exact: in-tile composition, a second after one mark, a mark moved into
+            // a base + mark decomposition) decide, and the rows still unproven are marked for the
+            // fallback kernels.
             const bool ok = chr && !bad && !xp;
-            const bool anyc = AK_KNOCKOUT != 15 && ok && (nfc_pair_cand(h, hprev) ||
-                                     (!(h & H_STABLE) && (nfc_l_cand(h, hprev) || nfc_d_cand(h, hprev))));
+            const bool t0 = ok && !(h & H_STABLE) && nfc_trig<false>(h, hprev);
+            const bool pc = ok && nfc_pair_cand(h, hprev);
             uint32_t cmp_hi = 0;
-            if (w_ballot(anyc)) {
-                const D2Exact r = d2_exact(M, P, H, c0, rows, vpos, carry_h, carry_cmp, h, cp, ok, chr, hp, hprev, mv);
-                hp = r.hp;
-                hprev = r.hprev;
-                mv = r.mv;
-                pfb = r.pfb;
-                lok = r.lok;
-                cmp_hi = r.cmp_hi;
-            }
-            const bool trig = chr && (bad || pfb || (!(h & H_STABLE) && !xp && !lok && nfc_trig<false>(h, hprev)));
-            if (w_ballot(trig)) {
+            if (w_ballot(bad || t0 || pc)) {
+                bool pfb = false, lok = false;
+                if (AK_KNOCKOUT != 15) {
+                    const D2Exact r = d2_exact(M, P, H, c0, rows, vpos, carry_h, carry_cmp, h, cp, ok, chr, hp, hprev, mv);
+                    hp = r.hp;
+                    hprev = r.hprev;
+                    mv = r.mv;
+                    pfb = r.pfb;
+                    lok = r.lok;
+                    cmp_hi = r.cmp_hi;
+                }
+                const bool trig = bad || pfb || (ok && !(h & H_STABLE) && !lok && nfc_trig<false>(h, hprev));
                 if (trig) M.fb[row] = 1;
             }
             const bool two = mark && row > 0;
@@ -935,13 +937,11 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
             // normalize_text's output maps to itself).
             const uint64_t RM = w_ballot(keep && (x == V_B || x == V_FB));
             const bool hfc = keep && !special && !(h & H_HFST);
-            bool trig = hfc && nfc_trig<true>(h, hprev);
+            const bool trig = hfc && nfc_trig<true>(h, hprev);
             const bool hpc = hfc && nfc_pair_cand(h, hprev);
-            if (w_ballot(hpc)) {
-                if (hpc && compose_pair<NF_HFK>(hprev & 0xFFFFu, x)) trig = true;
-            }
-            if (w_ballot(trig)) {
-                if (trig) M.fb[rs + w_rank_incl(RM) - 1] = 1;
+            if (w_ballot(trig || hpc)) {
+                const uint32_t rrow = rs + w_rank_incl(RM) - 1;
+                if (trig || (hpc && compose_pair<NF_HFK>(hprev & 0xFFFFu, x))) M.fb[rrow] = 1;
             }
             // pre-tokenizer + ids
             const bool wordchar = keep && !special && cls != HF_S;
