@@ -177,6 +177,89 @@ __device__ __forceinline__ void spm_relax(SpmWaveMem &M, int ee, float cand, uin
 // that step; the rare branches (a start with no single-char piece, a rebase) sit behind ballots.
 // back[] of (p0, p1] must be BK_NONE on entry. Inactive lanes pass p1 <= p0. Returns the smallest
 // gap between a candidate and the stored leader (the margin).
+#ifndef AK_SPM_FLAT2  // the loop body branch-free (selects, unconditional loads): fewer exec-mask juggling
+#define AK_SPM_FLAT2 1    // scalar instructions per trie step
+#endif
+#if AK_SPM_FLAT2
+__device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, int p0, int p1) {
+    float minm = 3.0e38f;
+    bool act = p0 < p1;
+    int s = p0, k = p0, node = 0, nb = m.root_base, reach = p0;
+    float till = 0.0f;
+    bool hs = false;
+    uint32_t v = M.w[act ? p0 : 0];
+    // from base 0 a word's running score stays within (its chars) x the largest |score|: only a word
+    // that could reach the rebase bound needs the rebase check (wave-uniform, once per call)
+    const bool may_rebase = w_ballot(act && (float)(p1 - p0) * m.abs_score_max >= 0.5f * SPM_REBASE) != 0;
+    while (w_ballot(act)) {
+        const bool coded = act && (v & W_CODED);
+        const int t = coded ? nb + (int)(v & 0x7FFFu) : m.root_base;  // idle lanes read a node in range
+        const int4 e = m.trie[t];
+        const bool ok = coded && e.x == node;
+        const int value = e.z;
+        const bool hv = ok && value >= 0 && ((value >> 24) & 3) != 2;
+        const int ee = k + 1;
+        {  // the piece's candidate as selects: every lane reads and writes a slot (its own, or the dummy)
+            const int es = hv ? ee : S_W;
+            const uint32_t bk = M.back[es];
+            const float bb = M.best[es];
+            const float cand = __int_as_float(e.w) + till;
+            const bool none = bk == BK_NONE;
+            const bool take = none || cand > bb;
+            const float gap = take ? cand - bb : bb - cand;
+            minm = hv && !none ? fminf(minm, gap) : minm;
+            M.best[es] = take ? cand : bb;
+            M.back[es] = take ? (((uint32_t)(value & 0xFFFFFF) << 8) | (uint32_t)(ee - s)) : bk;
+            reach = hv && ee > reach ? ee : reach;
+            hs = hs || (hv && k == s);
+        }
+        node = ok ? t : node;
+        nb = ok ? e.y : nb;
+        k = ok ? ee : k;
+        const uint32_t vn = M.w[k < S_W ? k : S_W - 1];
+        const bool end = act && (!ok || k >= p1 || !(vn & W_CODED));
+        {  // a start with no piece of exactly its first char: an unk node (rare; selects, no branch).
+           // The piece candidate above was not at s + 1 then (that would be such a piece).
+            const bool unk = end && !hs;
+            const int es = unk ? s + 1 : S_W;
+            const uint32_t bk = M.back[es];
+            const float bb = M.best[es];
+            const float cand = m.unk_score + till;
+            const bool none = bk == BK_NONE;
+            const bool take = none || cand > bb;
+            const float gap = take ? cand - bb : bb - cand;
+            minm = unk && !none ? fminf(minm, gap) : minm;
+            M.best[es] = take ? cand : bb;
+            M.back[es] = take ? (((uint32_t)m.unk_id << 8) | 1u) : bk;
+            reach = unk && s + 1 > reach ? s + 1 : reach;
+        }
+        const int sn = s + 1;
+        const bool fin = end && sn >= p1;
+        const bool next = end && !fin;
+        const int sc = next ? sn : p0;
+        const float tn = M.best[sc];
+        const uint32_t vs = M.w[sc];
+        s = next ? sn : s;
+        k = next ? sn : k;
+        node = next ? 0 : node;
+        nb = next ? m.root_base : nb;
+        hs = hs && !next;
+        till = next ? tn : till;
+        v = next ? vs : vn;
+        act = act && !fin;
+        if (may_rebase) {
+            if (w_ballot(next && (till < -SPM_REBASE || till > SPM_REBASE))) {  // rare: sentencepiece's rebase
+                if (next && (till < -SPM_REBASE || till > SPM_REBASE)) {
+                    for (int q = s + 1; q <= reach; ++q)
+                        if (M.back[q] != BK_NONE) M.best[q] -= till;
+                    till = 0.0f;
+                }
+            }
+        }
+    }
+    return minm;
+}
+#else
 __device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, int p0, int p1) {
     float minm = 3.0e38f;
     bool act = p0 < p1;
@@ -254,6 +337,7 @@ __device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, in
     }
     return minm;
 }
+#endif
 
 // backtrack a solved word into forward links nxt[s] = chars of the piece at s; returns its id
 // count (byte fallback: one id per UTF-8 byte of an unk char)
