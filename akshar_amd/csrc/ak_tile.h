@@ -796,12 +796,17 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
         }
     }
     uint32_t d[WREG / 2];
+    // the batch's longest miss bounds the set-up: a pair no lane has is not looked up (each lookup
+    // is a gather instruction, ~70 texture-path cycles whatever its active lanes)
 #pragma unroll
     for (int k = 0; k < WREG / 2; ++k) {
         const int i = 2 * k;
         const uint32_t a0 = p[k] & 0xFFFFu, a1 = p[k] >> 16, a2 = k + 1 < WREG / 2 ? p[k + 1] & 0xFFFFu : 0xFFFFu;
-        // looked up unconditionally (the table slot of any symbol pair is in range), kept below n
-        const uint32_t l0 = merge_lookup_c(m, a0, a1), l1 = i + 2 < WREG ? merge_lookup_c(m, a1, a2) : 0xFFFFu;
+        uint32_t l0 = 0xFFFFu, l1 = 0xFFFFu;
+        // looked up by every lane (the table slot of any symbol pair is in range), kept below n; a
+        // pair position no lane has is skipped (wave-uniform)
+        if (AK_KNOCKOUT == 18 || i == 0 || w_ballot(i + 1 < n)) l0 = merge_lookup_c(m, a0, a1);
+        if (i + 2 < WREG && (AK_KNOCKOUT == 18 || w_ballot(i + 2 < n))) l1 = merge_lookup_c(m, a1, a2);
         const uint32_t lo = i + 1 < n ? l0 & 0xFFFFu : 0xFFFFu;
         const uint32_t hi = (i + 2 < WREG && i + 2 < n) ? l1 & 0xFFFFu : 0xFFFFu;
         d[k] = lo | (hi << 16);
