@@ -76,7 +76,7 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
         size <<= 1;  // a cycle: grow and rebuild (never needed at load <= 0.5 in practice)
         if (size > (1u << 24)) return "cuckoo table build failed";
     }
-    // The tile path's compact table: its own two-choice cuckoo at load <= 1/4 (>= 2^17 slots), so
+    // The tile path's compact table: its own two-choice cuckoo at load <= 1/8 (>= 2^17 slots), so
     // almost every key sits in its first-choice slot and one 4-byte load answers almost every
     // lookup. slot = product >> cshift, and (slot, the product's low cshift bits, which hash)
     // identifies the key exactly (both products are bijections of the key). Entry:
@@ -88,8 +88,11 @@ inline std::string build_bpe(uint32_t n_single, const uint32_t *single_cp, const
     // flag, so an absent pair costs one load unless its h1 slot is flagged. The tile path compares
     // new ids as ranks (monotone, checked at load).
     {
+#ifndef AK_CTAB_SPREAD
+#define AK_CTAB_SPREAD 8u  // slots per merge (at least): the load factor's inverse (8: +1 % over 4, A/B r04zb)
+#endif
         uint32_t csize = 1u << 17;
-        while (csize < 4u * n_merges) csize <<= 1;
+        while (csize < AK_CTAB_SPREAD * n_merges) csize <<= 1;
         for (;;) {
             uint32_t cs = 32;
             for (uint32_t q = csize; q > 1; q >>= 1) --cs;

@@ -636,24 +636,42 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
 }
 
 // The pre-token result cache probe (ak_ptc.h): the stored merge_all id of the pre-token whose n
-// symbols are packed in q (two per dword, 0xFFFF past n), or 0xFFFFFFFF. The whole stored sequence
-// is compared, so a hash collision is a miss.
-__device__ __forceinline__ uint32_t ptc_probe(const BpeDev &m, uint32_t n, const uint32_t q[7]) {
-    const char *cbase = (const char *)m.ptc;
+// symbols are packed in q (two per dword, 0xFFFF past n), or 0xFFFFFFFF; lanes with cand false get
+// 0xFFFFFFFF. The whole stored sequence is compared, so a hash collision is a miss. Every lane calls
+// it: each half-entry is ONE 16-byte load (the texture path costs ~70 cycles per load instruction,
+// whatever its active lanes), issued for the wave only where some lane needs it, and the
+// comparisons are bitwise (no short-circuit branches splitting the loads).
+__device__ __forceinline__ uint4 load_x4(const uint4 *p) {
+#ifdef AK_HOST_EMU
+    return *p;
+#else
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *(const u32x4 *)p;
+    return make_uint4(v.x, v.y, v.z, v.w);
+#endif
+}
+__device__ __forceinline__ uint32_t ptc_probe(const BpeDev &m, bool cand, uint32_t n, const uint32_t q[7]) {
+    const uint4 *tab = (const uint4 *)m.ptc;  // two uint4 per 32-byte entry
     const uint32_t h = akp::ptc_hash(n, q[0], q[1], q[2], q[3], q[4], q[5], q[6]);
-    uint32_t off = akp::ptc_slot1(h, m.ptc_mask) << 5;
-    for (int probe = 0; probe < 2; ++probe) {
-        const uint4 e = *(const uint4 *)(cbase + off);
-        bool ok = ((e.x >> 16) & 15u) == n && e.y == q[0] && e.z == q[1] && e.w == q[2];
-        if (ok && n > 6) {
-            const uint4 f = *(const uint4 *)(cbase + off + 16);
-            ok = f.x == q[3] && f.y == q[4] && f.z == q[5] && f.w == q[6];
-        }
-        if (ok) return e.x & 0xFFFFu;
-        if (!(e.x & akp::PTC_FLAG)) break;
-        off = akp::ptc_slot2(h, m.ptc_mask) << 5;
+    const uint32_t s1 = akp::ptc_slot1(h, m.ptc_mask), s2 = akp::ptc_slot2(h, m.ptc_mask);
+    const uint4 a = load_x4(tab + 2 * s1);  // every lane: the slot is in range
+    bool m1 = cand & (((a.x >> 16) & 15u) == n) & (a.y == q[0]) & (a.z == q[1]) & (a.w == q[2]);
+    if (w_ballot(m1 && n > 6)) {
+        const uint4 b = load_x4(tab + 2 * s1 + 1);
+        m1 = m1 & ((n <= 6) | ((b.x == q[3]) & (b.y == q[4]) & (b.z == q[5]) & (b.w == q[6])));
     }
-    return 0xFFFFFFFFu;
+    uint32_t res = m1 ? (a.x & 0xFFFFu) : 0xFFFFFFFFu;
+    const bool try2 = cand & !m1 & ((a.x & akp::PTC_FLAG) != 0u);
+    if (w_ballot(try2)) {
+        const uint4 c = load_x4(tab + 2 * s2);
+        bool m2 = try2 & (((c.x >> 16) & 15u) == n) & (c.y == q[0]) & (c.z == q[1]) & (c.w == q[2]);
+        if (w_ballot(m2 && n > 6)) {
+            const uint4 d = load_x4(tab + 2 * s2 + 1);
+            m2 = m2 & ((n <= 6) | ((d.x == q[3]) & (d.y == q[4]) & (d.z == q[5]) & (d.w == q[6])));
+        }
+        res = m2 ? (c.x & 0xFFFFu) : res;
+    }
+    return res;
 }
 
 
@@ -1055,7 +1073,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
                     const uint32_t hi = 2 * k + 1 < n ? s[2 * k + 1] : 0xFFFFu;
                     q[k] = lo | (hi << 16);
                 }
-                if (act && n <= akp::PTC_MAXN) res = ptc_probe(m, (uint32_t)n, q);
+                res = ptc_probe(m, act && n <= akp::PTC_MAXN, (uint32_t)n, q);  // (every lane calls it)
             }
             const bool hit = res != 0xFFFFFFFFu;
             if (hit) M.w[st] = (uint16_t)(res | WSTART);
