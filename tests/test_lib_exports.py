@@ -44,3 +44,19 @@ def test_header_tier_constant_matches_the_kernels():
     rv = int(re.search(r"constexpr uint32_t SLOW_CAP = (\d+);", rows).group(1))
     assert hv == rv
     assert "AK_LIMIT_" not in h
+
+
+def test_null_arguments_fail_with_arg_errors_cpu():
+    """The C-ABI entry points a non-Python caller binds reject null handles and buffers with
+    AK_ERR_ARG before touching a device (the per-call path and the cache queries included)."""
+    import ctypes as C
+    from akshar_amd import _lib
+    L = _lib.lib()
+    n = C.c_uint64()
+    out = (C.c_int32 * 4)()
+    assert L.ak_bpe_encode_host(None, None, 3, b"ab", 2, out, 4, C.byref(n), None) == _lib.AK_ERR_ARG
+    assert L.ak_spm_encode_host(None, None, 3, b"ab", 2, out, 4, C.byref(n), None) == _lib.AK_ERR_ARG
+    info = (C.c_uint64 * 4)()
+    assert L.ak_bpe_cache_info(None, info) == _lib.AK_ERR_ARG
+    assert L.ak_spm_cache_info(None, info) == _lib.AK_ERR_ARG
+    assert L.ak_ws_check(None) == _lib.AK_ERR_ARG
