@@ -47,10 +47,6 @@ constexpr uint16_t W_B = 0x7FFE;      // row start / end sentinels (not coded: t
 constexpr uint16_t W_END = 0x7FFF;
 constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
 
-#ifndef AK_SPM_STARTS  // pass V walks every start of the tile with lanes taking the next start when done
-#define AK_SPM_STARTS 0  // (spm_walk_starts), the DP then runs over the found pieces in LDS (word_dp_pool)
-#endif
-constexpr int S_POOL = 376;  // pieces a tile's starts may find (more: the tile solves words as before)
 #ifndef AK_SPM_SELECT_RELAX  // the lattice update as selects into a dummy slot: fewer scalar (exec-mask)
 #define AK_SPM_SELECT_RELAX 1  // instructions, +2.8-3.6 % (A/B on MI355X, 4 M rows)
 #endif
@@ -62,12 +58,7 @@ struct SpmWaveMem {
     float best[S_W + AK_SPM_SELECT_RELAX];     // Viterbi best score per W position (word-local)
     uint32_t back[S_W + AK_SPM_SELECT_RELAX];  // best piece ending here: id << 8 | chars ([S_W]: dummy)
     uint8_t wrow[S_WORDS];                   // row of each word
-#if AK_SPM_STARTS
-    uint2 pool[S_POOL];                      // pass V: pieces found by the start walks {score bits, id << 8 | chars}
-    uint16_t sidx[S_W];                      // per W position: first piece | count << 12 | single-char piece << 15
-#else
     uint8_t wmiss[S_WORDS];                  // words the word cache did not hold (pass V)
-#endif
     uint8_t fb[T_MAXR];
     uint8_t mfail[T_MAXR];                   // row has a lattice node within the rounding bound (pass V2)
     uint16_t rowend[T_MAXR];
@@ -364,151 +355,6 @@ __device__ __forceinline__ uint32_t word_backtrack(SpmWaveMem &M, const SpmDev &
     return cnt;
 }
 
-#if AK_SPM_STARTS
-// Pass V, phase 1: the trie walk of EVERY start of the tile (W positions [0, wlen)), lanes taking the
-// next start as soon as their walk ends, so each trie load serves as many lanes as there are starts
-// left (the pass is bound by the count of load instructions, ~70 texture cycles each, not by lanes).
-// A walk records its pieces (up to 4, in length order) and whether one is a single char; at the
-// walk's end the lane appends them to the tile's pool and indexes them by start (sidx). A walk stops
-// before the next word's "▁" (no piece holds one past its first char) and at an uncoded char or a
-// row sentinel. Returns false when a start has more than 4 pieces or the pool is full: the tile then
-// solves its words with word_dp_flat.
-__device__ __forceinline__ bool spm_walk_starts(SpmWaveMem &M, const SpmDev &m, uint32_t wlen) {
-    const int lane = w_lane();
-    uint32_t next_item = 64, pool_n = 0;
-    uint32_t pos = (uint32_t)lane;
-    bool act = pos < wlen;
-    uint32_t v = M.w[act ? pos : 0];
-    bool walk = act && (v & W_CODED);
-    int k = (int)pos, node = 0, nb = m.root_base;
-    uint32_t c = 0;
-    bool hs = false, ovf = false;
-    uint2 q0 = make_uint2(0, 0), q1 = q0, q2 = q0, q3 = q0;
-    while (w_ballot(act)) {
-        const int t = walk ? nb + (int)(v & 0x7FFFu) : m.root_base;  // idle lanes read a node in range
-        const int4 e = m.trie[t];
-        const bool ok = walk && e.x == node;
-        const bool hv = ok && e.z >= 0 && ((e.z >> 24) & 3) != 2;
-        const int ee = k + 1;
-        const uint2 pe = make_uint2((uint32_t)e.w, ((uint32_t)(e.z & 0xFFFFFF) << 8) | (uint32_t)(ee - (int)pos));
-        q0 = hv && c == 0 ? pe : q0;
-        q1 = hv && c == 1 ? pe : q1;
-        q2 = hv && c == 2 ? pe : q2;
-        q3 = hv && c == 3 ? pe : q3;
-        ovf = ovf || (hv && c >= 4);
-        c += hv ? 1u : 0u;
-        hs = hs || (hv && k == (int)pos);
-        node = ok ? t : node;
-        nb = ok ? e.y : nb;
-        k = ok ? ee : k;
-        const uint32_t vn = M.w[k < S_W ? k : S_W - 1];
-        walk = ok && (vn & W_CODED) && vn != m.ws_code;
-        v = vn;
-        // walks that ended: their pieces to the pool, then the next start
-        const bool done = act && !walk;
-        const uint32_t cc = done ? (c < 4u ? c : 4u) : 0u;
-        uint32_t tot;
-        const uint32_t base = pool_n + w_exscan(cc, &tot);
-        const bool fits = base + cc <= (uint32_t)S_POOL;
-        ovf = ovf || (done && !fits);
-        if (done && fits) {
-            if (cc > 0) M.pool[base] = q0;
-            if (cc > 1) M.pool[base + 1] = q1;
-            if (cc > 2) M.pool[base + 2] = q2;
-            if (cc > 3) M.pool[base + 3] = q3;
-            M.sidx[pos] = (uint16_t)(base | (cc << 12) | (hs ? 0x8000u : 0u));
-        }
-        pool_n += tot;
-        const uint64_t DM = w_ballot(done);
-        const uint32_t mine = next_item + w_rank(DM);
-        next_item += (uint32_t)w_popc(DM);
-        pos = done ? mine : pos;
-        act = done ? mine < wlen : act;
-        const uint32_t vs = M.w[act ? pos : 0];
-        v = done ? vs : v;
-        walk = done ? (act && (vs & W_CODED)) : walk;
-        k = done ? (int)pos : k;
-        node = done ? 0 : node;
-        nb = done ? m.root_base : nb;
-        c = done ? 0u : c;
-        hs = hs && !done;
-    }
-    w_sync();
-    return !w_ballot(ovf);
-}
-
-// Pass V, phase 2 for one word (W positions [p0, p1)): the unigram lattice from base 0 over the
-// pieces phase 1 found, in the order word_dp_flat meets them (starts ascending, each start's pieces
-// by length, then its unk node if it has no single-char piece), so the same float adds, decisions
-// and margin, and the same rebase. LDS only: one piece per iteration. back[] of (p0, p1] must be
-// BK_NONE on entry.
-__device__ __forceinline__ float word_dp_pool(SpmWaveMem &M, const SpmDev &m, int p0, int p1) {
-    float minm = 3.0e38f;
-    bool act = p0 < p1;
-    int s = p0, reach = p0;
-    float till = 0.0f;
-    uint32_t si = M.sidx[act ? p0 : 0];
-    uint32_t i = 0;
-    const bool may_rebase = w_ballot(act && (float)(p1 - p0) * m.abs_score_max >= 0.5f * SPM_REBASE) != 0;
-    const uint32_t bk_unk = ((uint32_t)m.unk_id << 8) | 1u;
-    while (w_ballot(act)) {
-        const uint32_t cnt = (si >> 12) & 7u;
-        const bool hasp = act && i < cnt;
-        const uint2 pe = M.pool[hasp ? (si & 0xFFFu) + i : 0];
-        {
-            const int ee = s + (int)(pe.y & 0xFFu);
-            const int es = hasp ? ee : S_W;
-            const uint32_t bk = M.back[es];
-            const float bb = M.best[es];
-            const float cand = __uint_as_float(pe.x) + till;
-            const bool none = bk == BK_NONE;
-            const bool take = none || cand > bb;
-            const float gap = take ? cand - bb : bb - cand;
-            minm = hasp && !none ? fminf(minm, gap) : minm;
-            M.best[es] = take ? cand : bb;
-            M.back[es] = take ? pe.y : bk;
-            reach = hasp && ee > reach ? ee : reach;
-        }
-        const bool ends = act && i + 1 >= cnt;  // this start's last piece (or none): then its unk node
-        {
-            const bool unk = ends && !(si & 0x8000u);
-            const int es = unk ? s + 1 : S_W;
-            const uint32_t bk = M.back[es];
-            const float bb = M.best[es];
-            const float cand = m.unk_score + till;
-            const bool none = bk == BK_NONE;
-            const bool take = none || cand > bb;
-            const float gap = take ? cand - bb : bb - cand;
-            minm = unk && !none ? fminf(minm, gap) : minm;
-            M.best[es] = take ? cand : bb;
-            M.back[es] = take ? bk_unk : bk;
-            reach = unk && s + 1 > reach ? s + 1 : reach;
-        }
-        const int sn = s + 1;
-        const bool fin = ends && sn >= p1;
-        const bool next = ends && !fin;
-        const int sc = next ? sn : S_W;
-        const float tn = M.best[sc];
-        const uint32_t sin_ = M.sidx[next ? sn : 0];
-        s = next ? sn : s;
-        till = next ? tn : till;
-        si = next ? sin_ : si;
-        i = ends ? 0u : i + 1u;
-        act = act && !fin;
-        if (may_rebase) {
-            if (w_ballot(next && (till < -SPM_REBASE || till > SPM_REBASE))) {  // rare: sentencepiece's rebase
-                if (next && (till < -SPM_REBASE || till > SPM_REBASE)) {
-                    for (int q = s + 1; q <= reach; ++q)
-                        if (M.back[q] != BK_NONE) M.best[q] -= till;
-                    till = 0.0f;
-                }
-            }
-        }
-    }
-    return minm;
-}
-#endif
-
 // The word cache probe (ak_swc.h) for the n W codes packed in q (two per dword, 0 past n): the
 // entry's dwords 0-3 (head, margin, pieces 0-1) in hd and its address, or null. The whole stored
 // code sequence is compared, so a hash collision is a miss.
@@ -621,25 +467,6 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
     for (uint32_t i = (uint32_t)lane; i < wlen; i += 64) M.back[i] = BK_NONE;  // word_dp_flat's entry state
     w_sync();
-#if AK_SPM_STARTS
-    const bool pooled = spm_walk_starts(M, m, wlen);
-    pc.count(TC_PROBES, 1);                // tiles
-    pc.count(TC_HITS, pooled ? 1 : 0);     // tiles whose starts fit the pool
-    pc.mark(TP_C);
-    for (uint32_t jb = 0; jb < nw; jb += 64) {
-        const uint32_t j = jb + (uint32_t)lane;
-        const bool act = j < nw;
-        const int row = act ? (int)wrow[j] : 0;
-        const int p0 = act ? (int)starts[j] : 0;
-        const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
-        const float minm = pooled ? word_dp_pool(M, m, p0, p1) : word_dp_flat(M, m, p0, p1);
-        if (act) {
-            if (!spm_margin_ok(M, m, row, p0, p1, minm)) M.mfail[row] = 1;
-            wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
-        }
-    }
-    w_sync();
-#else
     uint32_t nmiss = 0;
     for (uint32_t jb = 0; jb < nw; jb += 64) {
         const uint32_t j = jb + (uint32_t)lane;
@@ -711,7 +538,6 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         }
     }
     w_sync();
-#endif
     // ---------------- pass V2 (rare): lane per row with a close call, its words in order from the
     // carried float base, exactly as sentencepiece's whole-row lattice (ak_dev.h SpmSink)
     {
