@@ -392,10 +392,14 @@ struct TileRows {
 
 // Pass D2's exact NFC clauses (rare: the caller's ONE ballot) for the lanes of one step: a char
 // that composes with the char right before it (nfc_pair_cand), a second after one mark (nfc_l_cand),
-// a mark moved into the previous starter's base + mark decomposition (nfc_d_cand). Out of line
+// a mark moved into the previous starter's base + mark decomposition (nfc_d_cand), two marks out
+// of canonical order after a starter (AK_D2_SWAP). Out of line
 // (AK_D2_NOINLINE) or inlined; every lane of the wave calls it.
 #ifndef AK_D2_NOINLINE
 #define AK_D2_NOINLINE 0
+#endif
+#ifndef AK_D2_SWAP  // the two-mark reorder clause
+#define AK_D2_SWAP 1
 #endif
 #if AK_D2_NOINLINE && !defined(AK_HOST_EMU)
 #define AK_D2_INLINE __noinline__
@@ -475,6 +479,32 @@ __device__ AK_D2_INLINE D2Exact d2_exact(MemT &M, const uint16_t *P, const uint3
     lok = cand2 && compose_pair<NF_UCD>(first, cp) == 0u;
     // a composite written by the step before is not what LDS holds there: no proof
     if ((lane == 0 && carry_cmp) || (lane == 1 && (carry_cmp & 2u))) lok = false;
+    // A mark that sorts before the single mark p right before it (0 < ccc(m) < ccc(p)): NFC swaps
+    // the two. Exact when the char before p is a starter (or the row start) that composes with
+    // neither mark, the char after m is a starter or a mark not below p, and all of it lies in
+    // this step (m on lanes 1..62): the two lanes then emit each other's normalize_text map.
+#if AK_D2_SWAP
+    const uint32_t hpp = w_prev(hprev, H_ROWSTART);                   // the char before p (all lanes: DPP)
+    const uint32_t hnx = w_next(h, H_ROWSTART);                       // the char after m
+    const bool ncmp = w_next((uint32_t)cmp, 1u) != 0u;               // ... composes into m: no swap
+    const bool pok = w_prev((uint32_t)ok, 0u) != 0u;                 // p decoded, not a nukta letter
+    const uint32_t cm = h >> H_CCC_SHIFT, cpv = hprev >> H_CCC_SHIFT;
+    const uint32_t cnx = (hnx & (H_STABLE | H_EXP)) ? 0u : (hnx >> H_CCC_SHIFT);
+    bool scand = ok && pok && !cmp && !pfb && !lok && lane >= 1 && lane <= 62 && !(h & (H_STABLE | H_DECOMP)) &&
+                 hprev != H_ROWSTART && !(hprev & (H_STABLE | H_DECOMP)) && cm != 0u && cm < cpv &&
+                 (hpp == H_ROWSTART || (hpp >> H_CCC_SHIFT) == 0u) && (cnx == 0u || cnx >= cpv) && !ncmp &&
+                 !(lane == 1 && (carry_cmp & 2u));
+    if (w_ballot(scand && (h & H_SECOND))) {  // the starter may compose with m once m sorts next to it
+        if (scand && (h & H_SECOND) && compose_pair<NF_UCD>(ppcp, cp) != 0u) scand = false;
+    }
+    const uint32_t mvn = w_next(mv), mvp = w_prev(mv, 0u);            // (all lanes: DPP)
+    const bool sfirst = w_next((uint32_t)scand) != 0u;
+    if (scand) {
+        mv = mvp;
+        lok = true;
+    }
+    if (sfirst) mv = mvn;
+#endif
     // the composing pair: this lane emits nothing; the lane before emits the composite
     const uint32_t cnext = w_next(cmp ? (cmv | 0x10000u) : 0u);  // lane 63: 0 (patched by the next step)
     if (cmp) mv = 0u;

@@ -129,8 +129,13 @@ NFC_CHANGES = ["a\u0316\u0301",      # second after one mark, composes with the 
                "\u0130\u093c\u0328",  # ... behind a mark of lower ccc
                "\u01d6\u0323",        # base + two marks: the conservative clause
                "e\u0302\u0301",       # a chain of compositions
-               "\u0950\u093c\u0334"]  # a reorder
-NFC_IN_TILE = ["\u0928\u093c", "\u09c7\u09be", "A\u030a", "ka\u0301"]  # a composing pair: in-tile
+               "\u0928\u0301\u093c",  # two marks swap, then the starter composes with the first
+               "k\u0301\u0952\u093c",  # three marks out of order
+               "k\u0301\u093c\u0334",  # two marks swap, the next mark sorts before both
+               "q\u0301\u093c\u0302"]  # ... then a second after them (the conservative clause)
+NFC_IN_TILE = ["\u0928\u093c", "\u09c7\u09be", "A\u030a", "ka\u0301",  # a composing pair
+               "\u0950\u093c\u0334", "q\u0301\u093c", "\u09a4\u0301\u09bc x",  # two marks swap
+               "\u0301\u093c", "\u0915\u0951\u093c\u0915", "q\u0301\u093c\u0951 \u0951\u093c"]
 
 
 def test_nfc_clauses_are_exact(em, bpe_model):
@@ -139,7 +144,8 @@ def test_nfc_clauses_are_exact(em, bpe_model):
     a composition second after one mark (composes with the starter two back or not), a mark that NFC
     moves into the previous starter's base + mark decomposition (U+0130 = I + U+0307), a starter
     second after a decomposable starter, a second after an in-tile composite (falls back: it may chain);
-    a composing pair is composed in the tile. The ids equal the oracle's either way."""
+    a composing pair is composed in the tile, and two marks out of canonical order after a starter
+    are swapped in the tile. The ids equal the oracle's either way."""
     import unicodedata
     assert all(unicodedata.normalize("NFC", t) == t for t in NFC_SAME)
     assert all(unicodedata.normalize("NFC", t) != t for t in NFC_CHANGES + NFC_IN_TILE)
@@ -149,3 +155,15 @@ def test_nfc_clauses_are_exact(em, bpe_model):
         assert emu.last_fallback_rows() == fb
         ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
         assert rows_ints(ids, oo) == rows_ints(ref, ro)
+
+
+def test_nfc_swap_at_step_edges(em, bpe_model):
+    """Two marks out of order placed across every lane position of a 64-char step (the tile swaps
+    them only inside one step; at the edges the row falls back): the ids equal the oracle's."""
+    texts = ["x" * k + "\u0915\u0301\u093c" + "y" * (k % 5) for k in range(56, 72)]
+    texts += ["\u0915" * k + "\u0951\u093c\u0915\u0301\u093c" for k in range(58, 68)]
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=4)
+    assert emu.last_fallback_rows() < len(texts)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)
