@@ -167,3 +167,22 @@ def test_nfc_swap_at_step_edges(em, bpe_model):
     assert emu.last_fallback_rows() < len(texts)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
     assert rows_ints(ids, oo) == rows_ints(ref, ro)
+
+
+def test_nfc_mark_fuzz(em, bpe_model):
+    """Random rows of starters (Latin, Devanagari, Bengali; composition firsts, precomposed nukta
+    letters, decomposable chars) with 12 % combining marks of mixed ccc (composition seconds,
+    nuktas, Vedic accents, viramas, ZWJ): the tile's ids equal the oracle's, whichever rows it keeps."""
+    import random
+    rng = random.Random(7)
+    starters = list("aqkeAIn ") + ["\u0928", "\u0915", "\u0930", "\u09a1", "\u09a4", "\u0130", "\u01d6", "\u0958",
+                                   "\u09dc", "\u0929"]
+    marks = ["\u0301", "\u0302", "\u0308", "\u0316", "\u0323", "\u0327", "\u0328", "\u0334", "\u093c", "\u09bc",
+             "\u0951", "\u0952", "\u094d", "\u09cd", "\u09be", "\u09d7", "\u200d"]
+    texts = ["".join(rng.choice(marks) if rng.random() < 0.12 else rng.choice(starters)
+                     for _ in range(rng.randint(1, 150))) for _ in range(2000)]
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(em, buf, offs, rows=4)
+    assert emu.last_fallback_rows() < len(texts)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)
