@@ -126,7 +126,10 @@ __global__ __launch_bounds__(256) void k_tile_copy(const T *__restrict__ stage, 
 // rows (its unit_fb mask) copies row by row: non-fallback rows from their place in the run
 // (exclusive scan of their counts), fallback rows from their slot mul * offs[r] + add * r in the
 // second staging half.
-constexpr int UC_B = 4;
+#ifndef AK_UC_B
+#define AK_UC_B 4
+#endif
+constexpr int UC_B = AK_UC_B;
 
 template <class T>
 __device__ __forceinline__ void copy_run(const T *__restrict__ src, uint64_t src_cap, T *__restrict__ dst,
