@@ -22,7 +22,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "akshar.h"
@@ -176,8 +178,24 @@ struct ak_spm {
     uint32_t wc_slots = 0;
 };
 
+// The live handles: filled by ak_*_create (ak_*_load goes through them), cleared by ak_*_free, so
+// model_kind never dereferences a pointer that is not a live handle (a freed or foreign pointer is
+// "neither", not a read of freed memory).
+static std::mutex g_live_mu;
+static std::unordered_set<const void *> g_live;
+static void live_add(const void *h) {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    g_live.insert(h);
+}
+static bool live_remove(const void *h) {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    return g_live.erase(h) != 0;
+}
+
 int ak::model_kind(const void *h) {
     if (!h) return 0;
+    std::lock_guard<std::mutex> g(g_live_mu);
+    if (!g_live.count(h)) return 0;
     const uint32_t t = *(const uint32_t *)h;
     return t == MODEL_TAG_BPE ? 1 : t == MODEL_TAG_SPM ? 2 : 0;
 }
@@ -234,6 +252,7 @@ extern "C" int ak_bpe_create(uint32_t n_single, const uint32_t *single_cp, const
         m->dev.ptc_mask = mask;
         m->ptc_slots = mask + 1;
     }
+    live_add(m);
     *out = m;
     return AK_OK;
 }
@@ -258,6 +277,7 @@ extern "C" int ak_spm_cache_info(const ak_spm *m, uint64_t info[4]) {
 
 extern "C" void ak_bpe_free(ak_bpe *m) {
     if (!m) return;
+    (void)live_remove(m);
     m->tag = 0;
     (void)hipFree(m->d_tab);
     (void)hipFree(m->d_ctab);
@@ -399,12 +419,14 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
         const int rc = upload_dec(m->d_dec, m->dec, text, off, kind, bv);
         if (rc) { ak_spm_free(m); return rc; }
     }
+    live_add(m);
     *out = m;
     return AK_OK;
 }
 
 extern "C" void ak_spm_free(ak_spm *m) {
     if (!m) return;
+    (void)live_remove(m);
     m->tag = 0;
     (void)hipFree(m->d_trie);
     (void)hipFree(m->d_cmap_page);
@@ -861,6 +883,7 @@ int ak::ws_total_bytes(AkWs *w, const uint64_t *offs, uint64_t n, hipStream_t st
 __global__ void k_err_words(const uint32_t *ctr, const uint32_t *misc, uint32_t *dst) {
     dst[0] = ctr[CTR_ERR];
     dst[1] = misc ? misc[1] : 0u;
+    dst[2] = ctr[CTR_HUGE];
 }
 
 // ak_*_encode_host: one row through pinned host staging. Device staging layout (16-byte aligned):
@@ -913,6 +936,9 @@ static int encode_host(ak_ws *w, const uint8_t *text, uint64_t len, int32_t *ids
     const uint32_t *err = (const uint32_t *)(w->pin + o_err);
     if (err[0]) return fail(AK_ERR_HIP, "internal: a row overflowed its staging slot or the huge tier (engine bug)");
     if (err[1]) return fail(AK_ERR_HIP, "tile staging slot overflow (a row produced more ids than bytes + 2)");
+    // run_huge_tier skips its read-back when the row fits the slow tier's regions; a row that still
+    // reached the huge list would be left unencoded, so that invariant is checked here (no extra copy)
+    if (err[2] && 3 * len + 64 <= SLOW_CAP) return fail(AK_ERR_HIP, "internal: a short row overflowed the slow tier (engine bug)");
     if (n > dcap) return fail(AK_ERR_HIP, "internal: more ids than the encode bound (engine bug)");
     *n_ids = n;
     if (n > cap) return fail(AK_ERR_NOMEM, "encode_host: ids buffer too small (*n_ids holds the count)");
@@ -927,7 +953,10 @@ static int encode_host(ak_ws *w, const uint8_t *text, uint64_t len, int32_t *ids
 extern "C" int ak_bpe_encode_host(const ak_bpe *m, ak_ws *w, int flags, const uint8_t *text, uint64_t len, int32_t *ids,
                                   uint64_t cap, uint64_t *n_ids, void *stream) {
     if (!m) return fail(AK_ERR_ARG, "ak_bpe_encode_host: null model");
-    return encode_host(w, text, len, ids, cap, n_ids, len + 2 + 16, (hipStream_t)stream, "ak_bpe_encode_host: null argument",
+    // the ids bound of the path that runs: bytes + 2 with clean_hinglish (BPE_MUL), 6 x bytes + 2 under
+    // HF's full NFKC without it (BPE_NFKC_MUL, ak_k_bpe_f01.hip: U+FDFA is 3 bytes -> 18 code points)
+    const uint64_t dcap = ((flags & AK_NORM_CLEAN) ? len : 6 * len) + 2 + 16;
+    return encode_host(w, text, len, ids, cap, n_ids, dcap, (hipStream_t)stream, "ak_bpe_encode_host: null argument",
                        [&](const uint8_t *in, const uint64_t *offs, uint32_t *out, uint64_t c, uint64_t *oo) {
                            return ak_bpe_encode(m, w, flags, in, offs, 1, out, c, oo, nullptr, stream);
                        });

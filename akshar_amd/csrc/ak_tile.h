@@ -727,8 +727,11 @@ __device__ __forceinline__ uint32_t pool_class(uint32_t n) {
     return n <= 7u ? n - 2u : (n <= 9u ? 6u : 7u);
 }
 
-// loads of data this wave stored earlier in the kernel: served by L2 (a plain load could hit a line
-// this CU's L1 cached before the store); the stores have completed (pool_flush waits for them)
+// loads of data this wave stored earlier in the kernel (pool_flush). Correct because the writer and
+// the reader are the same wave on the same CU: its stores have completed (pool_flush waits with
+// s_waitcnt vmcnt(0)) and the CU's vector L1 is write-through, so it holds no older copy of those
+// lines. The nontemporal bit is only a cache-policy hint (the line is not kept); it does not bypass
+// L1. A read of another CU's stores would need an agent-scope (sc1) load or an acquire.
 __device__ __forceinline__ uint4 load_l2(const uint4 *p) {
 #ifdef AK_HOST_EMU
     return *p;

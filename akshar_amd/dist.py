@@ -3,8 +3,8 @@
 Every `encode(line)` of the reference is independent (tokenizer.py:167-193), so a batch shards
 by document: each rank encodes a contiguous, byte-balanced range of rows with no data-path
 collective. When the caller wants the whole batch's id streams on every rank, `gather_ids`
-reassembles them with one all-gather of the per-rank sizes and exact-size broadcasts of each
-rank's slice straight into the final buffers. Works with the "nccl" (RCCL)
+reassembles them with one all-gather of the per-rank sizes and ONE all-gather of the per-rank
+(offsets | ids) records padded to the largest shard. Works with the "nccl" (RCCL)
 backend on device tensors and with "gloo" on CPU tensors (tests).
 """
 import numpy as np
@@ -36,12 +36,15 @@ def gather_ids(ids, out_offs, group=None, out=None):
     ids: int32 [n_ids]; out_offs: int64 [n_rows + 1] with out_offs[0] == 0. Returns
     (all_ids int32, all_offs int64) identical on every rank.
 
-    One all-gather of the per-rank sizes (16 bytes each), then every rank's exact-size slices
-    travel straight into the final buffers: each rank writes its own ids and its offsets rebased by
-    the ids before it into its slice of the result (its only device copy), and broadcasts that
-    slice to the others, which receive into theirs (one broadcast per source rank, all in flight
-    together; no padding, no compaction, no concatenation). `out` = (all_ids, all_offs) preallocated
-    by the caller may be passed; if `ids` already is this rank's slice of out[0], it is not copied.
+    Two collectives per call, whatever the world size:
+      1. all_gather_into_tensor of the per-rank sizes (16 bytes each);
+      2. ONE all_gather_into_tensor of a fixed-size record per rank, padded to the largest shard:
+         [its row offsets rebased by the ids of the ranks before it (int64, as int32 pairs) |
+          its ids (int32)]. Shards are byte-balanced (shard_rows), so the padding is small.
+    The records are then compacted locally into the final buffers (one concatenation per output;
+    `out` = (all_ids, all_offs) preallocated by the caller receives them in place). With RCCL over
+    xGMI the data all-gather is one ring / direct collective on every link at once; per-rank
+    broadcasts would serialise on the communicator's stream.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -62,24 +65,28 @@ def gather_ids(ids, out_offs, group=None, out=None):
                              % (all_ids.numel(), all_offs.numel(), tot_ids, tot_rows + 1))
     all_offs[0] = 0
     ib = [0] * (world + 1)
-    rb = [0] * (world + 1)
     for r in range(world):
         ib[r + 1] = ib[r] + sz[r][0]
-        rb[r + 1] = rb[r] + sz[r][1]
-    mine_ids = all_ids[ib[rank]:ib[rank + 1]]
-    mine_offs = all_offs[rb[rank] + 1:rb[rank + 1] + 1]
-    if sz[rank][0] and mine_ids.data_ptr() != ids.data_ptr():
-        mine_ids.copy_(ids)
-    if sz[rank][1]:
-        torch.add(out_offs[1:], ib[rank], out=mine_offs)
-    work = []
-    for r in range(world):
-        if sz[r][0]:
-            work.append(dist.broadcast(all_ids[ib[r]:ib[r + 1]], src=dist.get_global_rank(group, r) if group else r,
-                                       group=group, async_op=True))
-        if sz[r][1]:
-            work.append(dist.broadcast(all_offs[rb[r] + 1:rb[r + 1] + 1],
-                                       src=dist.get_global_rank(group, r) if group else r, group=group, async_op=True))
-    for w in work:
-        w.wait()
+    max_ids = max(x[0] for x in sz)
+    max_rows = max(x[1] for x in sz)
+    # int32 words per rank record: offsets first, and an even length, so every record's offsets
+    # are 8-byte aligned and read as int64 in place
+    rec = 2 * max_rows + max_ids + (max_ids & 1)
+    if rec == 0:
+        return all_ids[:0], all_offs[:1]
+    mine = torch.empty(rec, dtype=torch.int32, device=dev)
+    n_ids, n_rows = sz[rank]
+    if n_rows:
+        torch.add(out_offs[1:], ib[rank], out=mine[:2 * max_rows].view(torch.int64)[:n_rows])
+    if n_ids:
+        mine[2 * max_rows:2 * max_rows + n_ids].copy_(ids.view(torch.int32))
+    gathered = torch.empty(world * rec, dtype=torch.int32, device=dev)
+    dist.all_gather_into_tensor(gathered, mine, group=group)
+    g = gathered.view(world, rec)
+    g_offs = g[:, :2 * max_rows].view(torch.int64)
+    g_ids = g[:, 2 * max_rows:]
+    if tot_rows:
+        torch.cat([g_offs[r, :sz[r][1]] for r in range(world)], out=all_offs[1:tot_rows + 1])
+    if tot_ids:
+        torch.cat([g_ids[r, :sz[r][0]] for r in range(world)], out=all_ids[:tot_ids].view(torch.int32))
     return all_ids[:tot_ids], all_offs[:tot_rows + 1]

@@ -334,8 +334,11 @@ class BPE:
 
     def encode_host(self, raw, flags=3):
         """One UTF-8 string (bytes) -> numpy int32 ids (ak_bpe_encode_host: the per-call path)."""
+        # the library's ids bound for the flags (ak_bpe_encode_host): bytes + 2 with clean_hinglish,
+        # 6 x bytes + 2 under HF's full NFKC without it
+        mul = 1 if flags & AK_NORM_CLEAN else 6
         return _encode_host(_lib.lib().ak_bpe_encode_host, "ak_bpe_encode_host", self.h, self.dev, raw, flags,
-                            len(raw) + 18)
+                            mul * len(raw) + 18)
 
     def __del__(self):
         h = getattr(self, "h", None)

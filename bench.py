@@ -107,24 +107,42 @@ def cgroup_cpu_quota():
         return None
 
 
+def usable_cpus(avail):
+    """The CPUs this process can really run on at once: its affinity set, capped by the cgroup
+    quota (cpu.max quota / period, rounded up). On the GPU box the affinity set is the whole
+    machine but the quota is 16 CPUs."""
+    q = cgroup_cpu_quota()
+    if q:
+        parts = q.split()
+        try:
+            if parts[0] != "max":
+                return max(1, min(avail, -(-int(parts[0]) // int(parts[1]))))
+        except (ValueError, IndexError, ZeroDivisionError):
+            pass
+    return avail
+
+
 def cpu_baseline(args, buf, offs, kind):
     """The oracle (oracle/akshar_oracle.c) on the same batch, time-bounded legs run inside the C
     library on OpenMP threads (oracle.encode_timed: 2,000-row chunks from a shared cursor,
     per-thread reusable buffers, no Python in the loop): a sweep of 1, 8, 32, 64, 128, 256
-    threads (capped at this process's affinity set, the node's host cores), plus the per-GPU share
-    of the cores (affinity / 8). The single thread is the single-process reference the >= 10x
-    target is quoted against; the all-core value is the best leg of the sweep."""
+    threads (capped at this process's affinity set), plus the per-GPU share of the cores (the
+    usable CPUs / 8). `cores` is what a leg can really use: min(threads, affinity, cgroup quota);
+    `threads` is the OpenMP thread count. The single thread is the single-process reference the
+    >= 10x target is quoted against; the all-core value is the best leg of the sweep."""
     from akshar_amd.models import BPEModel, SPMModel
     from oracle import oracle as O
     model = (O.OracleBPE(BPEModel(os.path.join(ROOT, "models", "akshar.json"))) if kind == "bpe"
              else O.OracleSPM(SPMModel(os.path.join(ROOT, "models", "akshar.model"))))
     cpu_model, nproc, avail = cpu_info()
+    usable = usable_cpus(avail)
     sec = args.cpu_seconds
     n = len(offs) - 1
 
     def leg(threads):
         nb, ni, dt = O.encode_timed(model, buf, offs, threads, sec, chunk_rows=min(2000, n))
-        return {"value": round(nb / 1e6 / dt, 3), "unit": "MB/s", "cores": threads, "kind": "port",
+        return {"value": round(nb / 1e6 / dt, 3), "unit": "MB/s", "cores": min(threads, usable), "threads": threads,
+                "kind": "port",
                 "tokens_per_s": round(ni / dt, 1),
                 "sample": "%.1f MB (%d-row chunks of the timed batch) in %.2f s on %d OpenMP thread(s), "
                           "oracle/akshar_oracle.c %s encode (or_encode_timed)" % (nb / 1e6, min(2000, n), dt, threads, kind)}
@@ -142,15 +160,17 @@ def cpu_baseline(args, buf, offs, kind):
         if t > avail:
             break
         sweep.append(leg(t))
-    if avail not in [x["cores"] for x in sweep]:
+    if avail not in [x["threads"] for x in sweep]:
         sweep.append(leg(avail))
-    share = leg(max(1, avail // 8))
+    share = leg(max(1, usable // 8))
     full = dict(max(sweep, key=lambda x: x["value"]))
     full.update({"cpu_model": cpu_model, "nproc": nproc, "affinity_cpus": avail, "cgroup_cpu_max": cgroup_cpu_quota(),
+                 "usable_cpus": usable,
                  "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "per_gpu_share": share,
                  "single_thread": single,
-                 "sweep": [{"threads": x["cores"], "mb_s": x["value"]} for x in sweep],
-                 "value_is": "the best leg of the thread sweep (all host cores this process may use)"})
+                 "sweep": [{"threads": x["threads"], "cores": x["cores"], "mb_s": x["value"]} for x in sweep],
+                 "value_is": "the best leg of the thread sweep (all host cores this process may use); cores = "
+                             "min(threads, affinity, cgroup quota)"})
     return full
 
 

@@ -144,6 +144,8 @@ int ak_spm_cache_info(const ak_spm *m, uint64_t info[4]);
  *   (replaces SentencePieceProcessor.Load, tokenizer.py:88-90).
  * ak_model_load: model_type "bpe" (-> ak_bpe*) or "sentencepiece" (-> ak_spm*), the reference's
  *   aksharTokenizer(model_path, model_type) choice (tokenizer.py:54-102); ak_model_free likewise.
+ *   The library keeps a set of its live handles: ak_model_free of a pointer that is not one (never
+ *   created, or already freed) sets AK_ERR_ARG's message and touches nothing.
  * ak_model_info (parse only, no device): info[0] vocab / piece count, BPE: [1] single-char
  *   entries, [2] merges, [3] bos, [4] eos, [5] added tokens; SPM: [1] unk id; [7] a 64-bit FNV-1a
  *   of every array the loader would pass to the create calls, in their argument order. */

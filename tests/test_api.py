@@ -206,3 +206,17 @@ def test_single_call_host_path(golden):
     rc = _lib.lib().ak_spm_encode_host(spm.model.h, ws, 3, raw, len(raw), out.ctypes.data, 0 if len(want) else 1,
                                        ctypes.byref(n), engine._stream(spm.model.dev))
     assert n.value == len(want) and rc == (_lib.AK_ERR_NOMEM if len(want) else 0)
+
+
+@gpu
+def test_single_call_bpe_nfkc_expansion():
+    """clean_hinglish=False BPE runs HF's full NFKC, which can give more ids than bytes (U+2177
+    'ⅷ' is 3 bytes and "viii" under NFKC, 4 ids a pair of bytes more than its UTF-8; U+33AF the
+    same; U+FDFA is 18 code points): encode(str) sizes its ids buffer by the flag's bound
+    (ak_bpe_encode_host) and equals encode_batch on such rows."""
+    texts = ["ⅷ" * 40, "㎯" * 33 + "ⅷ", "ﷺ" * 25 + " x", "a ⅷ b ⑽ " * 30, "ⅷ", "⑽⒇" * 40]
+    for nr in (False, True):
+        tk = aksharTokenizer(model_path=BPE_PATH, model_type="bpe", normalize_roman=nr, clean_hinglish=False)
+        got = [tk.encode(t) for t in texts]
+        assert got == tk.encode_batch(texts), nr
+        assert max(len(g) - len(t.encode()) for g, t in zip(got, texts)) > 0  # more ids than bytes

@@ -164,3 +164,6 @@ def test_model_free_by_kind_on_device():
     assert L.ak_model_load(BPE_PATH.encode(), b"bpe", ctypes.byref(h)) == 0
     L.ak_model_free(h, b"sentencepiece")
     assert b"does not match the handle" in L.ak_last_error()
+    # freed: no longer a live handle, so a second free touches nothing (no use after free)
+    L.ak_model_free(h, b"bpe")
+    assert b"not a model handle" in L.ak_last_error()
