@@ -1,6 +1,7 @@
 """In-tree builds of the native pieces (no JIT cache: the .so files travel with the repo).
 
   _synth.so       host C corpus generator (bench/test utility)
+  _pylist*.so     CPython extension: list[str] -> packed UTF-8, packed ids -> list[list[int]]
   _akshar_hip.so  the product: HIP kernels for gfx950 + the C-ABI declared in include/akshar.h
   oracle/_oracle.so  the CPU restatement (test infrastructure; built by oracle/Makefile)
 """
@@ -33,6 +34,16 @@ def build_synth(force=False):
     out = os.path.join(HERE, "_synth.so")
     if force or _stale(out, [src]):
         _run(["gcc", "-O2", "-fopenmp", "-fPIC", "-shared", "-o", out, src])
+    return out
+
+
+def build_pylist(force=False):
+    """The drop-in list API's host plumbing (CPython extension: list[str] packing, id lists)."""
+    import sysconfig
+    src = os.path.join(CSRC, "ak_pylist.c")
+    out = os.path.join(HERE, "_pylist" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if force or _stale(out, [src]):
+        _run(["gcc", "-O2", "-fPIC", "-shared", "-I", sysconfig.get_paths()["include"], "-o", out, src])
     return out
 
 
@@ -139,6 +150,7 @@ def build_oracle(force=False):
 
 def build_all(force=False):
     build_synth(force)
+    build_pylist(force)
     build_oracle(force)
     build_hip(force)
 

@@ -52,8 +52,27 @@ def flags_of(normalize_roman=True, clean_hinglish=True):
     return (AK_NORM_LOWER if normalize_roman else 0) | (AK_NORM_CLEAN if clean_hinglish else 0)
 
 
+try:  # host plumbing of the list API (csrc/ak_pylist.c): two C loops instead of per-row Python
+    from . import _pylist
+except ImportError:  # not built: the same results from the Python loops below
+    _pylist = None
+
+
+def id_lists(ids, offs):
+    """Host int32 ids + int64 row offsets (numpy) -> list[list[int]]."""
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    if _pylist is not None:
+        return _pylist.split(ids, offs)
+    flat, o = ids.tolist(), offs.tolist()
+    return [flat[a:b] for a, b in zip(o, o[1:])]
+
+
 def pack_host(texts):
     """list[str] -> (numpy u8 bytes padded to 16, numpy int64 offsets)."""
+    if _pylist is not None:
+        buf, offs = _pylist.pack(texts)
+        return np.frombuffer(buf, dtype=np.uint8), np.frombuffer(offs, dtype=np.int64)
     enc = [t.encode("utf-8", "surrogatepass") for t in texts]
     offs = np.zeros(len(enc) + 1, dtype=np.int64)
     if enc:

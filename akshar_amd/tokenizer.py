@@ -87,11 +87,12 @@ class aksharTokenizer:
             raise ValueError("need model for IDs")
         if not texts:
             return []
-        buf, offs = engine.pack(texts)
-        ids, oo = self.encode_packed(buf, offs)
-        ids = ids.cpu().numpy()
-        oo = oo.cpu().numpy()
-        return [[int(x) for x in ids[oo[i]:oo[i + 1]]] for i in range(len(texts))]
+        if len(texts) == 1:  # a batch of one: the single-call path (host staging, one sync)
+            return [self.encode(texts[0])]
+        hb, ho = engine.pack_host(texts)
+        buf, offs = engine.to_device(hb, ho)
+        ids, oo = self.encode_packed(buf, offs, nbytes=int(ho[-1]))
+        return engine.id_lists(ids.cpu().numpy(), oo.cpu().numpy())
 
     def encode(self, text: str) -> List[int]:
         if self.model is None:

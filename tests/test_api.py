@@ -193,11 +193,13 @@ def test_single_call_host_path(golden):
         for mp, mt in ((SPM_PATH, "sentencepiece"), (BPE_PATH, "bpe")):
             tk = aksharTokenizer(model_path=mp, model_type=mt, normalize_roman=nr, clean_hinglish=ch)
             assert [tk.encode(t) for t in texts] == tk.encode_batch(texts), (mt, nr, ch)
-    assert spm.encode("") == spm.encode_batch([""])[0] and bpe.encode("") == bpe.encode_batch([""])[0]
+    # (a batch of one takes the single-call path itself: two rows keep the batch path)
+    assert spm.encode("") == spm.encode_batch(["", "x"])[0] and bpe.encode("") == bpe.encode_batch(["", "x"])[0]
+    assert spm.encode_batch([texts[0]]) == [spm.encode(texts[0])] and bpe.encode_batch([texts[0]]) == [bpe.encode(texts[0])]
     long = " ".join(r["text"] for r in golden if r["set"] == "corpus") * 220
     nlong = len(long.encode())
     assert nlong > 300_000, nlong
-    assert spm.encode(long) == spm.encode_batch([long])[0]
+    assert spm.encode(long) == spm.encode_batch([long, ""])[0]
     raw = golden[0]["text"].encode()
     want = spm.model.encode_host(raw)
     out = np.zeros(1, np.int32)
