@@ -127,33 +127,8 @@ def test_hit_rate_on_bench_rows(em, bpe_model):
 
 
 def _tiny_model(path):
-    """A 43-token BPE model where two vocab strings are NOT their own merge_all result:
-    "abc" (merges b c -> bc before a b -> ab, and no a bc merge: [a, bc]) and "cab" ([c, ab])."""
-    import json
-    letters = "abcdefghijklmnopqrstuvwxyz"
-    specials = ["<pad>", "<unk>", "<s>", "</s>", "<mask>"]
-    vocab = {t: i for i, t in enumerate(specials)}
-    for ch in letters:
-        vocab[ch] = len(vocab)
-    merges = [("b", "c"), ("a", "b"), ("ab", "c"), ("d", "e"), ("de", "f"), ("x", "y"), ("y", "z"), ("xy", "z"),
-              ("c", "a"), ("bc", "a"), ("ab", "ab"), ("ca", "b")]
-    for a, b in merges:
-        vocab.setdefault(a + b, len(vocab))
-    tmpl = [{"SpecialToken": {"id": "<s>", "type_id": 0}}, {"Sequence": {"id": "A", "type_id": 0}},
-            {"SpecialToken": {"id": "</s>", "type_id": 0}}]
-    j = {"version": "1.0", "truncation": None, "padding": None,
-         "added_tokens": [{"id": i, "content": t, "single_word": False, "lstrip": False, "rstrip": False,
-                           "normalized": False, "special": True} for i, t in enumerate(specials)],
-         "normalizer": {"type": "NFKC"}, "pre_tokenizer": {"type": "Whitespace"},
-         "post_processor": {"type": "TemplateProcessing", "single": tmpl, "pair": tmpl + tmpl,
-                            "special_tokens": {"<s>": {"id": "<s>", "ids": [2], "tokens": ["<s>"]},
-                                               "</s>": {"id": "</s>", "ids": [3], "tokens": ["</s>"]}}},
-         "decoder": None,
-         "model": {"type": "BPE", "dropout": None, "unk_token": None, "continuing_subword_prefix": None,
-                   "end_of_word_suffix": None, "fuse_unk": False, "byte_fallback": False, "ignore_merges": False,
-                   "vocab": vocab, "merges": [[a, b] for a, b in merges]}}
-    path.write_text(json.dumps(j))
-    return str(path)
+    from tests.util import tiny_bpe_model
+    return tiny_bpe_model(path)
 
 
 @pytest.mark.parametrize("bits", [-1, 0, 2])

@@ -494,3 +494,79 @@ def test_spm_word_cache_on_device(eng, spm_model, monkeypatch, bits):
     assert info["slots"] > 0 and info["stored"] > 0
     ids, oo = m.encode_batch(gb, go)
     assert torch.equal(oo, ref_oo) and torch.equal(ids, ref_ids)
+
+
+@pytest.mark.parametrize("bits", ["2", "0"])
+def test_bpe_pretoken_cache_collisions_on_device(eng, bpe_model, monkeypatch, bits):
+    """The BPE pre-token cache forced into a 4-slot (AK_PTC_BITS=2: every probe collides, almost
+    every key dropped) or a 1-slot table: the headline kernel's ids equal the default build's on
+    200 k synthetic rows and the oracle's on 20 k of them."""
+    buf, offs = _synth(1, 200_000, 37)
+    gb, go = _to_dev(eng, buf, offs)
+    ref_ids, ref_oo = eng.BPE(bpe_model).encode_batch(gb, go)
+    monkeypatch.setenv("AK_PTC_BITS", bits)
+    m = eng.BPE(bpe_model)
+    info = m.cache_info()
+    assert info["slots"] == 1 << int(bits) and info["stored"] <= info["slots"]
+    ids, oo = m.encode_batch(gb, go)
+    assert torch.equal(oo, ref_oo) and torch.equal(ids, ref_ids)
+    n = 20_000
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf[:offs[n]], offs[:n + 1])
+    o = _cpu(oo)[:n + 1]
+    assert np.array_equal(o.astype(np.uint64), ro) and np.array_equal(_cpu(ids)[:o[-1]].astype(np.uint32), ref)
+
+
+@pytest.mark.parametrize("bits", [None, "0", "2"])
+def test_bpe_vocab_string_not_its_merge_result_on_device(eng, tmp_path, monkeypatch, bits):
+    """A model where the vocab strings "abc" and "cab" are NOT their own merge_all result ([a, bc]
+    and [c, ab]: tests/util.py tiny_bpe_model) is never answered from the pre-token cache with
+    the vocab id, under the default table and tables of one and four slots (tests/test_emu_ptc.py
+    on the device)."""
+    from akshar_amd.models import BPEModel
+    from tests.util import tiny_bpe_model
+    if bits is not None:
+        monkeypatch.setenv("AK_PTC_BITS", bits)
+    bm = BPEModel(tiny_bpe_model(tmp_path / "tiny.json"))
+    m = eng.BPE(bm)
+    assert m.cache_info()["multi"] == 2
+    words = ["abc", "cab", "bca", "abab", "xyz", "def", "de", "ab", "abcabc", "cabcab", "bcabca", "xyzxyz", "q"]
+    rng = np.random.default_rng(5)
+    texts = ["abc", "cab", "ABC cab!"] + [" ".join(rng.choice(words, size=rng.integers(1, 40))) for _ in range(5000)]
+    ids, oo = m.encode_batch(*eng.pack(texts))
+    ref, ro = O.OracleBPE(bm).encode_batch(*O.pack(texts))
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    v = bm.vocab
+    got = rows_ints(_cpu(ids), _cpu(oo))[:3]
+    assert got == [[2, v["a"], v["bc"], 3], [2, v["c"], v["ab"], 3], [2, v["a"], v["bc"], v["c"], v["ab"], 3]]
+
+
+def test_bpe_merge_pool_ring_bound(eng, bpe_model):
+    """The merge pool's ring at its bound (ak_tile.h POOL_RING >= 63 + T_SCAP): in every 64-row
+    unit one tile leaves 63 misses waiting (below a batch), the next tile adds T_SCAP = 240 more
+    (every multi-symbol pre-token a pair with no merge: never in the cache, two ids after the
+    merge rounds), so 303 entries wait before the drain; a third row holds T_SCAP + 1 such
+    pre-tokens, past what a tile lists, and goes to the fallback kernels. The rest of each unit is
+    synthetic rows; 300 units, so every wave's ring wraps many times. Equal to the oracle."""
+    import numpy as _np
+    v = bpe_model.vocab
+    pairs_merged = {(int(a), int(b)) for a, b, _ in _np.asarray(bpe_model.merges)}
+    L = "abcdefghijklmnopqrstuvwxyz"
+    nomerge = [a + b for a in L for b in L if a != b and a in v and b in v and (v[a], v[b]) not in pairs_merged]
+    assert len(nomerge) > 100
+    rng = np.random.default_rng(11)
+    from akshar_amd import synth
+    filler = synth.lines(1, 300 * 61, seed=41)
+    texts = []
+    for u in range(300):
+        texts.append(" ".join(rng.choice(nomerge, 63)))    # 188 B: its own tile (the next row does not fit)
+        texts.append(" ".join(rng.choice(nomerge, 240)))   # 719 B: T_SCAP misses in one tile
+        texts.append(" ".join(rng.choice(nomerge, 241)))   # 722 B: T_SCAP + 1: the fallback kernels
+        texts.extend(filler[61 * u:61 * (u + 1)])
+    m = eng.BPE(bpe_model)
+    ids, oo = m.encode_batch(*eng.pack(texts))
+    fb = eng.fallback_rows()
+    assert fb[0] >= 300, fb
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(*O.pack(texts))
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    got = _cpu(oo)
+    assert got[1] - got[0] == 128 and got[2] - got[1] == 482 and got[3] - got[2] == 484
