@@ -810,12 +810,20 @@ struct SpmDev {
     uint16_t ws_code;      // tile path W entry of U+2581 (0x8000 | code, or the code point if no piece holds it)
     const uint32_t *wc;    // tile path: the word cache (ak_swc.h; null = off)
     uint32_t wc_mask;
+    uint32_t pool_ok;      // tile path: the word pool may take words (ak_tile_spm.h spm_pool_ok)
 };
 
 // word chars are stored as 0x80000000 | code for chars some piece holds, the plain code point
 // otherwise (the walk stops there; such a char can only become an unk node)
 constexpr uint32_t SPM_CODED = 0x80000000u;
 constexpr float SPM_REBASE = 100000.0f;  // sentencepiece 0.2.2: |best| beyond this is rebased to 0
+constexpr int SPM_POOL_MAXL = 24;        // longest word of the tile path's word pool (ak_tile_spm.h)
+// The word pool solves each word from base 0 with no rebase: allowed when no pooled word can reach
+// the rebase bound (the in-tile lattice's may_rebase test) and every char some piece holds is a piece
+// itself (a pooled word's id count is then at most its chars, plus UTF-8 bytes for chars in no piece)
+inline bool spm_pool_allowed(bool single_all, float abs_score_max) {
+    return single_all && (float)(SPM_POOL_MAXL + 1) * abs_score_max < 0.5f * SPM_REBASE;
+}
 
 __device__ __forceinline__ uint32_t spm_code(const SpmDev &m, uint32_t cp) {
     const uint32_t pg = m.cmap_page[cp >> 7];

@@ -373,6 +373,9 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     m->dev.unk_score = t.min_score - 10.0f;
     m->dev.abs_score_max = t.abs_score_max;
     m->dev.ws_code = t.ws_code;
+    // the tile path's word pool (ak_tile_spm.h): AK_SPM_POOL=0 leaves it off (development aid, A/B)
+    const char *pe = getenv("AK_SPM_POOL");
+    m->dev.pool_ok = spm_pool_allowed(t.single_all, t.abs_score_max) && !(pe && pe[0] == '0') ? 1u : 0u;
     // the tile kernel's word cache (ak_swc.h): off unless AK_SWC=1 (measured slower on MI355X: the
     // lattice runs lane per word in rounds of 64, and a tile's words fit one round, so hits do not
     // shorten it while every word pays the probe). AK_SWC_BITS=b forces 2^b slots.
@@ -538,6 +541,7 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->unit_fb);
     (void)hipFree(w->unit_len);
     (void)hipFree(w->bpool);
+    (void)hipFree(w->row_span);
     (void)hipFree(w->counts);
     (void)hipFree(w->slow_list);
     (void)hipFree(w->huge_list);

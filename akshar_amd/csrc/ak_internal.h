@@ -62,10 +62,12 @@ struct AkWs {
     uint64_t cap_fb2 = 0;
     uint64_t *unit_fb = nullptr;    // tile BPE: per 64-row unit, the mask of its fallback rows
     uint64_t cap_unit_fb = 0;
-    uint32_t *unit_len = nullptr;   // tile BPE: per unit, its staging run's length (ids + dead entries)
+    uint32_t *unit_len = nullptr;   // tile BPE / SentencePiece: per unit, its staging run's length (ids + dead entries)
     uint64_t cap_unit_len = 0;
-    uint4 *bpool = nullptr;         // tile BPE: the waves' merge pools (ak_tile.h pool_flush)
-    uint64_t cap_bpool = 0;         // ... entries
+    uint4 *bpool = nullptr;         // tile BPE / SentencePiece: the waves' merge / word pools (ak_tile.h
+    uint64_t cap_bpool = 0;         // pool_flush, ak_tile_spm.h spm_pool_flush), entries
+    uint32_t *row_span = nullptr;   // tile SentencePiece: per row, its entries in the unit run
+    uint64_t cap_row_span = 0;
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)

@@ -7,7 +7,8 @@
 //                    lattice with the carried base), into the same slots; rows past its buffers go
 //   k_rows_tier      ... to the slow and huge tiers (ak_internal.h)
 //   scan_counts      per-row counts -> u64 row offsets (out_offs)
-//   k_tile_copy      staged ids -> ids[out_offs[r] ...]
+//   k_unit_copy_spm  the unit runs -> ids[out_offs[r] ...], dropping the STAGE_DEAD slots the word
+//                    pool left (ak_tile_spm.h spm_pool_flush); fallback rows from their slots
 #include <stdlib.h>
 
 #include "ak_internal.h"
@@ -80,6 +81,50 @@ __global__ __launch_bounds__(SPM_FB_BLOCK) void k_spm_tile_fb(TileArgs ta) {
     }
 }
 
+// The unit runs -> final positions, dropping STAGE_DEAD (one wave per unit). A unit without fallback
+// rows streams its run (unit_len[u] entries) and compacts each 64-entry step by ballot. A unit with
+// fallback rows copies row by row: row j's entries of the run start at the sum of the spans the rows
+// before it reserved (row_span; 0 for a row the tile sent to the fallback kernels), so a row a pooled
+// word sent there later (its entries are in the run) is skipped the same way; fallback rows come from
+// their slots in the second staging half.
+__global__ __launch_bounds__(256) void k_unit_copy_spm(const uint32_t *__restrict__ stage, const uint32_t *__restrict__ stage_fb,
+                                                       const uint64_t *__restrict__ offs, const uint64_t *__restrict__ out_offs,
+                                                       const uint64_t *__restrict__ unit_fb, const uint32_t *__restrict__ unit_len,
+                                                       const uint32_t *__restrict__ row_span, uint64_t n,
+                                                       uint32_t *__restrict__ out, uint64_t cap, uint64_t half) {
+    const int lane = w_lane();
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t nunits = (n + TILE_UNIT - 1) / TILE_UNIT;
+    for (uint64_t u = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < nunits; u += nwaves) {
+        const uint64_t u0 = u * TILE_UNIT;
+        const int nr = (int)(u0 + TILE_UNIT < n ? TILE_UNIT : n - u0);
+        const uint64_t fbm = unit_fb[u];
+        const uint64_t base = SPM_T_MUL * offs[u0] + SPM_T_ADD * u0;
+        if (fbm == 0) {
+            unit_copy_live(stage, half, base, unit_len[u], out, cap, out_offs[u0], lane);
+            continue;
+        }
+        const uint64_t r = u0 + (uint64_t)lane;
+        const bool in = lane < nr;
+        const uint64_t ro = in ? out_offs[r] : 0ull;
+        const uint64_t c = in ? out_offs[r + 1] - ro : 0ull;
+        const uint32_t span = in ? row_span[r] : 0u;
+        uint32_t tot;
+        const uint64_t sbeg = base + w_exscan(span, &tot);
+        for (int j = 0; j < nr; ++j) {
+            const uint64_t cj = w_bcast(c, j), dj = w_bcast(ro, j);
+            if ((fbm >> j) & 1ull) {
+                const uint64_t rj = u0 + (uint64_t)j;
+                const uint64_t sj = SPM_T_MUL * offs[rj] + SPM_T_ADD * rj;
+                for (uint64_t k = (uint64_t)lane; k < cj; k += 64)
+                    if (dj + k < cap && sj + k < half) out[dj + k] = stage_fb[sj + k];
+            } else {
+                unit_copy_live(stage, half, w_bcast(sbeg, j), w_bcast(span, j), out, cap, dj, lane);
+            }
+        }
+    }
+}
+
 static std::atomic<int> g_spm_blocks_per_cu{0};  // occupancy (same gfx950 part on every device; idempotent store)
 
 int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t st) {
@@ -98,6 +143,22 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     const int R = w->tile_rows;
     const uint64_t ntiles = (a0.n + TILE_UNIT - 1) / TILE_UNIT;  // units of the work queue (ak_tile.h tile_first_unit)
     if ((rc = ws_unit_fb_reserve(w, ntiles))) return rc;
+    if (w->cap_unit_len < ntiles) {
+        (void)hipFree(w->unit_len);
+        w->unit_len = nullptr;
+        w->cap_unit_len = 0;
+        HIP_TRY(hipMalloc(&w->unit_len, ntiles * 4));
+        w->cap_unit_len = ntiles;
+    }
+    if (w->cap_row_span < a0.n) {
+        (void)hipFree(w->row_span);
+        w->row_span = nullptr;
+        w->cap_row_span = 0;
+        HIP_TRY(hipMalloc(&w->row_span, a0.n * 4));
+        w->cap_row_span = a0.n;
+    }
+    // the units' fallback masks are OR-ed into (a pooled word may add a row to a finished unit)
+    HIP_TRY(hipMemsetAsync(w->unit_fb, 0, ntiles * 8, st));
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count, [3] the unit queue
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
@@ -141,6 +202,18 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     int bpc = g_spm_blocks_per_cu.load(std::memory_order_relaxed);
     if (const char *e = getenv("AK_SPM_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));  // development aid
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)num_cus() * (uint64_t)bpc);
+    // the waves' word pools: SP_CAP entries per wave slot of the grid (shared with the BPE merge pools)
+    const uint64_t pool_entries = (uint64_t)grid * wpb * SP_CAP;
+    if (w->cap_bpool < pool_entries) {
+        (void)hipFree(w->bpool);
+        w->bpool = nullptr;
+        w->cap_bpool = 0;
+        HIP_TRY(hipMalloc(&w->bpool, pool_entries * sizeof(uint4)));
+        w->cap_bpool = pool_entries;
+    }
+    ta.pool = w->bpool;
+    ta.unit_len = w->unit_len;
+    ta.row_span = w->row_span;
     AK_PROF(AK_PROF_SPM_TILES, false, st);
     k_spm_tiles<3><<<grid, SPM_TILE_BLOCK, 0, st>>>(ta);
     AK_PROF(AK_PROF_SPM_TILES, true, st);
@@ -166,8 +239,12 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     if (rc) return rc;
     AK_PROF(AK_PROF_SCAN, true, st);
     AK_PROF(AK_PROF_COPY, false, st);
-    rc = copy_units<uint32_t>(w->stage, w->stage + half, half, a0.offs, out_offs, w->unit_fb, a0.n,
-                              (uint32_t *)a0.out, a0.cap, SPM_T_MUL, SPM_T_ADD, st);
+    {
+        const unsigned cgrid = (unsigned)std::min<uint64_t>((ntiles + 3) / 4, (uint64_t)num_cus() * 8);
+        k_unit_copy_spm<<<cgrid, 256, 0, st>>>(w->stage, w->stage + half, a0.offs, out_offs, w->unit_fb, w->unit_len,
+                                               w->row_span, a0.n, (uint32_t *)a0.out, a0.cap, half);
+        HIP_TRY(hipGetLastError());
+    }
     AK_PROF(AK_PROF_COPY, true, st);
     return rc;
 }

@@ -269,6 +269,8 @@ struct SpmTables {
     float min_score = 0;
     float abs_score_max = 0;          // largest |score| one lattice node adds (normal, user defined, unk)
     uint16_t ws_code = 0;             // tile-path W entry of U+2581 (0x8000 | code, or 0x2581 if no piece holds it)
+    bool single_all = false;          // every char some piece holds is itself a (used) piece: such a
+                                      // char never becomes an unk node (the tile word pool's id bound)
 };
 
 constexpr uint32_t SPM_CMAP_PAGES = 0x110000u >> 7;
@@ -420,6 +422,11 @@ inline std::string build_spm(uint32_t n, const uint8_t *piece_bytes, const uint6
     }
     out.n_nodes = (uint32_t)nn;
     out.root_base = base[0];
+    out.single_all = true;
+    for (int c = 1; c <= K; ++c) {
+        const int t = base[0] + c;
+        if (check[t] != 0 || value[t] < 0 || ((value[t] >> 24) & 3) == 2) out.single_all = false;
+    }
     out.min_score = min_score;
     // the tile path's rounding bound (ak_tile_spm.h): normal scores, user-defined bonuses and the
     // unk score (min - 10)

@@ -40,9 +40,6 @@ constexpr int T_MAXR = 16;    // rows per tile (upper bound of the runtime R)
 #ifndef AK_TILE_UNIT
 #define AK_TILE_UNIT 64
 #endif
-#ifndef AK_STAGE_PF  // touch the next tile's bytes into L2 during this tile's decode
-#define AK_STAGE_PF 1
-#endif
 #ifndef AK_KNOCKOUT
 // timing experiments only (wrong ids): 1 no merges, 2 set-up without rounds, 8 / 9 / 10 / 11 / 12 /
 // 13 / 14 stop after staging / D1 / D2 / N / S / C / F
@@ -89,7 +86,8 @@ struct TileArgs {
     uint64_t *unit_fb;    // BPE: per 64-row unit, the mask of its rows sent to the fallback kernels
     uint64_t *passprof;   // optional: device cycles per pass summed over waves, then counters (T_NPROF entries)
     uint4 *pool;          // BPE: the waves' merge pools (POOL_CAP entries per wave slot, ak_tile.h pool_flush)
-    uint32_t *unit_len;   // BPE: per unit, the length of its staging run (ids + STAGE_DEAD entries)
+    uint32_t *unit_len;   // per unit, the length of its staging run (ids + STAGE_DEAD entries)
+    uint32_t *row_span;   // SentencePiece: per row, the entries it reserved in its unit's run (0: fallback row)
     uint32_t *next_unit;  // the work queue: next unit to take (zeroed before the launch)
     uint64_t ntiles;
     int rows;             // R
@@ -542,19 +540,6 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
         uint4 *dst = (uint4 *)M.bytes;
         for (uint64_t b = (uint64_t)lane; b < nblk; b += 64) dst[b] = src[b];
     }
-    // The next tile's first bytes into L2 while this tile decodes: the rows past this buffer are
-    // the next tile's, so lanes 0..T_BCAP/128 touch one dword per 128-byte line of [S1, the end of
-    // the rows this call was offered) (never past a row this batch holds). The loaded word is
-    // consumed after pass D2 (AK_STAGE_PF), by then long returned, so the next stage's loads hit L2
-    // instead of paying the HBM latency again.
-#if AK_STAGE_PF
-    uint32_t touch = 0;
-    {
-        const uint64_t pend = w_bcast(myoff, nr0);
-        const uint64_t la = (S1 & ~127ull) + 128ull * (uint64_t)lane;
-        if (lane <= BCAP / 128 && la < pend) touch = *(const uint32_t *)(a.in + la);
-    }
-#endif
     const uint64_t nextoff = w_shfl(myoff, lane + 1);
     if (lane < nr) {
         M.fb[lane] = lane >= k ? 1 : 0;
@@ -677,10 +662,6 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             ++vpos;
         }
     }
-#if AK_STAGE_PF
-    // the prefetch's use: never true (a.n > r0 here), but the compiler cannot drop the load
-    if (touch == 0x9E3779B9u && a.n == 0) M.fb[0] = 1;
-#endif
     w_sync();
     return TileRows{k, nr, S0, a0, vpos};
 }
@@ -924,6 +905,30 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
         M.pcnt[c] -= cnt;
     }
     w_sync();
+}
+
+// A unit run's live entries (not STAGE_DEAD) -> out[d0 ...], in order: stage[base, base + len)
+// streamed with 4 dword loads per lane in flight, each 64-entry step compacted by ballot (one wave).
+__device__ __forceinline__ void unit_copy_live(const uint32_t *__restrict__ stage, uint64_t half, uint64_t base, uint64_t len,
+                                               uint32_t *__restrict__ out, uint64_t cap, uint64_t d0, int lane) {
+    constexpr int B = 4;
+    uint64_t d = d0;
+    for (uint64_t k0 = 0; k0 < len; k0 += 64 * B) {
+        uint32_t v[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            const uint64_t k = k0 + (uint64_t)(q * 64 + lane);
+            v[q] = k < len && base + k < half ? stage[base + k] : STAGE_DEAD;
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            const bool keep = v[q] != STAGE_DEAD;
+            const uint64_t KM = w_ballot(keep);
+            const uint64_t at = d + w_rank(KM);
+            if (keep && at < cap) out[at] = v[q];
+            d += (uint64_t)w_popc(KM);
+        }
+    }
 }
 
 // merge every class ring holding >= minc misses, 64 at a time (minc = 1 at the wave's end: all)

@@ -51,6 +51,25 @@ constexpr uint32_t BK_NONE = 0xFFFFFFFFu;
 #define AK_SPM_SELECT_RELAX 1  // instructions, +2.8-3.6 % (A/B on MI355X, 4 M rows)
 #endif
 
+// The word pool (pass F / spm_pool_flush): words of 2..SP_MAXL chars ("▁" included) wait in
+// per-wave rings in global memory, one ring per word length (lengths 2..12, then 13..24 in one
+// ring), until a batch is there (64 words; 32 of the long ring); a batch solves its words one
+// lane each from base 0 with every lane's lattice about as long as every other's (the trie walks
+// per word grow with its length: tools/spm_sim measured ~3 L - 3 steps, max within 10 % of the
+// mean), instead of a tile's 30-40 words of mixed lengths in one round bounded by its longest.
+constexpr int SP_MAXL = SPM_POOL_MAXL;      // longest pooled word (chars, "▁" included)
+constexpr int SP_SHORT = 12;                // longest word of the 64-lane batches
+constexpr int SP_NCLASS = SP_SHORT;         // rings: lengths 2..SP_SHORT, then SP_SHORT+1..SP_MAXL
+constexpr uint32_t SP_RING = 320;           // a ring holds < 64 waiting + one tile's words (<= S_WORDS)
+constexpr uint32_t SP_CAP = SP_NCLASS * SP_RING;  // entries (uint4) per wave slot
+static_assert(SP_RING >= 63 + 256, "a ring holds a batch - 1 waiting + a tile's words");
+__device__ __forceinline__ uint32_t sp_class(int L) { return L <= SP_SHORT ? (uint32_t)(L - 2) : (uint32_t)(SP_NCLASS - 1); }
+__device__ __forceinline__ uint32_t sp_batch(uint32_t c) { return c == (uint32_t)(SP_NCLASS - 1) ? 32u : 64u; }
+// LDS of one batch (over the tile buffers, free between tiles): W codes [CAPL][B] (u16), best
+// [CAPL + 1][B] (f32), back [CAPL + 1][B] (u32), position-major so that lanes at any positions hit
+// distinct banks; position 0 (the "▁" node, never read back) is every lane's dummy slot
+constexpr int sp_lds_bytes(int B, int CAPL) { return CAPL * B * 2 + 2 * (CAPL + 1) * B * 4; }
+
 struct SpmWaveMem {
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
     uint16_t v[S_E];                         // V; after pass W: nxt (u8 per W position)
@@ -59,6 +78,7 @@ struct SpmWaveMem {
     uint32_t back[S_W + AK_SPM_SELECT_RELAX];  // best piece ending here: id << 8 | chars ([S_W]: dummy)
     uint8_t wrow[S_WORDS];                   // row of each word
     uint8_t wmiss[S_WORDS];                  // words the word cache did not hold (pass V)
+    uint8_t wpool[S_WORDS];                  // word goes to the word pool (pass F)
     uint8_t fb[T_MAXR];
     uint8_t mfail[T_MAXR];                   // row has a lattice node within the rounding bound (pass V2)
     uint16_t rowend[T_MAXR];
@@ -66,10 +86,16 @@ struct SpmWaveMem {
     uint16_t wfirst[T_MAXR + 1];             // index of each row's first word (+ end)
     uint32_t rowcnt[T_MAXR];
     uint32_t rowfirst[T_MAXR];               // tile-stream position of the row's first id
+    // ---- kept across tiles (everything above is the batch area of spm_pool_flush between tiles)
     uint64_t passacc[T_NPROF];
     uint64_t unext;                          // the unit's staging run: next free position
     uint64_t ufbm;                           // the unit's rows (bit r - u0) sent to the fallback kernels
+    uint32_t phead[SP_NCLASS];               // the word pool's rings: first waiting entry
+    uint32_t pcnt[SP_NCLASS];                // ... and entries waiting
 };
+static_assert(offsetof(SpmWaveMem, passacc) >= sp_lds_bytes(64, SP_SHORT) &&
+                  offsetof(SpmWaveMem, passacc) >= sp_lds_bytes(32, SP_MAXL),
+              "a pool batch fits the tile buffers");
 static_assert(S_WORDS * 2 <= S_BCAP + 32, "word starts live in the byte buffer");
 static_assert(S_W + 2 * S_WORDS <= 2 * S_E, "nxt + word id counts live in V");
 
@@ -388,9 +414,222 @@ __device__ __forceinline__ bool spm_margin_ok(const SpmWaveMem &M, const SpmDev 
     return minm > tau;
 }
 
+// ---------------------------------------------------------------------------------------------
+// The word pool. A pooled word's entry {stage index of its first reserved slot, L, R, row, M}: pass
+// F reserves R slots for it in the unit run (R >= its id count: a char some piece holds gives at most
+// one piece end, one in no piece its UTF-8 bytes; model flag pool_ok) and writes its W codes there
+// as u16 pairs, which the batch reads back (same wave, its stores drained: ak_tile.h load_l2) and
+// overwrites with the ids and STAGE_DEAD for the slots left over. A word whose margin test fails
+// (the row needs the carried base: pass V2) sends its row to the fallback kernels instead: its
+// unit's fallback mask gets the row (the copy then takes the row from its fallback slot and skips
+// its run entries, k_unit_copy_spm) and the first such word appends it to the fallback list.
+
+// Position-major batch arrays: slot (pos, lane) at pos * B + lane
+template <int B, int CAPL>
+struct SpBatch {
+    uint16_t *codes;  // [CAPL][B]
+    float *best;      // [CAPL + 1][B]
+    uint32_t *back;   // [CAPL + 1][B]
+    __device__ __forceinline__ SpBatch(SpmWaveMem &M) {
+        uint8_t *b = (uint8_t *)&M;
+        codes = (uint16_t *)b;
+        best = (float *)(b + CAPL * B * 2);
+        back = (uint32_t *)(b + CAPL * B * 2 + (CAPL + 1) * B * 4);
+    }
+};
+
+// word_dp_flat over one lane's pooled word (positions 0..L, "▁" at 0), from base 0: the same
+// candidates in the same order, first arrival wins, the same margin bookkeeping; no rebase (pool_ok:
+// a pooled word cannot reach the bound from base 0). Lanes with act false pass L = 0.
+template <int B, int CAPL>
+__device__ __forceinline__ float word_dp_pool(const SpBatch<B, CAPL> &P, const SpmDev &m, int lane, int L) {
+    float minm = 3.0e38f;
+    bool act = L > 0;
+    int s = 0, k = 0, node = 0, nb = m.root_base;
+    float till = 0.0f;
+    bool hs = false;
+    const int ln = lane < B ? lane : 0;
+    uint32_t v = P.codes[ln];
+    while (w_ballot(act)) {
+        const bool coded = act && (v & W_CODED);
+        const int t = coded ? nb + (int)(v & 0x7FFFu) : m.root_base;  // idle lanes read a node in range
+        const int4 e = m.trie[t];
+        const bool ok = coded && e.x == node;
+        const int value = e.z;
+        const bool hv = ok && value >= 0 && ((value >> 24) & 3) != 2;
+        const int ee = k + 1;
+        {  // the piece's candidate as selects into the lane's slot, or its dummy (position 0)
+            const int es = (hv ? ee : 0) * B + ln;
+            const uint32_t bk = P.back[es];
+            const float bb = P.best[es];
+            const float cand = __int_as_float(e.w) + till;
+            const bool none = bk == BK_NONE;
+            const bool take = none || cand > bb;
+            const float gap = take ? cand - bb : bb - cand;
+            minm = hv && !none ? fminf(minm, gap) : minm;
+            P.best[es] = take ? cand : bb;
+            P.back[es] = take ? (((uint32_t)(value & 0xFFFFFF) << 8) | (uint32_t)(ee - s)) : bk;
+            hs = hs || (hv && k == s);
+        }
+        node = ok ? t : node;
+        nb = ok ? e.y : nb;
+        k = ok ? ee : k;
+        const uint32_t vn = P.codes[(k < CAPL ? k : CAPL - 1) * B + ln];
+        const bool end = act && (!ok || k >= L || !(vn & W_CODED));
+        {  // a start with no piece of exactly its first char: an unk node (never a char some piece
+           // holds under pool_ok, but the rule is kept whole)
+            const bool unk = end && !hs;
+            const int es = (unk ? s + 1 : 0) * B + ln;
+            const uint32_t bk = P.back[es];
+            const float bb = P.best[es];
+            const float cand = m.unk_score + till;
+            const bool none = bk == BK_NONE;
+            const bool take = none || cand > bb;
+            const float gap = take ? cand - bb : bb - cand;
+            minm = unk && !none ? fminf(minm, gap) : minm;
+            P.best[es] = take ? cand : bb;
+            P.back[es] = take ? (((uint32_t)m.unk_id << 8) | 1u) : bk;
+        }
+        const int sn = s + 1;
+        const bool fin = end && sn >= L;
+        const bool next = end && !fin;
+        const int sc = (next ? sn : 0) * B + ln;
+        const float tn = P.best[sc];
+        const uint32_t vs = P.codes[next ? sc : ln];
+        s = next ? sn : s;
+        k = next ? sn : k;
+        node = next ? 0 : node;
+        nb = next ? m.root_base : nb;
+        hs = hs && !next;
+        till = next ? tn : till;
+        v = next ? vs : vn;
+        act = act && !fin;
+    }
+    return minm;
+}
+
+__device__ __forceinline__ uint32_t utf8_bytes_of(uint32_t cp, uint32_t bytes[4]) {
+    const int cl = utf8_len(cp);
+    if (cl == 1) { bytes[0] = cp; }
+    else if (cl == 2) { bytes[0] = 0xC0u | (cp >> 6); bytes[1] = 0x80u | (cp & 63u); }
+    else if (cl == 3) { bytes[0] = 0xE0u | (cp >> 12); bytes[1] = 0x80u | ((cp >> 6) & 63u); bytes[2] = 0x80u | (cp & 63u); }
+    else { bytes[0] = 0xF0u | (cp >> 18); bytes[1] = 0x80u | ((cp >> 12) & 63u); bytes[2] = 0x80u | ((cp >> 6) & 63u); bytes[3] = 0x80u | (cp & 63u); }
+    return (uint32_t)cl;
+}
+
+// One batch of ring c: its first cnt (<= B) entries, lane l the l-th.
+template <int B, int CAPL>
+__device__ __noinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M, uint4 *pool, uint32_t c, uint32_t cnt,
+                                            PassClock &pc) {
+    const SpmDev &m = ta.ra.spm;
+    const int lane = w_lane();
+    const bool act = (uint32_t)lane < cnt;  // cnt <= B
+    const int ln = lane < B ? lane : 0;
+    const SpBatch<B, CAPL> P(M);
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's run / count / pool stores have landed
+#endif
+    uint4 *ring = pool + c * SP_RING;
+    const uint32_t head = w_bcast(M.phead[c], 0);
+    const uint4 e = load_l2(ring + (head + (uint32_t)lane) % SP_RING);  // every lane: a slot in range
+    const uint64_t dst = act ? (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32) : 0ull;
+    const int L = act ? (int)((e.y >> 16) & 0xFFu) : 0;
+    const uint32_t R = act ? e.y >> 24 : 0u;
+    const uint32_t row = e.z, mpos = e.w;
+    uint32_t *sp = (uint32_t *)ta.ra.out + dst;
+    // the codes back from the reserved slots (u16 pairs; dword-aligned 16-byte loads, the stage is
+    // padded past every run), into the position-major batch arrays; every back slot to BK_NONE
+#pragma unroll
+    for (int q = 0; q < (CAPL + 7) / 8; ++q) {
+        const uint4 x = load_l2((const uint4 *)sp + q);
+        const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+            const int pos = 8 * q + h;
+            if (pos < CAPL && lane < B) P.codes[pos * B + ln] = (uint16_t)(xs[h >> 1] >> (16 * (h & 1)));
+        }
+    }
+#pragma unroll
+    for (int pos = 0; pos <= CAPL; ++pos)
+        if (lane < B) P.back[pos * B + ln] = BK_NONE;
+    const float minm = word_dp_pool<B, CAPL>(P, m, lane, L);
+    // the margin test of spm_margin_ok with the word's position in its row (M = mpos x max |score|)
+    const float Mb = fminf((float)mpos * m.abs_score_max, SPM_REBASE + m.abs_score_max) + 1.0f;
+    const float tau = (float)(L + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
+    const bool redo = act && !(minm > tau);
+    if (pc.on) {
+        pc.count(TC_BBATCH, 1);
+        pc.count(TC_BLANES, w_ballot(act));
+        pc.count(TC_BROUNDS, w_ballot(redo));
+    }
+    if (redo) {  // the row needs the carried base: the fallback kernels (once per row)
+        const uint64_t bit = 1ull << (row % TILE_UNIT);
+        const unsigned long long old = atomicOr((unsigned long long *)(ta.unit_fb + row / TILE_UNIT), (unsigned long long)bit);
+        if (!(old & bit)) ta.fb_list[atomicAdd(ta.fb_count, 1u)] = row;
+    }
+    const bool emit = act && !redo;
+    // the ids: count along the back links, then write them from the end; STAGE_DEAD past them
+    uint32_t n = 0;
+    {
+        int ep = emit ? L : 0;
+        while (w_ballot(ep > 0)) {
+            if (ep > 0) {
+                const uint32_t bk = P.back[ep * B + ln];
+                const int s0 = ep - (int)(bk & 0xFFu);
+                n += (int)(bk >> 8) == m.unk_id ? (uint32_t)utf8_len(spm_wcp(m, P.codes[s0 * B + ln])) : 1u;
+                ep = s0;
+            }
+        }
+    }
+    {
+        int ep = emit ? L : 0;
+        uint32_t at = n;
+        while (w_ballot(ep > 0)) {
+            if (ep > 0) {
+                const uint32_t bk = P.back[ep * B + ln];
+                const int s0 = ep - (int)(bk & 0xFFu);
+                const uint32_t id = bk >> 8;
+                if ((int)id == m.unk_id) {  // byte fallback: one id per UTF-8 byte
+                    uint32_t bytes[4];
+                    const uint32_t cl = utf8_bytes_of(spm_wcp(m, P.codes[s0 * B + ln]), bytes);
+                    at -= cl;
+                    for (uint32_t q = 0; q < cl; ++q) sp[at + q] = (uint32_t)m.byte_ids[bytes[q]];
+                } else {
+                    sp[--at] = id;
+                }
+                ep = s0;
+            }
+        }
+    }
+    if (emit) {
+        for (uint32_t i = n; i < R; ++i) sp[i] = STAGE_DEAD;
+        if (R > n) atomicSub(ta.counts + row, R - n);
+    }
+    w_sync();
+    if (lane == 0) {
+        M.phead[c] = (head + cnt) % SP_RING;
+        M.pcnt[c] -= cnt;
+    }
+    w_sync();
+}
+
+// every ring holding a full batch (minc = 1 at the wave's end: every word), a batch at a time
+__device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, SpmWaveMem &M, uint4 *pool, bool all, PassClock &pc) {
+#pragma unroll 1
+    for (uint32_t c = 0; c < (uint32_t)SP_NCLASS; ++c) {
+        const uint32_t bw = sp_batch(c);
+        for (;;) {
+            const uint32_t k = w_bcast(M.pcnt[c], 0);
+            if (k == 0 || (!all && k < bw)) break;
+            if (c == (uint32_t)(SP_NCLASS - 1)) spm_pool_flush<32, SP_MAXL>(ta, M, pool, c, k < bw ? k : bw, pc);
+            else spm_pool_flush<64, SP_SHORT>(ta, M, pool, c, k < bw ? k : bw, pc);
+        }
+    }
+}
+
 template <int FLAGS>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
-                        SpmWaveMem &M, PassClock &pc) {
+                        SpmWaveMem &M, uint4 *pool, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
@@ -512,7 +751,20 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                 if (!spm_margin_ok(M, m, row, p0, p1, __uint_as_float(hd.y))) M.mfail[row] = 1;
             }
         }
-        const bool miss = act && !hit;
+        // a miss of 2..SP_MAXL chars in a row not sent to the fallback kernels waits in the word
+        // pool (pass F reserves its slots); the rest are solved here
+        const int L = p1 - p0;
+        const bool pooled = act && !hit && m.pool_ok && L >= 2 && L <= SP_MAXL && !M.fb[row];
+        if (act) M.wpool[j] = pooled ? 1 : 0;
+        if (pooled) {  // its id bound: one per char some piece holds, UTF-8 bytes for the others
+            uint32_t R = 0;
+            for (int q = p0; q < p1; ++q) {
+                const uint32_t x = M.w[q];
+                R += (x & W_CODED) ? 1u : (uint32_t)utf8_len(x);
+            }
+            wcnt[j] = (uint16_t)R;
+        }
+        const bool miss = act && !hit && !pooled;
         const uint64_t MM = w_ballot(miss);
         if (miss) M.wmiss[nmiss + w_rank(MM)] = (uint8_t)j;
         nmiss += (uint32_t)w_popc(MM);
@@ -542,6 +794,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     // carried float base, exactly as sentencepiece's whole-row lattice (ak_dev.h SpmSink)
     {
         const bool redo = lane < nr && M.mfail[lane] && !M.fb[lane];
+        pc.count(TC_BROUNDS, w_ballot(redo));  // rows redone from the carried base
         if (w_ballot(redo)) {
             if (redo) {
                 float base = 0.0f;
@@ -552,6 +805,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                     float unused = 0.0f;
                     word_dp<false>(M, m, p0, p1, base, unused);
                     wcnt[j] = (uint16_t)word_backtrack(M, m, nxt, p0, p1);
+                    M.wpool[j] = 0;  // the whole row is solved here
                     base = M.best[p1];
                 }
             }
@@ -595,8 +849,34 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         if (live && first) M.rowfirst[row] = P;
         w_sync();
         if (live && last_of_row) M.rowcnt[row] = P + c - M.rowfirst[row];  // a row's words are consecutive
-        if (live) {
-            const int p1 = !last_of_row ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1;
+        const int p1 = act ? (!last_of_row ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
+        const bool pooled = live && M.wpool[j];
+        if (pooled) {  // reserve its c = R slots and park its W codes there (u16 pairs) for the batch
+            if (P + c > scap) over = true;
+            else
+                for (int q = p0; q < p1; q += 2)
+                    stage[P + (uint32_t)((q - p0) >> 1)] = (uint32_t)M.w[q] | (q + 1 < p1 ? (uint32_t)M.w[q + 1] << 16 : 0u);
+        }
+        // the pooled words join their length's ring: {stage index, L << 16 | R << 24, row, M}
+        {
+            const int L = p1 - p0;
+            const uint32_t cls = pooled ? sp_class(L) : 0xFFu;
+            const uint64_t dst = sbase + P;
+            const uint4 ent = make_uint4((uint32_t)dst, (uint32_t)(dst >> 32) | ((uint32_t)L << 16) | (c << 24),
+                                         (uint32_t)(r0 + (uint64_t)row), (uint32_t)(p1 - (int)M.rowpos[row] + 1));
+            uint64_t CMs = w_ballot(pooled);
+            while (CMs) {  // the classes present in this step, one ballot each
+                const uint32_t cc = w_bcast(cls, __builtin_ctzll(CMs));
+                const uint64_t CM = w_ballot(cls == cc);
+                const uint32_t head = w_bcast(M.phead[cc], 0), k = w_bcast(M.pcnt[cc], 0);
+                if (cls == cc) pool[cc * SP_RING + (head + k + w_rank(CM)) % SP_RING] = ent;
+                w_sync();
+                if (lane == 0) M.pcnt[cc] = k + (uint32_t)w_popc(CM);
+                w_sync();
+                CMs &= ~CM;
+            }
+        }
+        if (live && !pooled) {
             uint64_t d = P;
             for (int s = p0; s < p1;) {
                 const int e = s + (int)nxt[s];
@@ -626,12 +906,17 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     if (lane == 0) M.unext = sbase + pos;
     if (w_ballot(over) && lane == 0) __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     w_sync();
-    if (lane < nr && !M.fb[lane]) {
-        ta.counts[r0 + lane] = M.rowcnt[lane];
-        if (a.row_status) a.row_status[r0 + lane] = 0;
+    if (lane < nr) {
+        if (!M.fb[lane]) {
+            ta.counts[r0 + lane] = M.rowcnt[lane];
+            if (a.row_status) a.row_status[r0 + lane] = 0;
+        }
+        ta.row_span[r0 + lane] = M.fb[lane] ? 0u : M.rowcnt[lane];  // the row's entries in the unit run
     }
     w_sync();
     pc.mark(TP_F);
+    spm_pool_drain(ta, M, pool, false, pc);  // full batches (the tile's buffers are free now)
+    pc.mark(TP_FBE);
     return nr;
 }
 
@@ -639,20 +924,34 @@ template <int FLAGS>
 __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
+    uint4 *pool = ta.pool + (uint64_t)wave_gid * SP_CAP;  // this wave's rings
+    if (w_lane() < SP_NCLASS) {
+        M.phead[w_lane()] = 0;
+        M.pcnt[w_lane()] = 0;
+    }
+    w_sync();
     // units of TILE_UNIT rows from the work queue (tile_first_unit); inside a unit, each tile
     // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
     for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
         pc.mark(TP_LOOP);
         const uint64_t r0 = t * TILE_UNIT;
         const uint64_t r1 = r0 + TILE_UNIT < ta.ra.n ? r0 + TILE_UNIT : ta.ra.n;
-        if (w_lane() == 0) {  // the unit's staging run starts at its rows' slot base 2 offs[r0] + 2 r0
-            M.unext = 2 * ta.ra.offs[r0] + 2 * r0;
+        const uint64_t run0 = 2 * ta.ra.offs[r0] + 2 * r0;  // the unit's staging run: its rows' slot base
+        if (w_lane() == 0) {
+            M.unext = run0;
             M.ufbm = 0;
         }
         w_sync();
-        for (uint64_t r = r0; r < r1;) r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, M, pc);
-        if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
+        for (uint64_t r = r0; r < r1;)
+            r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, M, pool, pc);
+        if (w_lane() == 0) {
+            // OR: a pooled word of this unit may already have sent a row to the fallback kernels
+            if (M.ufbm) atomicOr((unsigned long long *)(ta.unit_fb + t), (unsigned long long)M.ufbm);
+            ta.unit_len[t] = (uint32_t)(M.unext - run0);
+        }
     }
+    spm_pool_drain(ta, M, pool, true, pc);  // the rest: every pooled word solved before the wave leaves
+    pc.mark(TP_FBE);
     pc.flush(ta.passprof);
 }
 

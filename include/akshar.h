@@ -244,7 +244,9 @@ int ak_profile_tile_passes(ak_ws *ws, uint64_t *cycles, int n);
 /* Event counters of the same instrumented launches (profiling level 2), reset by each call:
  * [0] BPE pre-tokens probed in the pre-token cache (slot 3 of the pass breakdown), [1] its hits,
  * [2] merge batches (64 pre-tokens a wave merges at once), [3] merge rounds, [4] lanes merging, summed
- * over rounds (lane utilisation of the merge loop = [4] / (64 [3])).
+ * over rounds (lane utilisation of the merge loop = [4] / (64 [3])). SentencePiece launches: [0] / [1]
+ * word-cache probes / hits, [2] word-pool batches, [3] rows redone from the carried base (in the tile,
+ * or by the fallback kernels after a pooled word's margin test), [4] pooled words.
  * Returns the number of counters written (0 if no tile kernel has run), or a negative error. */
 #define AK_TILE_NCOUNTERS 5
 int ak_profile_tile_counters(ak_ws *ws, uint64_t *counts, int n);

@@ -103,6 +103,10 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     m->sdev.unk_score = m->spm.min_score - 10.0f;
     m->sdev.abs_score_max = m->spm.abs_score_max;
     m->sdev.ws_code = m->spm.ws_code;
+    {
+        const char *pe = getenv("AK_SPM_POOL");
+        m->sdev.pool_ok = spm_pool_allowed(m->spm.single_all, m->spm.abs_score_max) && !(pe && pe[0] == '0') ? 1u : 0u;
+    }
     m->piece_bytes.assign(bytes, bytes + offs[n]);
     m->piece_offs.assign(offs, offs + n + 1);
     m->types.assign(types, types + n);
@@ -376,6 +380,11 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     ta.ntiles = (n + TILE_UNIT - 1) / TILE_UNIT; ta.rows = rows;
     std::vector<uint64_t> prof(T_NPROF, 0);
     ta.passprof = prof.data();  // the pass clocks read 0 here; the counters are real
+    std::vector<uint4> pool((size_t)g_waves * SP_CAP);
+    std::vector<uint32_t> unit_len(nunits), row_span(n);
+    ta.pool = pool.data();
+    ta.unit_len = unit_len.data();
+    ta.row_span = row_span.data();
     std::vector<SpmWaveMem> M(g_waves);
     run_waves([&](int w) { spm_tiles_wave<3>(ta, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
     for (int i = 0; i < T_NCTR; ++i) g_last_ctr[i] = prof[T_NPASS + i];
@@ -405,14 +414,28 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     }
     out_offs[0] = 0;
     for (uint64_t r = 0; r < n; ++r) out_offs[r + 1] = out_offs[r] + counts[r];
-    for (uint64_t u = 0; u < nunits; ++u) {  // as k_unit_copy
+    for (uint64_t u = 0; u < nunits; ++u) {  // as k_unit_copy_spm
         const uint64_t u0 = u * TILE_UNIT;
         uint64_t p = 2 * offs[u0] + 2 * u0;
-        for (uint64_t r = u0; r < n && r < u0 + TILE_UNIT; ++r) {
+        if (unit_fb[u] == 0) {  // the run's live entries in order
+            uint64_t d = out_offs[u0];
+            for (uint64_t k = 0; k < unit_len[u]; ++k)
+                if (stage[p + k] != STAGE_DEAD && d < cap) out[d++] = stage[p + k];
+            if (d != out_offs[std::min<uint64_t>(n, u0 + TILE_UNIT)]) return -3;
+            continue;
+        }
+        for (uint64_t r = u0; r < n && r < u0 + TILE_UNIT; ++r) {  // row by row over the spans
             const bool fb = (unit_fb[u] >> (r - u0)) & 1ull;
-            const uint32_t *src = fb ? stage.data() + half + 2 * offs[r] + 2 * r : stage.data() + p;
-            for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = src[i];
-            if (!fb) p += counts[r];
+            if (fb) {
+                const uint32_t *src = stage.data() + half + 2 * offs[r] + 2 * r;
+                for (uint64_t i = 0; i < counts[r] && out_offs[r] + i < cap; ++i) out[out_offs[r] + i] = src[i];
+            } else {
+                uint64_t d = out_offs[r];
+                for (uint64_t k = 0; k < row_span[r]; ++k)
+                    if (stage[p + k] != STAGE_DEAD && d < cap) out[d++] = stage[p + k];
+                if (d != out_offs[r + 1]) return -3;
+            }
+            p += row_span[r];
         }
     }
     return (int64_t)out_offs[n];
