@@ -519,7 +519,7 @@ __device__ __forceinline__ uint32_t utf8_bytes_of(uint32_t cp, uint32_t bytes[4]
 
 // One batch of ring c: its first cnt (<= B) entries, lane l the l-th.
 template <int B, int CAPL>
-__device__ __noinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M, uint4 *pool, uint32_t c, uint32_t cnt,
+__device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M, uint4 *pool, uint32_t c, uint32_t cnt,
                                             PassClock &pc) {
     const SpmDev &m = ta.ra.spm;
     const int lane = w_lane();
