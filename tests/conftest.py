@@ -18,6 +18,15 @@ SPM_PATH = os.path.join(ROOT, "models", "akshar.model")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built HIP engine")
+    # The CPU suite (-m "not gpu") is mostly the host emulation of the tile kernels (64 threads per
+    # emulated wave): it runs on 4 pytest-xdist workers unless -n was given, so the whole suite takes
+    # minutes, not a quarter of an hour. GPU runs stay in one process.
+    if (os.environ.get("PYTEST_XDIST_WORKER") is None and config.pluginmanager.hasplugin("xdist")
+            and config.getoption("markexpr", "") == "not gpu" and not config.getoption("numprocesses", None)
+            and not config.getoption("collectonly") and os.environ.get("AK_TEST_SERIAL") != "1"):
+        config.option.numprocesses = 4
+        config.option.dist = "load"
+        config.option.tx = ["popen"] * 4
 
 
 @pytest.fixture(scope="session")
