@@ -811,6 +811,7 @@ struct SpmDev {
     const uint32_t *wc;    // tile path: the word cache (ak_swc.h; null = off)
     uint32_t wc_mask;
     uint32_t pool_ok;      // tile path: the word pool may take words (ak_tile_spm.h spm_pool_ok)
+    uint32_t pool_min;     // ... of at least this many chars ("▁" included; shorter ones stay in the tile)
 };
 
 // word chars are stored as 0x80000000 | code for chars some piece holds, the plain code point

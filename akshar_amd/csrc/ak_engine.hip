@@ -376,6 +376,10 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     // the tile path's word pool (ak_tile_spm.h): AK_SPM_POOL=0 leaves it off (development aid, A/B)
     const char *pe = getenv("AK_SPM_POOL");
     m->dev.pool_ok = spm_pool_allowed(t.single_all, t.abs_score_max) && !(pe && pe[0] == '0') ? 1u : 0u;
+    {  // AK_SPM_POOL_MIN: the shortest pooled word (development aid)
+        const char *pm = getenv("AK_SPM_POOL_MIN");
+        m->dev.pool_min = pm ? (uint32_t)std::max(2, atoi(pm)) : 2u;
+    }
     // the tile kernel's word cache (ak_swc.h): off unless AK_SWC=1 (measured slower on MI355X: the
     // lattice runs lane per word in rounds of 64, and a tile's words fit one round, so hits do not
     // shorten it while every word pays the probe). AK_SWC_BITS=b forces 2^b slots.

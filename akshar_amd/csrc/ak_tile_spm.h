@@ -754,7 +754,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         // a miss of 2..SP_MAXL chars in a row not sent to the fallback kernels waits in the word
         // pool (pass F reserves its slots); the rest are solved here
         const int L = p1 - p0;
-        const bool pooled = act && !hit && m.pool_ok && L >= 2 && L <= SP_MAXL && !M.fb[row];
+        const bool pooled = act && !hit && m.pool_ok && L >= (int)m.pool_min && L <= SP_MAXL && !M.fb[row];
         if (act) M.wpool[j] = pooled ? 1 : 0;
         if (pooled) {  // its id bound: one per char some piece holds, UTF-8 bytes for the others
             uint32_t R = 0;

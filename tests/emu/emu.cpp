@@ -106,6 +106,10 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     {
         const char *pe = getenv("AK_SPM_POOL");
         m->sdev.pool_ok = spm_pool_allowed(m->spm.single_all, m->spm.abs_score_max) && !(pe && pe[0] == '0') ? 1u : 0u;
+    {  // AK_SPM_POOL_MIN: the shortest pooled word (development aid)
+        const char *pm = getenv("AK_SPM_POOL_MIN");
+        m->sdev.pool_min = pm ? (uint32_t)std::max(2, atoi(pm)) : 2u;
+    }
     }
     m->piece_bytes.assign(bytes, bytes + offs[n]);
     m->piece_offs.assign(offs, offs + n + 1);
