@@ -546,6 +546,7 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->unit_len);
     (void)hipFree(w->bpool);
     (void)hipFree(w->row_span);
+    (void)hipFree(w->redo);
     (void)hipFree(w->counts);
     (void)hipFree(w->slow_list);
     (void)hipFree(w->huge_list);

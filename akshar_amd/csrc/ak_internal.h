@@ -68,6 +68,8 @@ struct AkWs {
     uint64_t cap_bpool = 0;         // pool_flush, ak_tile_spm.h spm_pool_flush), entries
     uint32_t *row_span = nullptr;   // tile SentencePiece: per row, its entries in the unit run
     uint64_t cap_row_span = 0;
+    uint32_t *redo = nullptr;       // tile SentencePiece: rows the word pool sent back (k_spm_redo)
+    uint64_t cap_redo = 0;
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)

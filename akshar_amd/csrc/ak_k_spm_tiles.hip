@@ -3,6 +3,8 @@
 //                    2 offs[r] + 2 r: a row's ids never exceed 2 x its bytes + 1) and writes per-row
 //                    id counts; rare rows (NFC / invalid UTF-8 / over the tile / a close lattice
 //                    call) go to a fallback list
+//   k_spm_redo       rows a pooled word's margin test sent back: wave per row, the tile pipeline
+//                    with the pool off (pass V2 solves the row from the carried base)
 //   k_spm_tile_fb    fallback rows, one lane per row (ak_rows.h process_row: the exact sequential
 //                    lattice with the carried base), into the same slots; rows past its buffers go
 //   k_rows_tier      ... to the slow and huge tiers (ak_internal.h)
@@ -38,6 +40,25 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     const uint32_t wave = threadIdx.x >> 6;
     spm_tiles_wave<FLAGS>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
                           gridDim.x * (SPM_TILE_BLOCK / 64));
+}
+
+// rows the word pool sent back (ak_tile_spm.h spm_redo_wave): wave per row, same LDS as k_spm_tiles
+template <int FLAGS>
+__global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_redo(TileArgs ta) {
+    __shared__ uint32_t hot_tab[HOT_N];
+    __shared__ uint16_t scode[HOT_N];
+    __shared__ SpmWaveMem wm[SPM_TILE_BLOCK / 64];
+    if (*ta.redo_count == 0) return;  // uniform: the common case
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
+        const uint32_t cp = hot_cp(i);
+        hot_tab[i] = hot_word(cp);
+        const uint32_t c = spm_code(ta.ra.spm, cp);
+        scode[i] = (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
+    }
+    __syncthreads();
+    const uint32_t wave = threadIdx.x >> 6;
+    spm_redo_wave<FLAGS>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
+                         gridDim.x * (SPM_TILE_BLOCK / 64));
 }
 
 // fallback rows with the fast row kernel's buffer sizes, straight into the row's tile slot. The
@@ -178,6 +199,12 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
         HIP_TRY(hipMalloc(&w->fb2, a0.n * 4));
         w->cap_fb2 = a0.n;
     }
+    if (w->cap_redo < a0.n) {
+        (void)hipFree(w->redo);
+        w->redo = nullptr;
+        HIP_TRY(hipMalloc(&w->redo, a0.n * 4));
+        w->cap_redo = a0.n;
+    }
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra = a0;
@@ -192,11 +219,14 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.fb2_list = w->fb2;
     ta.fb2_count = w->tile_misc + 2;
     ta.next_unit = w->tile_misc + 3;
+    ta.redo_list = w->redo;
+    ta.redo_count = w->tile_misc + 4;
     ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.rows = R;
-    // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4 * 4, st));
+    // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count, the
+    // unit queue, the word pool's redo count
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 5 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = SPM_TILE_BLOCK / 64;
     int bpc = g_spm_blocks_per_cu.load(std::memory_order_relaxed);
@@ -222,6 +252,8 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
+    k_spm_redo<3><<<(unsigned)num_cus() * (unsigned)bpc, SPM_TILE_BLOCK, 0, st>>>(tfb);
+    HIP_TRY(hipGetLastError());
     static std::atomic<int> fb_bpc{0};
     k_spm_tile_fb<3><<<resident_grid(k_spm_tile_fb<3>, SPM_FB_BLOCK, fb_bpc), SPM_FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;

@@ -88,6 +88,8 @@ struct TileArgs {
     uint4 *pool;          // BPE: the waves' merge pools (POOL_CAP entries per wave slot, ak_tile.h pool_flush)
     uint32_t *unit_len;   // per unit, the length of its staging run (ids + STAGE_DEAD entries)
     uint32_t *row_span;   // SentencePiece: per row, the entries it reserved in its unit's run (0: fallback row)
+    uint32_t *redo_list;  // SentencePiece: rows a pooled word's margin test sent back (k_spm_redo)
+    uint32_t *redo_count; // its length (zeroed before the launch)
     uint32_t *next_unit;  // the work queue: next unit to take (zeroed before the launch)
     uint64_t ntiles;
     int rows;             // R

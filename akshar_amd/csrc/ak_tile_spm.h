@@ -562,10 +562,10 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M
         pc.count(TC_BLANES, w_ballot(act));
         pc.count(TC_BROUNDS, w_ballot(redo));
     }
-    if (redo) {  // the row needs the carried base: the fallback kernels (once per row)
+    if (redo) {  // the row needs the carried base: k_spm_redo re-encodes it into its fallback slot (once)
         const uint64_t bit = 1ull << (row % TILE_UNIT);
         const unsigned long long old = atomicOr((unsigned long long *)(ta.unit_fb + row / TILE_UNIT), (unsigned long long)bit);
-        if (!(old & bit)) ta.fb_list[atomicAdd(ta.fb_count, 1u)] = row;
+        if (!(old & bit)) ta.redo_list[atomicAdd(ta.redo_count, 1u)] = row;
     }
     const bool emit = act && !redo;
     // the ids: count along the back links, then write them from the end; STAGE_DEAD past them
@@ -629,7 +629,7 @@ __device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, SpmWaveMem &M
 
 template <int FLAGS>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
-                        SpmWaveMem &M, uint4 *pool, PassClock &pc) {
+                        SpmWaveMem &M, uint4 *pool, PassClock &pc, bool redo_mode = false) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
@@ -754,7 +754,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         // a miss of 2..SP_MAXL chars in a row not sent to the fallback kernels waits in the word
         // pool (pass F reserves its slots); the rest are solved here
         const int L = p1 - p0;
-        const bool pooled = act && !hit && m.pool_ok && L >= (int)m.pool_min && L <= SP_MAXL && !M.fb[row];
+        const bool pooled = act && !hit && m.pool_ok && !redo_mode && L >= (int)m.pool_min && L <= SP_MAXL && !M.fb[row];
         if (act) M.wpool[j] = pooled ? 1 : 0;
         if (pooled) {  // its id bound: one per char some piece holds, UTF-8 bytes for the others
             uint32_t R = 0;
@@ -911,7 +911,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             ta.counts[r0 + lane] = M.rowcnt[lane];
             if (a.row_status) a.row_status[r0 + lane] = 0;
         }
-        ta.row_span[r0 + lane] = M.fb[lane] ? 0u : M.rowcnt[lane];  // the row's entries in the unit run
+        if (!redo_mode) ta.row_span[r0 + lane] = M.fb[lane] ? 0u : M.rowcnt[lane];  // the row's entries in the unit run
     }
     w_sync();
     pc.mark(TP_F);
@@ -953,6 +953,33 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
     spm_pool_drain(ta, M, pool, true, pc);  // the rest: every pooled word solved before the wave leaves
     pc.mark(TP_FBE);
     pc.flush(ta.passprof);
+}
+
+// Rows a pooled word's margin test sent back (k_spm_redo): each is encoded again as a tile of its own
+// with the pool off, so its words run in the tile, the close call triggers pass V2 and the row is
+// solved from the carried base; the ids go to the row's fallback slot (ta.ra.out is the second
+// staging half) and its count replaces the one pass F wrote. Its span in the unit run is left as it
+// was (k_unit_copy_spm steps over it).
+template <int FLAGS>
+__device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M, uint32_t wave_gid,
+                              uint32_t nwaves) {
+    PassClock pc;
+    pc.init(false, M.passacc);
+    if (w_lane() < SP_NCLASS) {
+        M.phead[w_lane()] = 0;
+        M.pcnt[w_lane()] = 0;
+    }
+    w_sync();
+    const uint32_t nredo = *ta.redo_count;
+    for (uint32_t i = wave_gid; i < nredo; i += nwaves) {
+        const uint64_t r = ta.redo_list[i];
+        if (w_lane() == 0) {
+            M.unext = 2 * ta.ra.offs[r] + 2 * r;
+            M.ufbm = 0;
+        }
+        w_sync();
+        (void)spm_tile<FLAGS>(ta, r, r + 1, H, scode, M, nullptr, pc, true);
+    }
 }
 
 }  // namespace ak

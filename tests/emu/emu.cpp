@@ -247,6 +247,8 @@ static uint32_t g_last_fb = 0;
 extern "C" uint32_t emu_last_fallback_rows() { return g_last_fb; }
 // the last tile launch's event counters (ak_tile.h TC_*: pre-token cache probes, hits)
 static uint64_t g_last_ctr[T_NCTR] = {};
+static uint32_t g_last_redo = 0;
+extern "C" uint32_t emu_last_redo_rows() { return g_last_redo; }
 extern "C" void emu_last_counters(uint64_t *out) { for (int i = 0; i < T_NCTR; ++i) out[i] = g_last_ctr[i]; }
 // waves the tile entries below emulate at once (each its own 64 threads and wave memory), all taking
 // units from the one work queue as on the GPU
@@ -385,12 +387,22 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     std::vector<uint64_t> prof(T_NPROF, 0);
     ta.passprof = prof.data();  // the pass clocks read 0 here; the counters are real
     std::vector<uint4> pool((size_t)g_waves * SP_CAP);
-    std::vector<uint32_t> unit_len(nunits), row_span(n);
+    std::vector<uint32_t> unit_len(nunits), row_span(n), redo(n);
+    uint32_t nredo = 0;
     ta.pool = pool.data();
     ta.unit_len = unit_len.data();
     ta.row_span = row_span.data();
+    ta.redo_list = redo.data();
+    ta.redo_count = &nredo;
     std::vector<SpmWaveMem> M(g_waves);
     run_waves([&](int w) { spm_tiles_wave<3>(ta, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
+    g_last_redo = nredo;
+    if (getenv("AK_EMU_DUMP_REDO")) { for (uint32_t i = 0; i < nredo; ++i) fprintf(stderr, "redo row %u\n", redo[i]); }
+    {  // as k_spm_redo: the rows the word pool sent back, into their fallback slots
+        TileArgs tr = ta;
+        tr.ra.out = stage.data() + half;
+        run_waves([&](int w) { spm_redo_wave<3>(tr, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
+    }
     for (int i = 0; i < T_NCTR; ++i) g_last_ctr[i] = prof[T_NPASS + i];
     if (err) return -1;
     g_last_fb = fbn;

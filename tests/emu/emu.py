@@ -191,3 +191,9 @@ def last_counters_all():
 
 def last_fallback_rows():
     return int(lib().emu_last_fallback_rows())
+
+
+def last_redo_rows():
+    """Rows the SentencePiece word pool sent back to be solved from the carried base (k_spm_redo)."""
+    lib().emu_last_redo_rows.restype = ctypes.c_uint32
+    return int(lib().emu_last_redo_rows())

@@ -119,3 +119,37 @@ def test_precomposed_nukta_letters(em, spm_model):
     assert emu.last_fallback_rows() == 0
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+@pytest.mark.parametrize("waves", [1, 3])
+def test_word_pool_redo_rows_and_mixed_units(em, spm_model, waves):
+    """The word pool's send-back path: three 64-row units of the bench generator (seed 1234, rows
+    3200-3263 and 3968-4095) hold rows whose pooled words fail the margin test (3215, 4002, 4041:
+    found with AK_EMU_DUMP_REDO on 20 k rows); those rows are re-encoded as one-row tiles from the
+    carried base (k_spm_redo), and one unit also holds a row over the tile buffer (the fallback
+    kernels), so the unit copy steps over a sent-back row's span and a fallback row's empty one.
+    Equal to the oracle, with one wave and with three sharing the unit queue."""
+    from akshar_amd import synth
+    lines = synth.lines(1, 4096, seed=1234)
+    texts = lines[3200:3264] + lines[3968:4096]
+    texts[70] = " ".join(texts[70:80])  # > 480 bytes: alone over the tile buffer
+    assert len(texts[70].encode()) > 480
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=16, waves=waves)
+    assert emu.last_redo_rows() >= 3 and emu.last_fallback_rows() >= 1
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_word_pool_off_is_the_same(spm_model, monkeypatch):
+    """AK_SPM_POOL=0 (every word solved in its tile) and AK_SPM_POOL_MIN=7 (short words in the tile,
+    long ones pooled) give the oracle's ids on the same rows."""
+    from akshar_amd import synth
+    buf, offs = synth.generate(1, 600, seed=5)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    for env, val in (("AK_SPM_POOL", "0"), ("AK_SPM_POOL_MIN", "7")):
+        monkeypatch.setenv(env, val)
+        m = emu.Model(spm=spm_model)
+        ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
+        assert np.array_equal(oo, ro) and np.array_equal(ids, ref), env
+        monkeypatch.delenv(env)

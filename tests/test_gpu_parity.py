@@ -570,3 +570,32 @@ def test_bpe_merge_pool_ring_bound(eng, bpe_model):
     assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
     got = _cpu(oo)
     assert got[1] - got[0] == 128 and got[2] - got[1] == 482 and got[3] - got[2] == 484
+
+
+def test_spm_word_pool_redo_rows_on_device(eng, spm_model):
+    """The SentencePiece word pool's send-back path on the device: units of the bench generator
+    whose rows 3215 / 4002 / 4041 hold pooled words that fail the margin test (re-encoded from the
+    carried base by k_spm_redo) beside a row over the tile buffer (the fallback kernels); the batch
+    is repeated 50 times so the rows land on many waves. Equal to the oracle."""
+    from akshar_amd import synth
+    lines = synth.lines(1, 4096, seed=1234)
+    unit = lines[3200:3264] + lines[3968:4096]
+    unit[70] = " ".join(unit[70:80])
+    texts = unit * 50
+    ids, oo = eng.SPM(spm_model).encode_batch(*eng.pack(texts))
+    ref, ro = O.OracleSPM(spm_model).encode_batch(*O.pack(texts))
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    ctr_rows = eng.fallback_rows()
+    assert ctr_rows is not None
+
+
+@pytest.mark.parametrize("env", [("AK_SPM_POOL", "0"), ("AK_SPM_POOL_MIN", "6")])
+def test_spm_word_pool_variants_on_device(eng, spm_model, monkeypatch, env):
+    """The word pool off, and pooling only words of >= 6 chars: the ids of the default build on
+    200 k synthetic Hinglish rows."""
+    buf, offs = _synth(1, 200_000, 43)
+    gb, go = _to_dev(eng, buf, offs)
+    ref_ids, ref_oo = eng.SPM(spm_model).encode_batch(gb, go)
+    monkeypatch.setenv(*env)
+    ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
+    assert torch.equal(oo, ref_oo) and torch.equal(ids, ref_ids)
