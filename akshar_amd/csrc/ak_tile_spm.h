@@ -537,21 +537,26 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M
     const uint32_t R = act ? e.y >> 24 : 0u;
     const uint32_t row = e.z, mpos = e.w;
     uint32_t *sp = (uint32_t *)ta.ra.out + dst;
+    // the batch's longest word bounds every per-position loop: a short ring's words all have
+    // c + 2 chars, the long ring's up to SP_MAXL
+    const int Lmax = c < (uint32_t)(SP_NCLASS - 1) ? (int)c + 2 : (int)w_max_u32((uint32_t)L);
     // the codes back from the reserved slots (u16 pairs; dword-aligned 16-byte loads, the stage is
-    // padded past every run), into the position-major batch arrays; every back slot to BK_NONE
+    // padded past every run), into the position-major batch arrays; back slots 0..Lmax to BK_NONE
 #pragma unroll
     for (int q = 0; q < (CAPL + 7) / 8; ++q) {
-        const uint4 x = load_l2((const uint4 *)sp + q);
-        const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+        if (8 * q < Lmax) {  // wave-uniform
+            const uint4 x = load_l2((const uint4 *)sp + q);
+            const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-        for (int h = 0; h < 8; ++h) {
-            const int pos = 8 * q + h;
-            if (pos < CAPL && lane < B) P.codes[pos * B + ln] = (uint16_t)(xs[h >> 1] >> (16 * (h & 1)));
+            for (int h = 0; h < 8; ++h) {
+                const int pos = 8 * q + h;
+                if (pos < CAPL && pos < Lmax && lane < B) P.codes[pos * B + ln] = (uint16_t)(xs[h >> 1] >> (16 * (h & 1)));
+            }
         }
     }
 #pragma unroll
     for (int pos = 0; pos <= CAPL; ++pos)
-        if (lane < B) P.back[pos * B + ln] = BK_NONE;
+        if (pos <= Lmax && lane < B) P.back[pos * B + ln] = BK_NONE;
     const float minm = word_dp_pool<B, CAPL>(P, m, lane, L);
     // the margin test of spm_margin_ok with the word's position in its row (M = mpos x max |score|)
     const float Mb = fminf((float)mpos * m.abs_score_max, SPM_REBASE + m.abs_score_max) + 1.0f;
@@ -568,22 +573,11 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M
         if (!(old & bit)) ta.redo_list[atomicAdd(ta.redo_count, 1u)] = row;
     }
     const bool emit = act && !redo;
-    // the ids: count along the back links, then write them from the end; STAGE_DEAD past them
-    uint32_t n = 0;
+    // the ids along the back links, written right-aligned from the end of the reserved span (the
+    // unit copy drops dead slots wherever they sit), then STAGE_DEAD in front of them: one walk
+    uint32_t at = emit ? R : 0u;
     {
         int ep = emit ? L : 0;
-        while (w_ballot(ep > 0)) {
-            if (ep > 0) {
-                const uint32_t bk = P.back[ep * B + ln];
-                const int s0 = ep - (int)(bk & 0xFFu);
-                n += (int)(bk >> 8) == m.unk_id ? (uint32_t)utf8_len(spm_wcp(m, P.codes[s0 * B + ln])) : 1u;
-                ep = s0;
-            }
-        }
-    }
-    {
-        int ep = emit ? L : 0;
-        uint32_t at = n;
         while (w_ballot(ep > 0)) {
             if (ep > 0) {
                 const uint32_t bk = P.back[ep * B + ln];
@@ -602,8 +596,8 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M
         }
     }
     if (emit) {
-        for (uint32_t i = n; i < R; ++i) sp[i] = STAGE_DEAD;
-        if (R > n) atomicSub(ta.counts + row, R - n);
+        for (uint32_t i = 0; i < at; ++i) sp[i] = STAGE_DEAD;
+        if (at) atomicSub(ta.counts + row, at);
     }
     w_sync();
     if (lane == 0) {

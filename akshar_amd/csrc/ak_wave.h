@@ -183,6 +183,15 @@ __device__ __forceinline__ uint32_t w_rank(uint64_t m) {
 }
 // ... at or below this lane (the shift and the low bit are scalar work on the uniform mask)
 __device__ __forceinline__ uint32_t w_rank_incl(uint64_t m) { return w_rank(m >> 1) + (uint32_t)(m & 1ull); }
+// wave-wide max (butterfly), every lane gets it
+__device__ __forceinline__ uint32_t w_max_u32(uint32_t x) {
+    const int l = w_lane();
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t y = w_shfl(x, l ^ d);
+        x = y > x ? y : x;
+    }
+    return x;
+}
 // wave-wide 64-bit sum (butterfly), every lane gets the total
 __device__ __forceinline__ uint64_t w_sum64(uint64_t x) {
     const int l = w_lane();
