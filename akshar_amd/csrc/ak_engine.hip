@@ -379,6 +379,8 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     {  // AK_SPM_POOL_MIN: the shortest pooled word (development aid)
         const char *pm = getenv("AK_SPM_POOL_MIN");
         m->dev.pool_min = pm ? (uint32_t)std::max(2, atoi(pm)) : 2u;
+        const char *pr = getenv("AK_SPM_POOL_ROWS");  // the smallest pooled launch (tests force 0)
+        m->dev.pool_rows = pr ? (uint64_t)strtoull(pr, nullptr, 10) : 131072ull;
     }
     // the tile kernel's word cache (ak_swc.h): off unless AK_SWC=1 (measured slower on MI355X: the
     // lattice runs lane per word in rounds of 64, and a tile's words fit one round, so hits do not

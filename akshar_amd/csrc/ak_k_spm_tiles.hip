@@ -219,6 +219,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.fb2_list = w->fb2;
     ta.fb2_count = w->tile_misc + 2;
     ta.next_unit = w->tile_misc + 3;
+    if (a0.n < ta.ra.spm.pool_rows) ta.ra.spm.pool_ok = 0;  // a small launch: every word in its tile
     ta.redo_list = w->redo;
     ta.redo_count = w->tile_misc + 4;
     ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;

@@ -109,6 +109,7 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     {  // AK_SPM_POOL_MIN: the shortest pooled word (development aid)
         const char *pm = getenv("AK_SPM_POOL_MIN");
         m->sdev.pool_min = pm ? (uint32_t)std::max(2, atoi(pm)) : 2u;
+        m->sdev.pool_rows = 0;  // the emulated batches are small: always pooled (as AK_SPM_POOL_ROWS=0)
     }
     }
     m->piece_bytes.assign(bytes, bytes + offs[n]);

@@ -572,7 +572,7 @@ def test_bpe_merge_pool_ring_bound(eng, bpe_model):
     assert got[1] - got[0] == 128 and got[2] - got[1] == 482 and got[3] - got[2] == 484
 
 
-def test_spm_word_pool_redo_rows_on_device(eng, spm_model):
+def test_spm_word_pool_redo_rows_on_device(eng, spm_model, monkeypatch):
     """The SentencePiece word pool's send-back path on the device: units of the bench generator
     whose rows 3215 / 4002 / 4041 hold pooled words that fail the margin test (re-encoded from the
     carried base by k_spm_redo) beside a row over the tile buffer (the fallback kernels); the batch
@@ -582,11 +582,19 @@ def test_spm_word_pool_redo_rows_on_device(eng, spm_model):
     unit = lines[3200:3264] + lines[3968:4096]
     unit[70] = " ".join(unit[70:80])
     texts = unit * 50
+    monkeypatch.setenv("AK_SPM_POOL_ROWS", "0")  # pooled at this size too
     ids, oo = eng.SPM(spm_model).encode_batch(*eng.pack(texts))
     ref, ro = O.OracleSPM(spm_model).encode_batch(*O.pack(texts))
     assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
-    ctr_rows = eng.fallback_rows()
-    assert ctr_rows is not None
+
+
+def test_spm_golden_pooled(golden, gpacked, eng, spm_model, monkeypatch):
+    """Every golden row (corpus, adversarial, fuzz, long rows) with the word pool forced on for this
+    small batch (AK_SPM_POOL_ROWS=0; by default launches under 131,072 rows keep every word in its
+    tile)."""
+    monkeypatch.setenv("AK_SPM_POOL_ROWS", "0")
+    ids, oo = eng.SPM(spm_model).encode_batch(*gpacked)
+    assert _bad(golden, "spm", rows_ints(_cpu(ids), _cpu(oo))) == []
 
 
 @pytest.mark.parametrize("env", [("AK_SPM_POOL", "0"), ("AK_SPM_POOL_MIN", "6")])
