@@ -811,7 +811,6 @@ struct SpmDev {
     const uint32_t *wc;    // tile path: the word cache (ak_swc.h; null = off)
     uint32_t wc_mask;
     uint32_t pool_ok;      // tile path: the word pool may take words (ak_tile_spm.h spm_pool_ok)
-    uint32_t pool_min;     // ... of at least this many chars ("▁" included; shorter ones stay in the tile)
     uint64_t pool_rows;    // ... in launches of at least this many rows (below, each wave has too few tiles
                            // to fill batches: the rings' partial batches at its end cost more than they save)
 };

@@ -376,9 +376,7 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
     // the tile path's word pool (ak_tile_spm.h): AK_SPM_POOL=0 leaves it off (development aid, A/B)
     const char *pe = getenv("AK_SPM_POOL");
     m->dev.pool_ok = spm_pool_allowed(t.single_all, t.abs_score_max) && !(pe && pe[0] == '0') ? 1u : 0u;
-    {  // AK_SPM_POOL_MIN: the shortest pooled word (development aid)
-        const char *pm = getenv("AK_SPM_POOL_MIN");
-        m->dev.pool_min = pm ? (uint32_t)std::max(2, atoi(pm)) : 2u;
+    {
         const char *pr = getenv("AK_SPM_POOL_ROWS");  // the smallest pooled launch (tests force 0)
         m->dev.pool_rows = pr ? (uint64_t)strtoull(pr, nullptr, 10) : 131072ull;
     }

@@ -13,6 +13,8 @@
 //                    pool left (ak_tile_spm.h spm_pool_flush); fallback rows from their slots
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "ak_internal.h"
 #include "ak_tile_spm.h"
 
@@ -25,11 +27,13 @@ constexpr int SPM_TILE_BLOCK = AK_SPM_TILE_BLOCK;  // 4 waves per block
 constexpr uint32_t SPM_T_MUL = 2, SPM_T_ADD = 2;  // staging slot of row r: 2 offs[r] + 2 r
 constexpr int SPM_FB_BLOCK = 64;
 
-template <int FLAGS>
+// POOLED: the word-pool variant (every word to the pool, bigger tiles: ak_tile_spm.h SpmWaveMemP)
+template <int FLAGS, bool POOLED>
 __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
+    using MemT = typename std::conditional<POOLED, SpmWaveMemP, SpmWaveMem>::type;
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
-    __shared__ SpmWaveMem wm[SPM_TILE_BLOCK / 64];
+    __shared__ MemT wm[SPM_TILE_BLOCK / 64];
     for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
         const uint32_t cp = hot_cp(i);
         hot_tab[i] = hot_word(cp);
@@ -38,8 +42,8 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     }
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
-    spm_tiles_wave<FLAGS>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
-                          gridDim.x * (SPM_TILE_BLOCK / 64));
+    spm_tiles_wave<FLAGS, MemT>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
+                                gridDim.x * (SPM_TILE_BLOCK / 64));
 }
 
 // rows the word pool sent back (ak_tile_spm.h spm_redo_wave): wave per row, same LDS as k_spm_tiles
@@ -190,7 +194,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     }
     if (!g_spm_blocks_per_cu.load(std::memory_order_relaxed)) {
         int b = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spm_tiles<3>, SPM_TILE_BLOCK, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spm_tiles<3, false>, SPM_TILE_BLOCK, 0));
         g_spm_blocks_per_cu.store(std::max(1, b), std::memory_order_relaxed);
     }
     if (w->cap_fb2 < a0.n) {
@@ -246,7 +250,8 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.unit_len = w->unit_len;
     ta.row_span = w->row_span;
     AK_PROF(AK_PROF_SPM_TILES, false, st);
-    k_spm_tiles<3><<<grid, SPM_TILE_BLOCK, 0, st>>>(ta);
+    if (ta.ra.spm.pool_ok) k_spm_tiles<3, true><<<grid, SPM_TILE_BLOCK, 0, st>>>(ta);
+    else k_spm_tiles<3, false><<<grid, SPM_TILE_BLOCK, 0, st>>>(ta);
     AK_PROF(AK_PROF_SPM_TILES, true, st);
     HIP_TRY(hipGetLastError());
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);

@@ -71,6 +71,9 @@ __device__ __forceinline__ uint32_t sp_batch(uint32_t c) { return c == (uint32_t
 constexpr int sp_lds_bytes(int B, int CAPL) { return CAPL * B * 2 + 2 * (CAPL + 1) * B * 4; }
 
 struct SpmWaveMem {
+    static constexpr int BC = S_BCAP;        // staged bytes per tile
+    static constexpr int WN = S_W;           // entries of W
+    static constexpr bool PL = false;        // the tile solves its words (best / back below)
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
     uint16_t v[S_E];                         // V; after pass W: nxt (u8 per W position)
     uint16_t w[S_W];                         // P (pass D1), then W
@@ -98,6 +101,57 @@ static_assert(offsetof(SpmWaveMem, passacc) >= sp_lds_bytes(64, SP_SHORT) &&
               "a pool batch fits the tile buffers");
 static_assert(S_WORDS * 2 <= S_BCAP + 32, "word starts live in the byte buffer");
 static_assert(S_W + 2 * S_WORDS <= 2 * S_E, "nxt + word id counts live in V");
+
+// The pooled variant (launches of >= pool_rows rows with the word pool on): every word of a row goes
+// to the pool, so the tile holds no lattice arrays and stages bigger tiles in the same LDS (the
+// pool batch area). A row with a word the pool does not take (over SP_MAXL chars) goes to
+// k_spm_redo, which solves it in the tile variant above.
+#ifndef AK_SP_BCAP
+#define AK_SP_BCAP 768
+#endif
+constexpr int SP_BCAP = AK_SP_BCAP;
+constexpr int SP_E = SP_BCAP + 2 * T_MAXR + 64;
+constexpr int SP_W = SP_E + T_MAXR + 16;
+constexpr int sp_batch_area() { return sp_lds_bytes(64, SP_SHORT) > sp_lds_bytes(32, SP_MAXL) ? sp_lds_bytes(64, SP_SHORT) : sp_lds_bytes(32, SP_MAXL); }
+struct SpmTileP {  // the per-tile part of SpmWaveMemP
+    alignas(16) uint8_t bytes[SP_BCAP + 32];
+    uint16_t v[SP_E];
+    uint16_t w[SP_W];
+    uint8_t wrow[S_WORDS];
+    uint8_t wpool[S_WORDS];
+    uint8_t fb[T_MAXR];
+    uint16_t rowend[T_MAXR];
+    uint16_t rowpos[T_MAXR + 1];
+    uint16_t wfirst[T_MAXR + 1];
+    uint32_t rowcnt[T_MAXR];
+    uint32_t rowfirst[T_MAXR];
+};
+struct SpmWaveMemP {
+    static constexpr int BC = SP_BCAP;
+    static constexpr int WN = SP_W;
+    static constexpr bool PL = true;
+    alignas(16) uint8_t bytes[SP_BCAP + 32];
+    uint16_t v[SP_E];
+    uint16_t w[SP_W];
+    uint8_t wrow[S_WORDS];
+    uint8_t wpool[S_WORDS];
+    uint8_t fb[T_MAXR];                      // 1: the fallback kernels; 2: k_spm_redo (a word the pool does not take)
+    uint16_t rowend[T_MAXR];
+    uint16_t rowpos[T_MAXR + 1];
+    uint16_t wfirst[T_MAXR + 1];
+    uint32_t rowcnt[T_MAXR];
+    uint32_t rowfirst[T_MAXR];
+    uint8_t pad[offsetof(SpmTileP, rowfirst) + 4 * T_MAXR < (size_t)sp_batch_area()
+                    ? sp_batch_area() - (offsetof(SpmTileP, rowfirst) + 4 * T_MAXR) : 8];
+    // ---- kept across tiles
+    uint64_t passacc[T_NPROF];
+    uint64_t unext;
+    uint64_t ufbm;
+    uint32_t phead[SP_NCLASS];
+    uint32_t pcnt[SP_NCLASS];
+};
+static_assert(offsetof(SpmWaveMemP, passacc) >= (size_t)sp_batch_area(), "a pool batch fits the tile buffers");
+static_assert(S_WORDS * 2 <= SP_BCAP + 32 && SP_W + 2 * S_WORDS <= 2 * SP_E, "word starts / counts fit");
 
 // W entry of a normalized char: LDS code table for the hot range, the model's paged map otherwise
 __device__ __forceinline__ uint16_t spm_wcode(const SpmDev &m, const uint16_t *scode, uint32_t cp) {
@@ -430,7 +484,8 @@ struct SpBatch {
     uint16_t *codes;  // [CAPL][B]
     float *best;      // [CAPL + 1][B]
     uint32_t *back;   // [CAPL + 1][B]
-    __device__ __forceinline__ SpBatch(SpmWaveMem &M) {
+    template <class MemT>
+    __device__ __forceinline__ SpBatch(MemT &M) {
         uint8_t *b = (uint8_t *)&M;
         codes = (uint16_t *)b;
         best = (float *)(b + CAPL * B * 2);
@@ -518,8 +573,8 @@ __device__ __forceinline__ uint32_t utf8_bytes_of(uint32_t cp, uint32_t bytes[4]
 }
 
 // One batch of ring c: its first cnt (<= B) entries, lane l the l-th.
-template <int B, int CAPL>
-__device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M, uint4 *pool, uint32_t c, uint32_t cnt,
+template <int B, int CAPL, class MemT>
+__device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint4 *pool, uint32_t c, uint32_t cnt,
                                             PassClock &pc) {
     const SpmDev &m = ta.ra.spm;
     const int lane = w_lane();
@@ -608,28 +663,31 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, SpmWaveMem &M
 }
 
 // every ring holding a full batch (minc = 1 at the wave's end: every word), a batch at a time
-__device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, SpmWaveMem &M, uint4 *pool, bool all, PassClock &pc) {
+template <class MemT>
+__device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, MemT &M, uint4 *pool, bool all, PassClock &pc) {
 #pragma unroll 1
     for (uint32_t c = 0; c < (uint32_t)SP_NCLASS; ++c) {
         const uint32_t bw = sp_batch(c);
         for (;;) {
             const uint32_t k = w_bcast(M.pcnt[c], 0);
             if (k == 0 || (!all && k < bw)) break;
-            if (c == (uint32_t)(SP_NCLASS - 1)) spm_pool_flush<32, SP_MAXL>(ta, M, pool, c, k < bw ? k : bw, pc);
-            else spm_pool_flush<64, SP_SHORT>(ta, M, pool, c, k < bw ? k : bw, pc);
+            if (c == (uint32_t)(SP_NCLASS - 1)) spm_pool_flush<32, SP_MAXL, MemT>(ta, M, pool, c, k < bw ? k : bw, pc);
+            else spm_pool_flush<64, SP_SHORT, MemT>(ta, M, pool, c, k < bw ? k : bw, pc);
         }
     }
 }
 
-template <int FLAGS>
+template <int FLAGS, class MemT>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
-                        SpmWaveMem &M, uint4 *pool, PassClock &pc, bool redo_mode = false) {
+                        MemT &M, uint4 *pool, PassClock &pc, bool redo_mode = false) {
+    constexpr int BCAP = MemT::BC, WN = MemT::WN;
+    constexpr bool PL = MemT::PL;
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
     const SpmDev &m = a.spm;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<S_BCAP>(a, r0, rend, H, M);
+    const TileRows tr = tile_front<BCAP>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
     pc.mark(TP_D);
@@ -684,11 +742,15 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             if (KM) carry = (uint16_t)w_bcast((uint32_t)x, msb64(KM));
         }
         if (lane == 0) { M.rowpos[rs] = (uint16_t)wlen; M.wfirst[rs] = (uint16_t)nw; }
-        if (nw > (uint32_t)S_WORDS || wlen > (uint32_t)S_W) {  // never in text: the tile's rows fall back
+        if (nw > (uint32_t)S_WORDS || wlen > (uint32_t)WN) {  // never in text: the tile's rows fall back
             if (lane < nr) M.fb[lane] = 1;
             nw = 0;
         }
-        if (lane < nr) { M.rowcnt[lane] = 0; M.rowfirst[lane] = 0; M.mfail[lane] = 0; }
+        if (lane < nr) {
+            M.rowcnt[lane] = 0;
+            M.rowfirst[lane] = 0;
+            if constexpr (!PL) M.mfail[lane] = 0;
+        }
     }
     w_sync();
     pc.mark(TP_E);
@@ -697,9 +759,11 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     // pieces and applies the margin test to its stored margin; the words it misses are listed and
     // then solved 64 at a time, lane per word, by the Viterbi from base 0 with the running margin
     // (word_dp_flat). A row with a close call is redone exactly below (pass V2).
-    uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + S_W);
-    for (uint32_t i = (uint32_t)lane; i < wlen; i += 64) M.back[i] = BK_NONE;  // word_dp_flat's entry state
-    w_sync();
+    uint16_t *wcnt = (uint16_t *)((uint8_t *)M.v + WN);
+    if constexpr (!PL) {
+        for (uint32_t i = (uint32_t)lane; i < wlen; i += 64) M.back[i] = BK_NONE;  // word_dp_flat's entry state
+        w_sync();
+    }
     uint32_t nmiss = 0;
     for (uint32_t jb = 0; jb < nw; jb += 64) {
         const uint32_t j = jb + (uint32_t)lane;
@@ -708,7 +772,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const int p0 = act ? (int)starts[j] : 0;
         const int p1 = act ? ((j + 1 < nw && (int)wrow[j + 1] == row) ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
         bool hit = false;
-        if (m.wc) {
+        if constexpr (!PL) if (m.wc) {
             const int n = p1 - p0;
             bool cand = act && n >= 2 && n <= aks::SWC_MAXN;
             uint32_t q[8];
@@ -748,7 +812,10 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         // a miss of 2..SP_MAXL chars in a row not sent to the fallback kernels waits in the word
         // pool (pass F reserves its slots); the rest are solved here
         const int L = p1 - p0;
-        const bool pooled = act && !hit && m.pool_ok && !redo_mode && L >= (int)m.pool_min && L <= SP_MAXL && !M.fb[row];
+        const bool pooled = PL && act && !hit && L >= 2 && L <= SP_MAXL && !M.fb[row];
+        if constexpr (PL) {  // a word the pool does not take: its row goes to k_spm_redo
+            if (act && !pooled && !M.fb[row]) M.fb[row] = 2;
+        }
         if (act) M.wpool[j] = pooled ? 1 : 0;
         if (pooled) {  // its id bound: one per char some piece holds, UTF-8 bytes for the others
             uint32_t R = 0;
@@ -758,13 +825,16 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             }
             wcnt[j] = (uint16_t)R;
         }
-        const bool miss = act && !hit && !pooled;
-        const uint64_t MM = w_ballot(miss);
-        if (miss) M.wmiss[nmiss + w_rank(MM)] = (uint8_t)j;
-        nmiss += (uint32_t)w_popc(MM);
+        if constexpr (!PL) {
+            const bool miss = act && !hit && !pooled;
+            const uint64_t MM = w_ballot(miss);
+            if (miss) M.wmiss[nmiss + w_rank(MM)] = (uint8_t)j;
+            nmiss += (uint32_t)w_popc(MM);
+        }
     }
     w_sync();
     pc.mark(TP_C);
+    if constexpr (!PL) {
     for (uint32_t ib = 0; ib < nmiss; ib += 64) {
         const uint32_t i = ib + (uint32_t)lane;
         const bool act = i < nmiss;
@@ -806,6 +876,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
             w_sync();
         }
     }
+    }  // !PL
     pc.mark(TP_B);
 
     // ---------------- fallback rows: append to the list (rare: one atomic per tile that has any)
@@ -814,10 +885,18 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         const uint64_t FM = w_ballot(isfb);
         if (lane == 0) M.ufbm |= FM << (r0 % TILE_UNIT);  // tiles never straddle a unit
         if (FM) {
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(ta.fb_count, (uint32_t)w_popc(FM));
+            // fb 1: the fallback kernels; fb 2 (pooled variant): a word the pool does not take, k_spm_redo
+            const bool tofb = isfb && M.fb[lane] == 1;
+            const uint64_t F1 = w_ballot(tofb), F2 = FM & ~F1;
+            uint32_t base = 0, base2 = 0;
+            if (lane == 0) {
+                if (F1) base = atomicAdd(ta.fb_count, (uint32_t)w_popc(F1));
+                if (F2) base2 = atomicAdd(ta.redo_count, (uint32_t)w_popc(F2));
+            }
             base = w_bcast(base, 0);
-            if (isfb) ta.fb_list[base + w_rank(FM)] = (uint32_t)(r0 + (uint64_t)lane);
+            base2 = w_bcast(base2, 0);
+            if (tofb) ta.fb_list[base + w_rank(F1)] = (uint32_t)(r0 + (uint64_t)lane);
+            else if (isfb) ta.redo_list[base2 + w_rank(F2)] = (uint32_t)(r0 + (uint64_t)lane);
         }
     }
     pc.mark(TP_FBC);
@@ -870,7 +949,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                 CMs &= ~CM;
             }
         }
-        if (live && !pooled) {
+        if constexpr (!PL) if (live && !pooled) {
             uint64_t d = P;
             for (int s = p0; s < p1;) {
                 const int e = s + (int)nxt[s];
@@ -909,21 +988,23 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     }
     w_sync();
     pc.mark(TP_F);
-    spm_pool_drain(ta, M, pool, false, pc);  // full batches (the tile's buffers are free now)
+    if constexpr (PL) spm_pool_drain(ta, M, pool, false, pc);  // full batches (the tile's buffers are free now)
     pc.mark(TP_FBE);
     return nr;
 }
 
-template <int FLAGS>
-__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M, uint32_t wave_gid, uint32_t nwaves) {
+template <int FLAGS, class MemT>
+__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, MemT &M, uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
     uint4 *pool = ta.pool + (uint64_t)wave_gid * SP_CAP;  // this wave's rings
-    if (w_lane() < SP_NCLASS) {
-        M.phead[w_lane()] = 0;
-        M.pcnt[w_lane()] = 0;
+    if constexpr (MemT::PL) {
+        if (w_lane() < SP_NCLASS) {
+            M.phead[w_lane()] = 0;
+            M.pcnt[w_lane()] = 0;
+        }
+        w_sync();
     }
-    w_sync();
     // units of TILE_UNIT rows from the work queue (tile_first_unit); inside a unit, each tile
     // takes up to ta.rows rows, as many as fit its byte buffer (greedy packing)
     for (uint64_t t = tile_first_unit(ta.next_unit, wave_gid); t < ta.ntiles; t = tile_next_unit(ta.next_unit, t, nwaves)) {
@@ -937,14 +1018,14 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
         }
         w_sync();
         for (uint64_t r = r0; r < r1;)
-            r += (uint64_t)spm_tile<FLAGS>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, M, pool, pc);
+            r += (uint64_t)spm_tile<FLAGS, MemT>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, M, pool, pc);
         if (w_lane() == 0) {
             // OR: a pooled word of this unit may already have sent a row to the fallback kernels
             if (M.ufbm) atomicOr((unsigned long long *)(ta.unit_fb + t), (unsigned long long)M.ufbm);
             ta.unit_len[t] = (uint32_t)(M.unext - run0);
         }
     }
-    spm_pool_drain(ta, M, pool, true, pc);  // the rest: every pooled word solved before the wave leaves
+    if constexpr (MemT::PL) spm_pool_drain(ta, M, pool, true, pc);  // the rest: every pooled word solved before the wave leaves
     pc.mark(TP_FBE);
     pc.flush(ta.passprof);
 }
@@ -972,7 +1053,7 @@ __device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint1
             M.ufbm = 0;
         }
         w_sync();
-        (void)spm_tile<FLAGS>(ta, r, r + 1, H, scode, M, nullptr, pc, true);
+        (void)spm_tile<FLAGS, SpmWaveMem>(ta, r, r + 1, H, scode, M, nullptr, pc, true);
     }
 }
 

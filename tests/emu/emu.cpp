@@ -106,9 +106,7 @@ extern "C" void *emu_spm_create(uint32_t n, const uint8_t *bytes, const uint64_t
     {
         const char *pe = getenv("AK_SPM_POOL");
         m->sdev.pool_ok = spm_pool_allowed(m->spm.single_all, m->spm.abs_score_max) && !(pe && pe[0] == '0') ? 1u : 0u;
-    {  // AK_SPM_POOL_MIN: the shortest pooled word (development aid)
-        const char *pm = getenv("AK_SPM_POOL_MIN");
-        m->sdev.pool_min = pm ? (uint32_t)std::max(2, atoi(pm)) : 2u;
+    {
         m->sdev.pool_rows = 0;  // the emulated batches are small: always pooled (as AK_SPM_POOL_ROWS=0)
     }
     }
@@ -396,7 +394,12 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     ta.redo_list = redo.data();
     ta.redo_count = &nredo;
     std::vector<SpmWaveMem> M(g_waves);
-    run_waves([&](int w) { spm_tiles_wave<3>(ta, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
+    if (m->sdev.pool_ok) {  // as the launcher: the pooled variant when the pool is on
+        std::vector<SpmWaveMemP> MP(g_waves);
+        run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMemP>(ta, hot_tab, scode, MP[w], (uint32_t)w, (uint32_t)g_waves); });
+    } else {
+        run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMem>(ta, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
+    }
     g_last_redo = nredo;
     if (getenv("AK_EMU_DUMP_REDO")) { for (uint32_t i = 0; i < nredo; ++i) fprintf(stderr, "redo row %u\n", redo[i]); }
     {  // as k_spm_redo: the rows the word pool sent back, into their fallback slots

@@ -142,14 +142,19 @@ def test_word_pool_redo_rows_and_mixed_units(em, spm_model, waves):
 
 
 def test_word_pool_off_is_the_same(spm_model, monkeypatch):
-    """AK_SPM_POOL=0 (every word solved in its tile) and AK_SPM_POOL_MIN=7 (short words in the tile,
-    long ones pooled) give the oracle's ids on the same rows."""
+    """AK_SPM_POOL=0 (the tile variant: every word solved in its tile) gives the oracle's ids on the
+    same rows, as the pooled variant (the default here) does; a word over SP_MAXL = 24 chars sends
+    its row to the redo pass in the pooled variant."""
     from akshar_amd import synth
-    buf, offs = synth.generate(1, 600, seed=5)
+    texts = synth.lines(1, 600, seed=5)
+    texts[3] = texts[3] + " " + "क" * 30 + " end"  # a 31-char word: not pooled
+    buf, offs = O.pack(texts)
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
-    for env, val in (("AK_SPM_POOL", "0"), ("AK_SPM_POOL_MIN", "7")):
-        monkeypatch.setenv(env, val)
-        m = emu.Model(spm=spm_model)
-        ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
-        assert np.array_equal(oo, ro) and np.array_equal(ids, ref), env
-        monkeypatch.delenv(env)
+    m = emu.Model(spm=spm_model)
+    ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    assert emu.last_redo_rows() >= 1
+    monkeypatch.setenv("AK_SPM_POOL", "0")
+    m = emu.Model(spm=spm_model)
+    ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)

@@ -597,13 +597,20 @@ def test_spm_golden_pooled(golden, gpacked, eng, spm_model, monkeypatch):
     assert _bad(golden, "spm", rows_ints(_cpu(ids), _cpu(oo))) == []
 
 
-@pytest.mark.parametrize("env", [("AK_SPM_POOL", "0"), ("AK_SPM_POOL_MIN", "6")])
-def test_spm_word_pool_variants_on_device(eng, spm_model, monkeypatch, env):
-    """The word pool off, and pooling only words of >= 6 chars: the ids of the default build on
-    200 k synthetic Hinglish rows."""
-    buf, offs = _synth(1, 200_000, 43)
-    gb, go = _to_dev(eng, buf, offs)
+def test_spm_word_pool_variants_on_device(eng, spm_model, monkeypatch):
+    """The tile variant (AK_SPM_POOL=0: every word solved in its tile) gives the pooled variant's ids
+    (the default at this size) on 200 k synthetic Hinglish rows, some holding words over the pool's
+    24 chars (their rows go to k_spm_redo)."""
+    from akshar_amd import synth
+    texts = synth.lines(1, 200_000, seed=43)
+    for i in range(0, len(texts), 997):
+        texts[i] = texts[i] + " " + "क" * (25 + i % 9) + " x"
+    gb, go = eng.pack(texts)
     ref_ids, ref_oo = eng.SPM(spm_model).encode_batch(gb, go)
-    monkeypatch.setenv(*env)
+    monkeypatch.setenv("AK_SPM_POOL", "0")
     ids, oo = eng.SPM(spm_model).encode_batch(gb, go)
     assert torch.equal(oo, ref_oo) and torch.equal(ids, ref_ids)
+    n = 3000
+    ref, ro = O.OracleSPM(spm_model).encode_batch(*O.pack(texts[:n]))
+    o = _cpu(oo)[:n + 1]
+    assert np.array_equal(o.astype(np.uint64), ro) and np.array_equal(_cpu(ids)[:o[-1]].astype(np.uint32), ref)
