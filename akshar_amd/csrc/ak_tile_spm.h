@@ -107,7 +107,7 @@ static_assert(S_W + 2 * S_WORDS <= 2 * S_E, "nxt + word id counts live in V");
 // pool batch area). A row with a word the pool does not take (over SP_MAXL chars) goes to
 // k_spm_redo, which solves it in the tile variant above.
 #ifndef AK_SP_BCAP
-#define AK_SP_BCAP 768
+#define AK_SP_BCAP 1024
 #endif
 constexpr int SP_BCAP = AK_SP_BCAP;
 constexpr int SP_E = SP_BCAP + 2 * T_MAXR + 64;
