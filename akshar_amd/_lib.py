@@ -76,6 +76,7 @@ SIGNATURES = {
     "ak_bpe_cache_info": (I32, [P, ctypes.POINTER(U64)]),
     "ak_spm_cache_info": (I32, [P, ctypes.POINTER(U64)]),
     "ak_ws_fallback_rows": (I32, [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+    "ak_ws_fallback_detail": (I32, [P, P]),
     "ak_normalize_cap": (U64, [U64, U64]),
     "ak_segment_cap": (U64, [U64, U64]),
     "ak_bpe_encode_cap": (U64, [U64, U64]),

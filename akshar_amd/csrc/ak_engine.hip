@@ -501,6 +501,23 @@ extern "C" int ak_ws_check(ak_ws *w) {
 namespace ak { int selftest_wave(); }
 extern "C" int ak_selftest(void) { return ak::selftest_wave(); }
 
+extern "C" int ak_ws_fallback_detail(ak_ws *w, uint64_t detail[4]) {
+    if (!w || !detail) return fail(AK_ERR_ARG, "ak_ws_fallback_detail: null argument");
+    for (int i = 0; i < 4; ++i) detail[i] = 0;
+    if (!w->tile_misc) return AK_OK;
+    uint32_t h[8] = {};
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(h, w->tile_misc, sizeof(h), hipMemcpyDeviceToHost));
+    // tile_misc: [0] fallback list, [2] slow tier, [4] SPM send-backs, [5] BPE rows k_bpe_nfc passed on
+    // ([6]: 1 when the last launch was SPM, which leaves [5] alone)
+    const bool spm = h[6] != 0;
+    detail[0] = spm ? (uint64_t)h[0] + h[4] : h[0];
+    detail[1] = spm ? h[4] : h[0] - std::min(h[0], h[5]);
+    detail[2] = spm ? h[0] : std::min(h[0], h[5]);
+    detail[3] = h[2];
+    return AK_OK;
+}
+
 extern "C" int ak_ws_fallback_rows(ak_ws *w, uint64_t *rows, uint64_t *pool_rows) {
     if (!w || !rows || !pool_rows) return fail(AK_ERR_ARG, "ak_ws_fallback_rows: null argument");
     *rows = 0;
@@ -547,6 +564,9 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->bpool);
     (void)hipFree(w->row_span);
     (void)hipFree(w->redo);
+    (void)hipFree(w->fb3);
+    (void)hipFree(w->nfc_buf);
+    (void)hipFree(w->nfc_aux);
     (void)hipFree(w->counts);
     (void)hipFree(w->slow_list);
     (void)hipFree(w->huge_list);

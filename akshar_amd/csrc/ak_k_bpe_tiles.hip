@@ -1,7 +1,9 @@
 // ak_k_bpe_tiles.hip — the tile-cooperative BPE encode (ak_tile.h) and its launcher:
 //   k_bpe_tiles      every wave encodes whole tiles of R rows into per-row staging slots and
 //                    writes per-row token counts; rare rows go to a fallback list
-//   k_tile_fb        fallback rows, one lane per row (ak_rows.h process_row, small private
+//   k_bpe_nfc        fallback rows, wave per row: NFC of the row (ak_nfc_wave.h), then the tile
+//                    pipeline over the NFC text with the NFC proof bypassed, into the row's slot
+//   k_tile_fb        the rows k_bpe_nfc could not take, one lane per row (ak_rows.h process_row, small private
 //                    buffers), straight into the same slots; rows that overflow those buffers go on
 //   k_rows_tier      ... to the slow tier (per-thread pool regions) and, past those, the huge
 //                    tier sized from the longest such row (ak_internal.h)
@@ -12,6 +14,7 @@
 #include <stdlib.h>
 
 #include "ak_internal.h"
+#include "ak_nfc_wave.h"
 #include "ak_tile.h"
 
 namespace ak {
@@ -41,6 +44,34 @@ __global__ __launch_bounds__(TILE_BLOCK, AK_BPE_TILE_WPE) void k_bpe_tiles(TileA
     const uint32_t wave = threadIdx.x >> 6;
     bpe_tiles_wave<FLAGS>(ta, hot_tab, sfast, wm[wave], blockIdx.x * (TILE_BLOCK / 64) + wave,
                           gridDim.x * (TILE_BLOCK / 64));
+}
+
+// The tile kernel's fallback rows, a wave per row (ak_nfc_wave.h): the row's NFC into the wave's
+// byte slot, then bpe_tile<NFCD> over that text as a one-row tile writing into the row's fallback
+// slot (ta.ra.out is the second staging half); its merge-pool misses go to the wave's own rings,
+// which leave STAGE_DEAD entries in the slot: after the wave's last batch each slot is compacted in
+// place (the copy takes a fallback row's count entries as they are). A row this cannot take
+// (invalid UTF-8, over NW_MAXB bytes, a segment past NW_DCAP, or a fallback again in the tile: HF's
+// NFKC changes the text) goes on to k_tile_fb through the second list (fb3).
+constexpr int NFC_BLOCK = 256;
+
+template <int FLAGS>
+__global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *nbuf, uint64_t *pairs, uint32_t *runlen,
+                                                      uint32_t *fb3, uint32_t *fb3_count) {
+    __shared__ uint32_t hot_tab[HOT_N];
+    __shared__ uint16_t sfast[SFAST_N];
+    __shared__ uint2 fast[FAST_N];
+    __shared__ TileWaveMem wm[NFC_BLOCK / 64];
+    __shared__ NfcWaveMem nm[NFC_BLOCK / 64];
+    const uint32_t nl = *ta.fb_count;
+    if (nl == 0) return;  // uniform: the common case
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += NFC_BLOCK) hot_tab[i] = hot_word(hot_cp(i));
+    for (uint32_t i = threadIdx.x; i < SFAST_N; i += NFC_BLOCK)
+        sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
+    stage_tables(fast, nullptr, nullptr, false);  // (syncs the block)
+    const uint32_t wave = threadIdx.x >> 6;
+    bpe_nfc_wave<FLAGS>(ta, nbuf, pairs, runlen, fb3, fb3_count, hot_tab, sfast, fast, wm[wave], nm[wave],
+                        blockIdx.x * (NFC_BLOCK / 64) + wave, gridDim.x * (NFC_BLOCK / 64));
 }
 
 // fallback rows, fast buffers (the row kernel's sizes); writes ids at the row's slot. Rows that
@@ -428,8 +459,15 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
         w->cap_fb2 = a0.n;
     }
     ta.fb2_list = w->fb2;
+    if (w->cap_fb3 < a0.n) {
+        (void)hipFree(w->fb3);
+        w->fb3 = nullptr;
+        HIP_TRY(hipMalloc(&w->fb3, a0.n * 4));
+        w->cap_fb3 = a0.n;
+    }
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
     HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4 * 4, st));
+    HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 2 * 4, st));  // k_bpe_nfc's pass-on count; [6]: a BPE launch
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit
@@ -458,6 +496,32 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
+    if (!getenv("AK_NO_NFC_WAVE")) {  // (development aid: the one-lane path for every fallback row)
+        const unsigned ngrid = (unsigned)num_cus();
+        const uint64_t nw = (uint64_t)ngrid * (NFC_BLOCK / 64);
+        if (w->cap_nfc < nw) {
+            (void)hipFree(w->nfc_buf);
+            w->nfc_buf = nullptr;
+            w->cap_nfc = 0;
+            HIP_TRY(hipMalloc(&w->nfc_buf, nw * (NFC_SLOT + 16) + 64));
+            w->cap_nfc = nw;
+        }
+        if (w->cap_nfc_aux < a0.n) {
+            (void)hipFree(w->nfc_aux);
+            w->nfc_aux = nullptr;
+            w->cap_nfc_aux = 0;
+            HIP_TRY(hipMalloc(&w->nfc_aux, (a0.n + 1) * 4));
+            w->cap_nfc_aux = a0.n;
+        }
+        HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
+        uint64_t *pairs = (uint64_t *)(w->nfc_buf + nw * NFC_SLOT);
+        k_bpe_nfc<3><<<ngrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, pairs, w->nfc_aux, w->fb3, w->tile_misc + 5);
+        HIP_TRY(hipGetLastError());
+        tfb.fb_list = w->fb3;
+        tfb.fb_count = w->tile_misc + 5;
+    } else {  // every fallback row goes on (ak_ws_fallback_detail)
+        HIP_TRY(hipMemcpyAsync(w->tile_misc + 5, w->tile_misc, 4, hipMemcpyDeviceToDevice, st));
+    }
     static std::atomic<int> fb_bpc{0};
     k_tile_fb<3><<<resident_grid(k_tile_fb<3>, FB_BLOCK, fb_bpc), FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;

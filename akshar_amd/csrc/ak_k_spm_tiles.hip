@@ -223,7 +223,8 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.fb2_list = w->fb2;
     ta.fb2_count = w->tile_misc + 2;
     ta.next_unit = w->tile_misc + 3;
-    if (a0.n < ta.ra.spm.pool_rows) ta.ra.spm.pool_ok = 0;  // a small launch: every word in its tile
+    // a small launch keeps every word in its tile; so does the opt-in word cache (AK_SWC, tile variant)
+    if (a0.n < ta.ra.spm.pool_rows || ta.ra.spm.wc) ta.ra.spm.pool_ok = 0;
     ta.redo_list = w->redo;
     ta.redo_count = w->tile_misc + 4;
     ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
@@ -232,6 +233,10 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count, the
     // unit queue, the word pool's redo count
     HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 5 * 4, st));
+    {  // [6]: this launch is SentencePiece (ak_ws_fallback_detail)
+        static const uint32_t one = 1;
+        HIP_TRY(hipMemcpyAsync(w->tile_misc + 6, &one, 4, hipMemcpyHostToDevice, st));
+    }
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = SPM_TILE_BLOCK / 64;
     int bpc = g_spm_blocks_per_cu.load(std::memory_order_relaxed);

@@ -310,6 +310,16 @@ __device__ __forceinline__ uint32_t decode_word(uint32_t x, int p, int e) {
     return ok ? cp : 0xFFFFFFFFu;
 }
 
+// the UTF-8 bytes of cp into bytes[0..n), returns n
+__device__ __forceinline__ uint32_t utf8_bytes_of(uint32_t cp, uint32_t bytes[4]) {
+    const int cl = utf8_len(cp);
+    if (cl == 1) { bytes[0] = cp; }
+    else if (cl == 2) { bytes[0] = 0xC0u | (cp >> 6); bytes[1] = 0x80u | (cp & 63u); }
+    else if (cl == 3) { bytes[0] = 0xE0u | (cp >> 12); bytes[1] = 0x80u | ((cp >> 6) & 63u); bytes[2] = 0x80u | (cp & 63u); }
+    else { bytes[0] = 0xF0u | (cp >> 18); bytes[1] = 0x80u | ((cp >> 12) & 63u); bytes[2] = 0x80u | ((cp >> 6) & 63u); bytes[3] = 0x80u | (cp & 63u); }
+    return (uint32_t)cl;
+}
+
 __device__ __forceinline__ int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }
 
 // per-half unsigned 16-bit min of two packed pairs (v_pk_min_u16)
@@ -524,7 +534,8 @@ __device__ AK_D2_INLINE D2Exact d2_exact(MemT &M, const uint16_t *P, const uint3
 //       (M.v) with V_B / V_E sentinels around each row.
 // A row whose NFC quick check trips or that holds invalid UTF-8 is marked in M.fb (the caller sends
 // it to the fallback kernels).
-template <int BCAP, class Mem>
+// NFCD: the rows are NFC already (k_bpe_nfc normalized them): only invalid UTF-8 is checked in D2.
+template <int BCAP, class Mem, bool NFCD = false>
 __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, uint64_t rend, const uint32_t *H, Mem &M) {
     const int lane = w_lane();
     const int nr0 = (int)(rend - r0);
@@ -629,12 +640,12 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             // a base + mark decomposition) decide, and the rows still unproven are marked for the
             // fallback kernels.
             const bool ok = chr && !bad && !xp;
-            const bool t0 = ok && !(h & H_STABLE) && nfc_trig<false>(h, hprev);
-            const bool pc = ok && nfc_pair_cand(h, hprev);
+            const bool t0 = !NFCD && ok && !(h & H_STABLE) && nfc_trig<false>(h, hprev);
+            const bool pc = !NFCD && ok && nfc_pair_cand(h, hprev);
             uint32_t cmp_hi = 0;
             if (w_ballot(bad || t0 || pc)) {
                 bool pfb = false, lok = false;
-                if (AK_KNOCKOUT != 15) {
+                if (AK_KNOCKOUT != 15 && !NFCD) {
                     const D2Exact r = d2_exact(M, P, H, c0, rows, vpos, carry_h, carry_cmp, h, cp, ok, chr, hp, hprev, mv);
                     hp = r.hp;
                     hprev = r.hprev;
@@ -643,7 +654,7 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
                     lok = r.lok;
                     cmp_hi = r.cmp_hi;
                 }
-                const bool trig = bad || pfb || (ok && !(h & H_STABLE) && !lok && nfc_trig<false>(h, hprev));
+                const bool trig = bad || pfb || (!NFCD && ok && !(h & H_STABLE) && !lok && nfc_trig<false>(h, hprev));
                 if (trig) M.fb[row] = 1;
             }
             const bool two = mark && row > 0;
@@ -945,7 +956,7 @@ __device__ __forceinline__ void pool_drain(const TileArgs &ta, TileWaveMem &M, u
     }
 }
 
-template <int FLAGS>
+template <int FLAGS, bool NFCD = false>
 __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *sfast,
                         TileWaveMem &M, uint4 *pool, PassClock &pc) {
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
@@ -953,7 +964,7 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
     const RowArgs &a = ta.ra;
     const BpeDev &m = a.bpe;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<T_BCAP>(a, r0, rend, H, M);
+    const TileRows tr = tile_front<T_BCAP, TileWaveMem, NFCD>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
     if (AK_KNOCKOUT == 10) return nr;

@@ -563,15 +563,6 @@ __device__ __forceinline__ float word_dp_pool(const SpBatch<B, CAPL> &P, const S
     return minm;
 }
 
-__device__ __forceinline__ uint32_t utf8_bytes_of(uint32_t cp, uint32_t bytes[4]) {
-    const int cl = utf8_len(cp);
-    if (cl == 1) { bytes[0] = cp; }
-    else if (cl == 2) { bytes[0] = 0xC0u | (cp >> 6); bytes[1] = 0x80u | (cp & 63u); }
-    else if (cl == 3) { bytes[0] = 0xE0u | (cp >> 12); bytes[1] = 0x80u | ((cp >> 6) & 63u); bytes[2] = 0x80u | (cp & 63u); }
-    else { bytes[0] = 0xF0u | (cp >> 18); bytes[1] = 0x80u | ((cp >> 12) & 63u); bytes[2] = 0x80u | ((cp >> 6) & 63u); bytes[3] = 0x80u | (cp & 63u); }
-    return (uint32_t)cl;
-}
-
 // One batch of ring c: its first cnt (<= B) entries, lane l the l-th.
 template <int B, int CAPL, class MemT>
 __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint4 *pool, uint32_t c, uint32_t cnt,

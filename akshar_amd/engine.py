@@ -515,3 +515,13 @@ def fallback_rows(dev=None):
     a, b = ctypes.c_uint64(), ctypes.c_uint64()
     check(_lib.lib().ak_ws_fallback_rows(ws, ctypes.byref(a), ctypes.byref(b)), "ak_ws_fallback_rows")
     return a.value, b.value
+
+
+def fallback_detail(dev=None):
+    """The last tile-path encode's fallback rows in detail (include/akshar.h ak_ws_fallback_detail):
+    sent off the tile kernel, finished by the tile path after all (BPE: wave NFC; SentencePiece: the
+    word pool's send-backs), left to the one-lane row pipeline, needing its slow tier."""
+    ws = workspace(dev)
+    d = (ctypes.c_uint64 * 4)()
+    check(_lib.lib().ak_ws_fallback_detail(ws, d), "ak_ws_fallback_detail")
+    return {"rows": d[0], "finished_in_tile_path": d[1], "one_lane": d[2], "slow_tier": d[3]}

@@ -14,6 +14,7 @@
 #include "../../akshar_amd/csrc/ak_model_build.h"
 #include "../../akshar_amd/csrc/ak_rows.h"
 #include "../../akshar_amd/csrc/ak_tile.h"
+#include "../../akshar_amd/csrc/ak_nfc_wave.h"
 #include "../../akshar_amd/csrc/ak_tile_spm.h"
 #include "../../akshar_amd/csrc/ak_tile_rows.h"
 
@@ -247,6 +248,8 @@ extern "C" uint32_t emu_last_fallback_rows() { return g_last_fb; }
 // the last tile launch's event counters (ak_tile.h TC_*: pre-token cache probes, hits)
 static uint64_t g_last_ctr[T_NCTR] = {};
 static uint32_t g_last_redo = 0;
+static uint32_t g_last_nfc = 0;
+extern "C" uint32_t emu_last_nfc_rows() { return g_last_nfc; }
 extern "C" uint32_t emu_last_redo_rows() { return g_last_redo; }
 extern "C" void emu_last_counters(uint64_t *out) { for (int i = 0; i < T_NCTR; ++i) out[i] = g_last_ctr[i]; }
 // waves the tile entries below emulate at once (each its own 64 threads and wave memory), all taking
@@ -305,6 +308,28 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     if (err) return -1;
     g_last_fb = fbn;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
+    // fallback rows as k_bpe_nfc: a wave per row, NFC then the tile pipeline with the NFC proof
+    // bypassed, into the row's slot; the rows it cannot take go on in fb3
+    std::vector<uint32_t> fb3(n), runlen(n + 1);
+    uint32_t fb3n = 0;
+    if (!getenv("AK_NO_NFC_WAVE")) {
+        std::vector<uint8_t> nbuf((size_t)g_waves * (NFC_SLOT + 16) + 64);
+        uint64_t *pairs = (uint64_t *)(nbuf.data() + (size_t)g_waves * NFC_SLOT);
+        std::vector<NfcWaveMem> NM(g_waves);
+        TileArgs tn = ta;
+        tn.ra.out = stage.data() + half;
+        tn.ra.cap = half;
+        run_waves([&](int w) {
+            bpe_nfc_wave<3>(tn, nbuf.data(), pairs, runlen.data(), fb3.data(), &fb3n, hot_tab, sfast.data(), fast, M[w],
+                            NM[w], (uint32_t)w, (uint32_t)g_waves);
+        });
+        if (err) return -1;
+        g_last_nfc = fbn - fb3n;
+        fbl.assign(fb3.begin(), fb3.begin() + fb3n);
+        fbn = fb3n;
+    } else {
+        g_last_nfc = 0;
+    }
     // fallback rows as k_tile_fb / k_tile_fb_slow: the row pipeline straight into the row's slot
     uint64_t maxlen = 0;
     for (uint64_t r = 0; r < n; ++r) maxlen = std::max<uint64_t>(maxlen, offs[r + 1] - offs[r]);
@@ -394,7 +419,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     ta.redo_list = redo.data();
     ta.redo_count = &nredo;
     std::vector<SpmWaveMem> M(g_waves);
-    if (m->sdev.pool_ok) {  // as the launcher: the pooled variant when the pool is on
+    if (m->sdev.pool_ok && !m->sdev.wc) {  // as the launcher: the pooled variant when the pool is on
         std::vector<SpmWaveMemP> MP(g_waves);
         run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMemP>(ta, hot_tab, scode, MP[w], (uint32_t)w, (uint32_t)g_waves); });
     } else {

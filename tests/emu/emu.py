@@ -16,7 +16,7 @@ def lib():
         so = os.path.join(HERE, "_emu.so")
         srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
                                                    ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h", "ak_ptc.h", "ak_swc.h",
-                                                    "ak_tile.h", "ak_tile_spm.h", "ak_tile_rows.h", "ak_wave.h")]
+                                                    "ak_tile.h", "ak_tile_spm.h", "ak_tile_rows.h", "ak_wave.h", "ak_nfc_wave.h")]
         srcs.append(os.path.join(HERE, "..", "..", "include", "akshar.h"))
         if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
             subprocess.check_call(["g++", "-O2", "-std=c++20", "-pthread", "-fPIC", "-shared", "-I",
@@ -191,6 +191,12 @@ def last_counters_all():
 
 def last_fallback_rows():
     return int(lib().emu_last_fallback_rows())
+
+
+def last_nfc_rows():
+    """BPE fallback rows the last bpe_tiles call finished through the wave NFC path (k_bpe_nfc)."""
+    lib().emu_last_nfc_rows.restype = ctypes.c_uint32
+    return int(lib().emu_last_nfc_rows())
 
 
 def last_redo_rows():

@@ -186,3 +186,22 @@ def test_nfc_mark_fuzz(em, bpe_model):
     assert emu.last_fallback_rows() < len(texts)
     ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
     assert rows_ints(ids, oo) == rows_ints(ref, ro)
+
+
+def test_fallback_rows_through_the_wave_nfc(golden, bpe_model, monkeypatch):
+    """The tile kernel's fallback rows of the golden set (alphabet / mixed-Unicode fuzz, adversarial
+    NFC rows) go through k_bpe_nfc's wave: NFC by segments, then the tile pipeline with the NFC proof
+    bypassed; most finish there (the rest: invalid UTF-8, HF NFKC changes, over the tile buffer), and
+    every row equals the oracle, as with the one-lane path alone (AK_NO_NFC_WAVE)."""
+    texts = [r["text"] for r in golden if r["set"] in ("alphabet", "fuzz", "adversarial")]
+    buf, offs = O.pack(texts)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    m = emu.Model(bpe=bpe_model)
+    ids, oo, _ = emu.bpe_tiles(m, buf, offs, rows=8)
+    fb, nfc = emu.last_fallback_rows(), emu.last_nfc_rows()
+    assert fb > 100 and nfc > 0.9 * fb, (fb, nfc)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    monkeypatch.setenv("AK_NO_NFC_WAVE", "1")
+    ids, oo, _ = emu.bpe_tiles(m, buf, offs, rows=8)
+    assert emu.last_nfc_rows() == 0
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)

@@ -614,3 +614,22 @@ def test_spm_word_pool_variants_on_device(eng, spm_model, monkeypatch):
     ref, ro = O.OracleSPM(spm_model).encode_batch(*O.pack(texts[:n]))
     o = _cpu(oo)[:n + 1]
     assert np.array_equal(o.astype(np.uint64), ro) and np.array_equal(_cpu(ids)[:o[-1]].astype(np.uint32), ref)
+
+
+def test_bpe_fallback_rows_through_the_wave_nfc(golden, golden_nfkc, eng, bpe_model, monkeypatch):
+    """The tile kernel's fallback rows (the golden alphabet / mixed-Unicode fuzz / adversarial sets,
+    replicated 40 times, so many waves take them) through k_bpe_nfc: most finish in the tile path
+    (NFC by the wave, the tile pipeline with the proof bypassed), the rest in the one-lane kernel;
+    the ids equal the oracle and the one-lane path alone (AK_NO_NFC_WAVE)."""
+    texts = [r["text"] for r in golden if r["set"] in ("alphabet", "fuzz", "adversarial")] * 40
+    gb, go = eng.pack(texts)
+    m = eng.BPE(bpe_model)
+    ids, oo = m.encode_batch(gb, go)
+    d = eng.fallback_detail()
+    assert d["rows"] > 1000 and d["finished_in_tile_path"] > 0.9 * d["rows"], d
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(*O.pack(texts))
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    monkeypatch.setenv("AK_NO_NFC_WAVE", "1")
+    ids2, oo2 = m.encode_batch(gb, go)
+    assert eng.fallback_detail()["one_lane"] == d["rows"]
+    assert torch.equal(oo2, oo) and torch.equal(ids2, ids)

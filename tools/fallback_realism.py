@@ -43,6 +43,7 @@ def measure(model, gb, go, nbytes, reps=3):
     fn()
     torch.cuda.synchronize()
     fb = engine.fallback_rows()
+    fd = engine.fallback_detail() if model is not None else None
     engine.profile_enable(True)
     engine.profile_reset()
     for _ in range(reps):
@@ -52,6 +53,7 @@ def measure(model, gb, go, nbytes, reps=3):
     engine.profile_enable(False)
     ms = sum(v[0] for v in prof.values()) / reps
     return {"mb_s": round(nbytes / 1e3 / ms, 1), "ms": round(ms, 3), "fallback_rows": fb[0], "pool_rows": fb[1],
+            "fallback_detail": fd,
             "kernel_ms": {k: round(v[0] / reps, 3) for k, v in prof.items() if v[1]}}
 
 
