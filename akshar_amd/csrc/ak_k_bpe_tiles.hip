@@ -475,8 +475,10 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     if (const char *e = getenv("AK_TILE_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + waves_per_block - 1) / waves_per_block,
                                                        (uint64_t)num_cus() * (uint64_t)bpc);
-    // the waves' merge pools: POOL_CAP entries per wave slot of the grid
-    const uint64_t pool_entries = (uint64_t)grid * waves_per_block * POOL_CAP;
+    // the waves' merge pools: POOL_CAP entries per wave slot of the grid, and of k_bpe_nfc's grid
+    // (num_cus() blocks of NFC_BLOCK / 64 waves, which a small launch's tile grid may not reach)
+    const uint64_t pool_waves = std::max<uint64_t>((uint64_t)grid * waves_per_block, (uint64_t)num_cus() * (NFC_BLOCK / 64));
+    const uint64_t pool_entries = pool_waves * POOL_CAP;
     if (w->cap_bpool < pool_entries) {
         (void)hipFree(w->bpool);
         w->bpool = nullptr;
@@ -514,6 +516,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
             w->cap_nfc_aux = a0.n;
         }
         HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
+        if (w->cap_bpool < nw * POOL_CAP) return set_error(AK_ERR_HIP, "internal: merge pools smaller than k_bpe_nfc's grid");
         uint64_t *pairs = (uint64_t *)(w->nfc_buf + nw * NFC_SLOT);
         k_bpe_nfc<3><<<ngrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, pairs, w->nfc_aux, w->fb3, w->tile_misc + 5);
         HIP_TRY(hipGetLastError());

@@ -152,7 +152,9 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *nbuf, uint64_t *pairs,
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the NFC bytes and the pair have landed
 #endif
             w_sync();
-            tl.ra.offs = pr - r;  // offs[r], offs[r + 1] of the one-row tile: the pair
+            // offs[r], offs[r + 1] of the one-row tile read the pair: the array placed r entries
+            // before it (plain 64-bit address arithmetic, wrapping; only entries r and r + 1 are read)
+            tl.ra.offs = (const uint64_t *)((uintptr_t)pr - (uintptr_t)r * sizeof(uint64_t));
             const uint64_t s0 = o0 + 2 * r;  // the row's fallback slot (BPE: offs[r] + 2 r)
             if (lane == 0) M.unext = s0;
             w_sync();
