@@ -29,7 +29,7 @@ AK_ROW_LIMIT = 4
 AK_TILE_PASSES = ("pre", "stage_decode_nfc_map", "elong_ws_pretok", "pretoken_cache", "pretoken_starts", "merge_or_viterbi",
                   "fallback_list", "ids_to_slots", "pool_merges", "loop")
 AK_PROF = {"count": 0, "count_slow": 1, "scan": 2, "emit": 3, "emit_slow": 4, "tiles": 5, "copy": 6, "spm_tiles": 7,
-           "row_tiles": 8}
+           "row_tiles": 8, "fallback_wave": 9}
 
 P = ctypes.c_void_p
 U64 = ctypes.c_uint64

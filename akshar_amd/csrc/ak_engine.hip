@@ -508,12 +508,13 @@ extern "C" int ak_ws_fallback_detail(ak_ws *w, uint64_t detail[4]) {
     uint32_t h[8] = {};
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(h, w->tile_misc, sizeof(h), hipMemcpyDeviceToHost));
-    // tile_misc: [0] fallback list, [2] slow tier, [4] SPM send-backs, [5] BPE rows k_bpe_nfc passed on
+    // tile_misc: [0] fallback list, [2] slow tier, [4] SPM send-backs, [5] rows k_*_nfc passed on
     // ([6]: 1 when the last launch was SPM, which leaves [5] alone)
     const bool spm = h[6] != 0;
+    const uint64_t one_lane = std::min(h[0], h[5]);
     detail[0] = spm ? (uint64_t)h[0] + h[4] : h[0];
-    detail[1] = spm ? h[4] : h[0] - std::min(h[0], h[5]);
-    detail[2] = spm ? h[0] : std::min(h[0], h[5]);
+    detail[1] = (spm ? h[4] : 0u) + h[0] - one_lane;
+    detail[2] = one_lane;
     detail[3] = h[2];
     return AK_OK;
 }

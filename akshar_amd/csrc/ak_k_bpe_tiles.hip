@@ -494,7 +494,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     HIP_TRY(hipGetLastError());
     // fallback rows: the full row pipeline (exact NFC, HF-NFC, any UTF-8) into the same slots, then
     // the slow and huge tiers for rows past its buffers
-    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
+    AK_PROF(AK_PROF_FALLBACK_WAVE, false, st);
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
@@ -525,6 +525,8 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     } else {  // every fallback row goes on (ak_ws_fallback_detail)
         HIP_TRY(hipMemcpyAsync(w->tile_misc + 5, w->tile_misc, 4, hipMemcpyDeviceToDevice, st));
     }
+    AK_PROF(AK_PROF_FALLBACK_WAVE, true, st);
+    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
     static std::atomic<int> fb_bpc{0};
     k_tile_fb<3><<<resident_grid(k_tile_fb<3>, FB_BLOCK, fb_bpc), FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;

@@ -65,6 +65,30 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_redo(TileArgs ta) {
                          gridDim.x * (SPM_TILE_BLOCK / 64));
 }
 
+// the tile kernel's fallback rows, a wave per row (ak_tile_spm.h spm_nfc_wave): NFC, then the tile
+// variant over the NFC text into the row's fallback slot; the rest go on in fb3 (k_spm_tile_fb)
+constexpr int SPM_NFC_BLOCK = 256;
+template <int FLAGS>
+__global__ __launch_bounds__(SPM_NFC_BLOCK) void k_spm_nfc(TileArgs ta, uint8_t *nbuf, uint64_t *pairs, uint32_t *fb3,
+                                                          uint32_t *fb3_count) {
+    __shared__ uint32_t hot_tab[HOT_N];
+    __shared__ uint16_t scode[HOT_N];
+    __shared__ uint2 fast[FAST_N];
+    __shared__ SpmWaveMem wm[SPM_NFC_BLOCK / 64];
+    __shared__ NfcWaveMem nm[SPM_NFC_BLOCK / 64];
+    if (*ta.fb_count == 0) return;  // uniform: the common case
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_NFC_BLOCK) {
+        const uint32_t cp = hot_cp(i);
+        hot_tab[i] = hot_word(cp);
+        const uint32_t c = spm_code(ta.ra.spm, cp);
+        scode[i] = (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
+    }
+    stage_tables(fast, nullptr, nullptr, false);  // (syncs the block)
+    const uint32_t wave = threadIdx.x >> 6;
+    spm_nfc_wave<FLAGS>(ta, nbuf, pairs, fb3, fb3_count, hot_tab, scode, fast, wm[wave], nm[wave],
+                        blockIdx.x * (SPM_NFC_BLOCK / 64) + wave, gridDim.x * (SPM_NFC_BLOCK / 64));
+}
+
 // fallback rows with the fast row kernel's buffer sizes, straight into the row's tile slot. The
 // lattice and NFC buffers of each lane are a private array, i.e. scratch (cached, lane-interleaved):
 // in LDS (1.1 KB per lane) they held the kernel to one wave per CU; as scratch eight 64-lane blocks
@@ -259,12 +283,39 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     else k_spm_tiles<3, false><<<grid, SPM_TILE_BLOCK, 0, st>>>(ta);
     AK_PROF(AK_PROF_SPM_TILES, true, st);
     HIP_TRY(hipGetLastError());
-    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
+    AK_PROF(AK_PROF_FALLBACK_WAVE, false, st);
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
     k_spm_redo<3><<<(unsigned)num_cus() * (unsigned)bpc, SPM_TILE_BLOCK, 0, st>>>(tfb);
     HIP_TRY(hipGetLastError());
+    if (!getenv("AK_NO_NFC_WAVE")) {  // (development aid: the one-lane path for every fallback row)
+        const unsigned ngrid = (unsigned)num_cus();
+        const uint64_t nw = (uint64_t)ngrid * (SPM_NFC_BLOCK / 64);
+        if (w->cap_nfc < nw) {
+            (void)hipFree(w->nfc_buf);
+            w->nfc_buf = nullptr;
+            w->cap_nfc = 0;
+            HIP_TRY(hipMalloc(&w->nfc_buf, nw * (NFC_SLOT + 16) + 64));
+            w->cap_nfc = nw;
+        }
+        if (w->cap_fb3 < a0.n) {
+            (void)hipFree(w->fb3);
+            w->fb3 = nullptr;
+            HIP_TRY(hipMalloc(&w->fb3, a0.n * 4));
+            w->cap_fb3 = a0.n;
+        }
+        HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
+        uint64_t *pairs = (uint64_t *)(w->nfc_buf + nw * NFC_SLOT);
+        k_spm_nfc<3><<<ngrid, SPM_NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, pairs, w->fb3, w->tile_misc + 5);
+        HIP_TRY(hipGetLastError());
+        tfb.fb_list = w->fb3;
+        tfb.fb_count = w->tile_misc + 5;
+    } else {  // every fallback row goes on (ak_ws_fallback_detail)
+        HIP_TRY(hipMemcpyAsync(w->tile_misc + 5, w->tile_misc, 4, hipMemcpyDeviceToDevice, st));
+    }
+    AK_PROF(AK_PROF_FALLBACK_WAVE, true, st);
+    AK_PROF(AK_PROF_EMIT_SLOW, false, st);
     static std::atomic<int> fb_bpc{0};
     k_spm_tile_fb<3><<<resident_grid(k_spm_tile_fb<3>, SPM_FB_BLOCK, fb_bpc), SPM_FB_BLOCK, 0, st>>>(tfb);
     RowArgs ra = tfb.ra;

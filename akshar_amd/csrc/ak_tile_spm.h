@@ -29,6 +29,7 @@
 // tau = (L + 3) M 2^-22 for a word of L chars is sufficient.
 // Reference semantics: normalize.py:117-148, tokenizer.py:190-191, cli.py:232-248.
 #pragma once
+#include "ak_nfc_wave.h"
 #include "ak_swc.h"
 #include "ak_tile.h"
 
@@ -668,7 +669,7 @@ __device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, MemT &M, uint
     }
 }
 
-template <int FLAGS, class MemT>
+template <int FLAGS, class MemT, bool NFCD = false>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
                         MemT &M, uint4 *pool, PassClock &pc, bool redo_mode = false) {
     constexpr int BCAP = MemT::BC, WN = MemT::WN;
@@ -678,7 +679,7 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     const RowArgs &a = ta.ra;
     const SpmDev &m = a.spm;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<BCAP>(a, r0, rend, H, M);
+    const TileRows tr = tile_front<BCAP, MemT, NFCD>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
     pc.mark(TP_D);
@@ -1045,6 +1046,50 @@ __device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint1
         }
         w_sync();
         (void)spm_tile<FLAGS, SpmWaveMem>(ta, r, r + 1, H, scode, M, nullptr, pc, true);
+    }
+}
+
+// The SentencePiece kernel's fallback rows a wave per row (k_spm_nfc), as bpe_nfc_wave
+// (ak_nfc_wave.h): NFC by segments into the wave's byte slot, then the tile variant over the NFC
+// text as a one-row tile (NFC proof bypassed, words in the tile, the carried base for close calls)
+// into the row's fallback slot; the rows it cannot take go on to the one-lane kernel (fb3).
+template <int FLAGS>
+__device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *nbuf, uint64_t *pairs, uint32_t *fb3, uint32_t *fb3_count,
+                             const uint32_t *H, const uint16_t *scode, const uint2 *fast, SpmWaveMem &M, NfcWaveMem &NM,
+                             uint32_t wave_gid, uint32_t nwaves) {
+    const uint32_t nl = *ta.fb_count;
+    const int lane = w_lane();
+    PassClock pc;
+    pc.init(false, M.passacc);
+    uint8_t *slot = nbuf + (uint64_t)wave_gid * NFC_SLOT;
+    uint64_t *pr = pairs + 2 * (uint64_t)wave_gid;
+    TileArgs tl = ta;
+    tl.fb_list = fb3;  // rows that fall back again
+    tl.fb_count = fb3_count;
+    tl.ra.in = nbuf;
+    for (uint32_t i = wave_gid; i < nl; i += nwaves) {
+        const uint64_t r = ta.fb_list[i];
+        const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
+        const int nb = len <= (uint64_t)NW_MAXB ? nfc_row_wave(ta.ra.in + o0, (int)len, slot, (int)NFC_SLOT - 16, NM, fast) : -1;
+        if (nb < 0) {
+            if (lane == 0) fb3[atomicAdd(fb3_count, 1u)] = (uint32_t)r;
+            continue;
+        }
+        if (lane == 0) {
+            pr[0] = (uint64_t)(slot - nbuf);
+            pr[1] = (uint64_t)(slot - nbuf) + (uint64_t)nb;
+        }
+#ifndef AK_HOST_EMU
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the NFC bytes and the pair have landed
+#endif
+        w_sync();
+        tl.ra.offs = (const uint64_t *)((uintptr_t)pr - (uintptr_t)r * sizeof(uint64_t));  // (bpe_nfc_wave)
+        if (lane == 0) {
+            M.unext = 2 * o0 + 2 * r;  // the row's fallback slot (SentencePiece: 2 offs[r] + 2 r)
+            M.ufbm = 0;
+        }
+        w_sync();
+        (void)spm_tile<FLAGS, SpmWaveMem, true>(tl, r, r + 1, H, scode, M, nullptr, pc, true);
     }
 }
 

@@ -221,7 +221,8 @@ int ak_spm_encode_host(const ak_spm *m, ak_ws *ws, int flags, const uint8_t *tex
 #define AK_PROF_COPY 6       /* staged ids -> final positions (tile path) */
 #define AK_PROF_SPM_TILES 7  /* tile-cooperative SentencePiece kernel */
 #define AK_PROF_ROW_TILES 8  /* tile-cooperative normalize / segment / switches / analyze kernel */
-#define AK_PROF_NKERNELS 9
+#define AK_PROF_FALLBACK_WAVE 9 /* fallback rows a wave each: SentencePiece redo, wave NFC + tile (BPE, SPM) */
+#define AK_PROF_NKERNELS 10
 /* level 0 off; 1 = HIP events around every launch (ak_profile_read; timing-neutral); 2 = also the
  * tile kernels' per-pass clocks (ak_profile_tile_passes), which instrument the kernels themselves */
 int ak_profile_enable(int level);

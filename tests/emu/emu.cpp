@@ -432,9 +432,32 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         tr.ra.out = stage.data() + half;
         run_waves([&](int w) { spm_redo_wave<3>(tr, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
     }
+    const uint32_t tile_fb = fbn;  // the tile kernel's fallback rows (last_fallback_rows)
+    if (!getenv("AK_NO_NFC_WAVE")) {  // as k_spm_nfc: the fallback rows a wave each, NFC then the tile
+        static uint2 sfastp[FAST_N];
+        for (uint32_t i = 0; i < FAST_N; ++i) sfastp[i] = prop_global(i);
+        std::vector<uint8_t> nbuf((size_t)g_waves * (NFC_SLOT + 16) + 64);
+        uint64_t *pairs = (uint64_t *)(nbuf.data() + (size_t)g_waves * NFC_SLOT);
+        std::vector<NfcWaveMem> NM(g_waves);
+        std::vector<uint32_t> fb3(n);
+        uint32_t fb3n = 0;
+        TileArgs tn = ta;
+        tn.ra.out = stage.data() + half;
+        run_waves([&](int w) {
+            spm_nfc_wave<3>(tn, nbuf.data(), pairs, fb3.data(), &fb3n, hot_tab, scode, sfastp, M[w], NM[w], (uint32_t)w,
+                            (uint32_t)g_waves);
+        });
+        if (err) return -1;
+        g_last_nfc = fbn - fb3n;
+        fbl.assign(fb3.begin(), fb3.begin() + fb3n);
+        fbl.resize(n);
+        fbn = fb3n;
+    } else {
+        g_last_nfc = 0;
+    }
     for (int i = 0; i < T_NCTR; ++i) g_last_ctr[i] = prof[T_NPASS + i];
     if (err) return -1;
-    g_last_fb = fbn;
+    g_last_fb = tile_fb;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
     uint64_t maxlen = 0;
     for (uint64_t r = 0; r < n; ++r) maxlen = std::max<uint64_t>(maxlen, offs[r + 1] - offs[r]);

@@ -158,3 +158,21 @@ def test_word_pool_off_is_the_same(spm_model, monkeypatch):
     m = emu.Model(spm=spm_model)
     ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_fallback_rows_through_the_wave_nfc(golden, spm_model, monkeypatch):
+    """SentencePiece's fallback rows of the golden alphabet / fuzz / adversarial sets through
+    k_spm_nfc's wave (NFC by segments, then the tile variant over the NFC text): most finish there,
+    and every row equals the oracle, as with the one-lane path alone (AK_NO_NFC_WAVE)."""
+    texts = [r["text"] for r in golden if r["set"] in ("alphabet", "fuzz", "adversarial")]
+    buf, offs = O.pack(texts)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    m = emu.Model(spm=spm_model)
+    ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
+    fb, nfc = emu.last_fallback_rows(), emu.last_nfc_rows()
+    assert fb > 100 and nfc > 0.8 * fb, (fb, nfc)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    monkeypatch.setenv("AK_NO_NFC_WAVE", "1")
+    ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
+    assert emu.last_nfc_rows() == 0
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)

@@ -633,3 +633,20 @@ def test_bpe_fallback_rows_through_the_wave_nfc(golden, golden_nfkc, eng, bpe_mo
     ids2, oo2 = m.encode_batch(gb, go)
     assert eng.fallback_detail()["one_lane"] == d["rows"]
     assert torch.equal(oo2, oo) and torch.equal(ids2, ids)
+
+
+def test_spm_fallback_rows_through_the_wave_nfc(golden, eng, spm_model, monkeypatch):
+    """As above for SentencePiece (k_spm_nfc after k_spm_redo): the fallback rows of the golden
+    alphabet / fuzz / adversarial sets, replicated 40 times, mostly finish in the wave path and
+    the ids equal the oracle and the one-lane path alone (AK_NO_NFC_WAVE)."""
+    texts = [r["text"] for r in golden if r["set"] in ("alphabet", "fuzz", "adversarial")] * 40
+    gb, go = eng.pack(texts)
+    m = eng.SPM(spm_model)
+    ids, oo = m.encode_batch(gb, go)
+    d = eng.fallback_detail()
+    assert d["rows"] > 1000 and d["finished_in_tile_path"] > 0.8 * d["rows"], d
+    ref, ro = O.OracleSPM(spm_model).encode_batch(*O.pack(texts))
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    monkeypatch.setenv("AK_NO_NFC_WAVE", "1")
+    ids2, oo2 = m.encode_batch(gb, go)
+    assert torch.equal(oo2, oo) and torch.equal(ids2, ids)
