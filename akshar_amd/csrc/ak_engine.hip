@@ -567,7 +567,6 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->redo);
     (void)hipFree(w->fb3);
     (void)hipFree(w->nfc_buf);
-    (void)hipFree(w->nfc_aux);
     (void)hipFree(w->counts);
     (void)hipFree(w->slow_list);
     (void)hipFree(w->huge_list);

@@ -72,10 +72,8 @@ struct AkWs {
     uint64_t cap_redo = 0;
     uint32_t *fb3 = nullptr;        // tile BPE: fallback rows k_bpe_nfc could not take (k_tile_fb)
     uint64_t cap_fb3 = 0;
-    uint8_t *nfc_buf = nullptr;     // tile BPE: k_bpe_nfc's per-wave NFC text slots + offset pairs
+    uint8_t *nfc_buf = nullptr;     // k_bpe_nfc / k_spm_nfc: per-wave epochs (ak_nfc_wave.h NE_BYTES each)
     uint64_t cap_nfc = 0;           // ... waves
-    uint32_t *nfc_aux = nullptr;    // ... per listed row, its run length in its slot
-    uint64_t cap_nfc_aux = 0;
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)

@@ -46,18 +46,16 @@ __global__ __launch_bounds__(TILE_BLOCK, AK_BPE_TILE_WPE) void k_bpe_tiles(TileA
                           gridDim.x * (TILE_BLOCK / 64));
 }
 
-// The tile kernel's fallback rows, a wave per row (ak_nfc_wave.h): the row's NFC into the wave's
-// byte slot, then bpe_tile<NFCD> over that text as a one-row tile writing into the row's fallback
-// slot (ta.ra.out is the second staging half); its merge-pool misses go to the wave's own rings,
-// which leave STAGE_DEAD entries in the slot: after the wave's last batch each slot is compacted in
-// place (the copy takes a fallback row's count entries as they are). A row this cannot take
-// (invalid UTF-8, over NW_MAXB bytes, a segment past NW_DCAP, or a fallback again in the tile: HF's
-// NFKC changes the text) goes on to k_tile_fb through the second list (fb3).
+// The tile kernel's fallback rows in each wave's epochs (ak_nfc_wave.h): the rows' NFC back to back
+// into the epoch's text, bpe_tile<NFCD> over it R rows at a time into the epoch's id region (the
+// merge-pool misses in the wave's own rings, drained at the epoch's end), then each row's live ids
+// to its fallback slot (ta.ra.out is the second staging half). A row this cannot take (invalid
+// UTF-8, over NW_MAXB bytes, a segment past NW_DCAP, a fallback again in the tile: HF's NFKC changes
+// the text, or ids past its slot) goes on to k_tile_fb through the second list (fb3).
 constexpr int NFC_BLOCK = 256;
 
 template <int FLAGS>
-__global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *nbuf, uint64_t *pairs, uint32_t *runlen,
-                                                      uint32_t *fb3, uint32_t *fb3_count) {
+__global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t sfast[SFAST_N];
     __shared__ uint2 fast[FAST_N];
@@ -70,7 +68,7 @@ __global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *nbu
         sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     stage_tables(fast, nullptr, nullptr, false);  // (syncs the block)
     const uint32_t wave = threadIdx.x >> 6;
-    bpe_nfc_wave<FLAGS>(ta, nbuf, pairs, runlen, fb3, fb3_count, hot_tab, sfast, fast, wm[wave], nm[wave],
+    bpe_nfc_wave<FLAGS>(ta, ebuf, fb3, fb3_count, hot_tab, sfast, fast, wm[wave], nm[wave],
                         blockIdx.x * (NFC_BLOCK / 64) + wave, gridDim.x * (NFC_BLOCK / 64));
 }
 
@@ -505,20 +503,12 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
             (void)hipFree(w->nfc_buf);
             w->nfc_buf = nullptr;
             w->cap_nfc = 0;
-            HIP_TRY(hipMalloc(&w->nfc_buf, nw * (NFC_SLOT + 16) + 64));
+            HIP_TRY(hipMalloc(&w->nfc_buf, nw * NE_BYTES));
             w->cap_nfc = nw;
-        }
-        if (w->cap_nfc_aux < a0.n) {
-            (void)hipFree(w->nfc_aux);
-            w->nfc_aux = nullptr;
-            w->cap_nfc_aux = 0;
-            HIP_TRY(hipMalloc(&w->nfc_aux, (a0.n + 1) * 4));
-            w->cap_nfc_aux = a0.n;
         }
         HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
         if (w->cap_bpool < nw * POOL_CAP) return set_error(AK_ERR_HIP, "internal: merge pools smaller than k_bpe_nfc's grid");
-        uint64_t *pairs = (uint64_t *)(w->nfc_buf + nw * NFC_SLOT);
-        k_bpe_nfc<3><<<ngrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, pairs, w->nfc_aux, w->fb3, w->tile_misc + 5);
+        k_bpe_nfc<3><<<ngrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
         HIP_TRY(hipGetLastError());
         tfb.fb_list = w->fb3;
         tfb.fb_count = w->tile_misc + 5;

@@ -65,11 +65,11 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_redo(TileArgs ta) {
                          gridDim.x * (SPM_TILE_BLOCK / 64));
 }
 
-// the tile kernel's fallback rows, a wave per row (ak_tile_spm.h spm_nfc_wave): NFC, then the tile
-// variant over the NFC text into the row's fallback slot; the rest go on in fb3 (k_spm_tile_fb)
+// the tile kernel's fallback rows in each wave's epochs (ak_tile_spm.h spm_nfc_wave): NFC, the tile
+// variant over the NFC text, the ids to the rows' fallback slots; the rest go on in fb3 (k_spm_tile_fb)
 constexpr int SPM_NFC_BLOCK = 256;
 template <int FLAGS>
-__global__ __launch_bounds__(SPM_NFC_BLOCK) void k_spm_nfc(TileArgs ta, uint8_t *nbuf, uint64_t *pairs, uint32_t *fb3,
+__global__ __launch_bounds__(SPM_NFC_BLOCK) void k_spm_nfc(TileArgs ta, uint8_t *ebuf, uint32_t *fb3,
                                                           uint32_t *fb3_count) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(SPM_NFC_BLOCK) void k_spm_nfc(TileArgs ta, uint8_t 
     }
     stage_tables(fast, nullptr, nullptr, false);  // (syncs the block)
     const uint32_t wave = threadIdx.x >> 6;
-    spm_nfc_wave<FLAGS>(ta, nbuf, pairs, fb3, fb3_count, hot_tab, scode, fast, wm[wave], nm[wave],
+    spm_nfc_wave<FLAGS>(ta, ebuf, fb3, fb3_count, hot_tab, scode, fast, wm[wave], nm[wave],
                         blockIdx.x * (SPM_NFC_BLOCK / 64) + wave, gridDim.x * (SPM_NFC_BLOCK / 64));
 }
 
@@ -296,7 +296,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
             (void)hipFree(w->nfc_buf);
             w->nfc_buf = nullptr;
             w->cap_nfc = 0;
-            HIP_TRY(hipMalloc(&w->nfc_buf, nw * (NFC_SLOT + 16) + 64));
+            HIP_TRY(hipMalloc(&w->nfc_buf, nw * NE_BYTES));
             w->cap_nfc = nw;
         }
         if (w->cap_fb3 < a0.n) {
@@ -306,8 +306,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
             w->cap_fb3 = a0.n;
         }
         HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
-        uint64_t *pairs = (uint64_t *)(w->nfc_buf + nw * NFC_SLOT);
-        k_spm_nfc<3><<<ngrid, SPM_NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, pairs, w->fb3, w->tile_misc + 5);
+        k_spm_nfc<3><<<ngrid, SPM_NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
         HIP_TRY(hipGetLastError());
         tfb.fb_list = w->fb3;
         tfb.fb_count = w->tile_misc + 5;

@@ -26,12 +26,21 @@ namespace ak {
 constexpr int NW_MAXB = T_BCAP;  // rows the tile kernel could take (a longer NFC text falls back anyway)
 constexpr int NW_DCAP = 32;      // code points of one segment's NFC
 
+// An epoch: the fallback rows a wave NFC-normalizes back to back before encoding them together
+constexpr uint32_t NE_TCAP = 8192;  // their NFC text, bytes
+constexpr uint32_t NE_VMAX = 128;   // rows
+
 struct NfcWaveMem {
     alignas(16) uint8_t bytes[NW_MAXB + 32];  // the row's UTF-8 (+ slack: decode reads 4-byte windows)
     uint32_t cps[NW_MAXB];                     // its chars
     uint16_t seg[NW_MAXB + 1];                 // segment starts (+ the end)
-    uint32_t dec[64 * NW_DCAP];                // lane l's segment output at [l * NW_DCAP ...)
+    uint32_t dec[64 * NW_DCAP];                // lane l's segment output at [l * NW_DCAP ...); after the
+                                               // epoch's NFC: its rows' runs (nfc_epoch_finish)
+    uint32_t vrow[NE_VMAX];                    // the epoch's rows (virtual row v -> row)
+    __device__ uint32_t *vstart() { return dec; }  // virtual row v's run in the epoch's id region
+    __device__ uint32_t *vlen() { return dec + NE_VMAX; }  // ... its length (0xFFFFFFFF: the tile sent it on)
 };
+static_assert(64 * NW_DCAP >= 2 * NE_VMAX, "the epoch's runs overlay dec");
 
 // NFC of the row in[0..len) (global) into out[0..out_cap) (global). Returns its byte length or -1.
 __device__ __forceinline__ int nfc_row_wave(const uint8_t *in, int len, uint8_t *out, int out_cap, NfcWaveMem &W,
@@ -110,18 +119,157 @@ __device__ __forceinline__ int nfc_row_wave(const uint8_t *in, int len, uint8_t 
     return (int)pos;
 }
 
-// The kernel k_bpe_nfc's wave (ak_k_bpe_tiles.hip): the tile kernel's fallback rows i = wave_gid,
-// + nwaves, ... of ta.fb_list, each NFC-normalized into the wave's byte slot of nbuf
-// (nfc_row_wave) and encoded by bpe_tile<NFCD> as a one-row tile into its fallback slot (ta.ra.out:
-// the second staging half); runlen[i] = the entries it left there (0xFFFFFFFF: not taken, the
-// row is in fb3 for the one-lane kernel); after the wave's last merge batch the slots are
-// compacted in place (their STAGE_DEAD entries dropped).
-constexpr uint32_t NFC_SLOT = 3 * NW_MAXB + 64;  // a wave's NFC text (NFC at most triples the bytes)
+// The fallback kernels' waves (k_bpe_nfc, k_spm_nfc) take the tile kernel's fallback rows
+// i = wave_gid, + nwaves, ... of ta.fb_list in epochs: each row NFC-normalized by the wave
+// (nfc_row_wave) into the epoch's text, back to back, as virtual rows 0..v-1 (their offsets
+// E.voffs, their rows NM.vrow); then the tile pipeline with the NFC proof bypassed
+// (tile_front<.., NFCD = true>) encodes the virtual rows R at a time, ids into the epoch's id region
+// (a BPE epoch's pooled merges drained at its end); then each row's ids go to its fallback slot
+// (ta.ra.out: the second staging half; BPE offs[r] + 2 r, len + 2 entries; SentencePiece
+// 2 offs[r] + 2 r, 2 len + 2) when they fit, else the row goes to fb3 for the one-lane kernel
+// (NFC can lengthen a row: composition exclusions such as U+0958 -> U+0915 U+093C; its slow tier
+// takes rows past their slot), as do rows the wave could not normalize (invalid UTF-8, over NW_MAXB
+// bytes, a segment over NW_DCAP) or the tile sent on (HF NFKC changes, over the tile buffer).
+// Encoding 8 KB epochs instead of one row per tile spreads the tile's fixed per-pass cost.
+constexpr uint32_t NE_RCAP = 2 * NE_TCAP + 2 * NE_VMAX;  // ids (SentencePiece's bound: 2 bytes + 2 per row)
+constexpr uint64_t NE_TEXT_B = NE_TCAP + 64;              // + slack: the tile's 16-byte block loads
+constexpr uint64_t NE_OFFS_B = ((NE_VMAX + 1) * 8 + 15) / 16 * 16;
+constexpr uint64_t NE_CNT_B = NE_VMAX * 4, NE_FB_B = NE_VMAX * 4 + 16;
+constexpr uint64_t NE_REG_B = (NE_RCAP + 64) * 4;         // + slack: pool_flush's 16-entry windows
+constexpr uint64_t NE_BYTES = (NE_TEXT_B + NE_OFFS_B + NE_CNT_B + NE_FB_B + NE_REG_B + 255) / 256 * 256;  // per wave
 
+struct NfcEpoch {
+    uint8_t *text;     // NE_TCAP (+ slack)
+    uint64_t *voffs;   // NE_VMAX + 1
+    uint32_t *vcnt;    // the tile's per-row counts (a BPE pooled merge subtracts its dead symbols)
+    uint32_t *vfb;     // the tile's own fallback list (unused: its M.fb says the same), NE_VMAX
+    uint32_t *vfbc;    // ... and length
+    uint32_t *region;  // NE_RCAP (+ slack)
+};
+
+__device__ __forceinline__ NfcEpoch nfc_epoch(uint8_t *ebuf, uint32_t wave_gid) {
+    uint8_t *b = ebuf + (uint64_t)wave_gid * NE_BYTES;
+    NfcEpoch E;
+    E.text = b;
+    E.voffs = (uint64_t *)(b + NE_TEXT_B);
+    E.vcnt = (uint32_t *)(b + NE_TEXT_B + NE_OFFS_B);
+    E.vfb = (uint32_t *)(b + NE_TEXT_B + NE_OFFS_B + NE_CNT_B);
+    E.vfbc = E.vfb + NE_VMAX;
+    E.region = (uint32_t *)(b + NE_TEXT_B + NE_OFFS_B + NE_CNT_B + NE_FB_B);
+    return E;
+}
+
+// The epoch's tile arguments: virtual rows over the epoch's text, ids into its region.
+__device__ __forceinline__ TileArgs nfc_epoch_args(const TileArgs &ta, const NfcEpoch &E) {
+    TileArgs tl = ta;
+    tl.ra.in = E.text;
+    tl.ra.offs = E.voffs;
+    tl.ra.out = E.region;
+    tl.ra.cap = NE_RCAP;
+    tl.ra.row_status = nullptr;
+    tl.counts = E.vcnt;
+    tl.fb_list = E.vfb;
+    tl.fb_count = E.vfbc;
+    return tl;
+}
+
+__device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint64_t r) {
+    if (w_lane() == 0) fb3[atomicAdd(fb3_count, 1u)] = (uint32_t)r;
+}
+
+// The next epoch from fallback-list index i (advanced past the rows taken): returns its rows v.
+__device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_t &i, uint32_t nl, uint32_t nwaves,
+                                                     const NfcEpoch &E, NfcWaveMem &NM, const uint2 *fast, uint32_t *fb3,
+                                                     uint32_t *fb3_count) {
+    const int lane = w_lane();
+    uint32_t v = 0, tpos = 0;
+    if (lane == 0) {
+        E.voffs[0] = 0;
+        atomicExch(E.vfbc, 0u);  // (ordered with the tile's atomics on it)
+    }
+    for (; i < nl && v < NE_VMAX; i += nwaves) {
+        const uint64_t r = ta.fb_list[i];
+        const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
+        if (len > (uint64_t)NW_MAXB) {
+            nfc_fb3(fb3, fb3_count, r);
+            continue;
+        }
+        if (tpos + 3 * len + 16 > NE_TCAP) break;  // (an empty epoch takes any row: 3 NW_MAXB + 16 < NE_TCAP)
+        const int nb = nfc_row_wave(ta.ra.in + o0, (int)len, E.text + tpos, (int)(NE_TCAP - tpos), NM, fast);
+        if (nb < 0) {
+            nfc_fb3(fb3, fb3_count, r);
+            continue;
+        }
+        tpos += (uint32_t)nb;
+        if (lane == 0) {
+            NM.vrow[v] = (uint32_t)r;
+            E.voffs[v + 1] = tpos;
+        }
+        ++v;
+    }
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the text and offsets have landed (the tile reads them)
+#endif
+    w_sync();
+    return v;
+}
+static_assert(3 * NW_MAXB + 16 < NE_TCAP, "an empty epoch takes any row the wave normalizes");
+
+// Virtual rows [r, r + took) of one tile: their runs in the region (lane l: row r + l; sb: the tile's
+// first position; first: the row's run from there, n: its length; fb: the tile sent the row on).
+__device__ __forceinline__ void nfc_epoch_runs(NfcWaveMem &NM, uint32_t r, int took, uint64_t sb, bool fb, uint32_t first,
+                                               uint32_t n) {
+    const int lane = w_lane();
+    if (lane < took) {
+        NM.vstart()[r + lane] = (uint32_t)sb + (fb ? 0u : first);
+        NM.vlen()[r + lane] = fb ? 0xFFFFFFFFu : n;
+    }
+    w_sync();
+}
+
+// Each encoded virtual row's ids (its run without STAGE_DEAD entries) -> its fallback slot and count,
+// if they fit the slot; else -> fb3. BPE: slot = offs[r] + 2 r, len + 2 entries (mul 1); SentencePiece
+// 2 offs[r] + 2 r, 2 len + 2 (mul 2).
+__device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEpoch &E, NfcWaveMem &NM, uint32_t v,
+                                                 uint32_t mul, uint32_t *fb3, uint32_t *fb3_count) {
+    const int lane = w_lane();
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the region's ids, merges and counts have landed
+#endif
+    uint32_t *stage = (uint32_t *)ta.ra.out;
+    for (uint32_t j = 0; j < v; ++j) {
+        const uint64_t r = NM.vrow[j];
+        const uint32_t rl = NM.vlen()[j];
+        const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
+        const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : load_l2(E.vcnt + j);
+        if (rl == 0xFFFFFFFFu || (uint64_t)cnt > mul * len + 2) {
+            nfc_fb3(fb3, fb3_count, r);
+            continue;
+        }
+        const uint64_t s0 = mul * o0 + 2 * r;
+        const uint32_t b0 = NM.vstart()[j];
+        uint32_t d = 0;
+        for (uint32_t k0 = 0; k0 < rl; k0 += 64) {
+            const uint32_t k = k0 + (uint32_t)lane;
+            const uint32_t x = k < rl ? load_l2(E.region + b0 + k) : STAGE_DEAD;
+            const bool keep = x != STAGE_DEAD;
+            const uint64_t KM = w_ballot(keep);
+            if (keep) stage[s0 + d + w_rank(KM)] = x;
+            d += (uint32_t)w_popc(KM);
+        }
+        if (lane == 0) {
+            ta.counts[r] = cnt;
+            if (ta.ra.row_status) ta.ra.row_status[r] = 0;
+        }
+    }
+}
+
+// The kernel k_bpe_nfc's wave (ak_k_bpe_tiles.hip): epochs as above; the merge pool drained at each
+// epoch's end (its entries point into the region).
 template <int FLAGS>
-__device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *nbuf, uint64_t *pairs, uint32_t *runlen, uint32_t *fb3,
-                             uint32_t *fb3_count, const uint32_t *H, const uint16_t *sfast, const uint2 *fast,
-                             TileWaveMem &M, NfcWaveMem &NM, uint32_t wave_gid, uint32_t nwaves) {
+__device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count, const uint32_t *H,
+                             const uint16_t *sfast, const uint2 *fast, TileWaveMem &M, NfcWaveMem &NM, uint32_t wave_gid,
+                             uint32_t nwaves) {
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
     PassClock pc;
@@ -132,61 +280,24 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *nbuf, uint64_t *pairs,
         M.pcnt[lane] = 0;
     }
     w_sync();
-    uint8_t *slot = nbuf + (uint64_t)wave_gid * NFC_SLOT;
-    uint64_t *pr = pairs + 2 * (uint64_t)wave_gid;
-    TileArgs tl = ta;
-    tl.fb_list = fb3;  // rows that fall back again
-    tl.fb_count = fb3_count;
-    tl.ra.in = nbuf;
-    for (uint32_t i = wave_gid; i < nl; i += nwaves) {
-        const uint64_t r = ta.fb_list[i];
-        const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
-        const int nb = len <= (uint64_t)NW_MAXB ? nfc_row_wave(ta.ra.in + o0, (int)len, slot, (int)NFC_SLOT - 16, NM, fast) : -1;
-        uint32_t rl = 0xFFFFFFFFu;  // not taken here
-        if (nb >= 0) {
-            if (lane == 0) {
-                pr[0] = (uint64_t)(slot - nbuf);
-                pr[1] = (uint64_t)(slot - nbuf) + (uint64_t)nb;
-            }
-#ifndef AK_HOST_EMU
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the NFC bytes and the pair have landed
-#endif
-            w_sync();
-            // offs[r], offs[r + 1] of the one-row tile read the pair: the array placed r entries
-            // before it (plain 64-bit address arithmetic, wrapping; only entries r and r + 1 are read)
-            tl.ra.offs = (const uint64_t *)((uintptr_t)pr - (uintptr_t)r * sizeof(uint64_t));
-            const uint64_t s0 = o0 + 2 * r;  // the row's fallback slot (BPE: offs[r] + 2 r)
-            if (lane == 0) M.unext = s0;
-            w_sync();
-            const int took = bpe_tile<FLAGS, true>(tl, r, r + 1, H, sfast, M, pool, pc);
-            (void)took;
-            rl = (uint32_t)(w_bcast(M.unext, 0) - s0);
-            if (rl == 0) rl = 0xFFFFFFFFu;  // fell back again (a row writes >= 2 ids): bpe_tile listed it in fb3
-        } else if (lane == 0) {
-            fb3[atomicAdd(fb3_count, 1u)] = (uint32_t)r;
+    const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
+    const TileArgs tl = nfc_epoch_args(ta, E);
+    for (uint32_t i = wave_gid; i < nl;) {
+        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, NM, fast, fb3, fb3_count);
+        if (v == 0) continue;
+        if (lane == 0) M.unext = 0;
+        w_sync();
+        for (uint32_t r = 0; r < v;) {
+            const uint64_t sb = M.unext;
+            const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
+            const int took = bpe_tile<FLAGS, true>(tl, r, re, H, sfast, M, pool, pc);
+            const bool in = lane < took;
+            nfc_epoch_runs(NM, r, took, sb, in && M.fb[lane], in ? M.rowop[lane] : 0u,
+                           in ? M.rowop[lane + 1] - M.rowop[lane] : 0u);
+            r += (uint32_t)took;
         }
-        if (lane == 0) runlen[i] = rl;
-    }
-    pool_drain(ta, M, pool, 1u, pc);  // every miss merged
-#ifndef AK_HOST_EMU
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    // the slots without their STAGE_DEAD entries, in place (writes never pass the reads)
-    uint32_t *stage = (uint32_t *)ta.ra.out;
-    for (uint32_t i = wave_gid; i < nl; i += nwaves) {
-        const uint32_t rl = load_l2(runlen + i);
-        if (rl == 0xFFFFFFFFu) continue;
-        const uint64_t r = ta.fb_list[i];
-        const uint64_t s0 = ta.ra.offs[r] + 2 * r;
-        uint32_t d = 0;
-        for (uint32_t k0 = 0; k0 < rl; k0 += 64) {
-            const uint32_t k = k0 + (uint32_t)lane;
-            const uint32_t v = k < rl ? load_l2(stage + s0 + k) : STAGE_DEAD;
-            const bool keep = v != STAGE_DEAD;
-            const uint64_t KM = w_ballot(keep);
-            if (keep) stage[s0 + d + w_rank(KM)] = v;
-            d += (uint32_t)w_popc(KM);
-        }
+        pool_drain(tl, M, pool, 1u, pc);  // every miss of the epoch merged
+        nfc_epoch_finish(ta, E, NM, v, 1u, fb3, fb3_count);
     }
 }
 

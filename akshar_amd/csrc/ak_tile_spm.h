@@ -1049,47 +1049,37 @@ __device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint1
     }
 }
 
-// The SentencePiece kernel's fallback rows a wave per row (k_spm_nfc), as bpe_nfc_wave
-// (ak_nfc_wave.h): NFC by segments into the wave's byte slot, then the tile variant over the NFC
-// text as a one-row tile (NFC proof bypassed, words in the tile, the carried base for close calls)
-// into the row's fallback slot; the rows it cannot take go on to the one-lane kernel (fb3).
+// The SentencePiece kernel's fallback rows in a wave's epochs (k_spm_nfc), as bpe_nfc_wave
+// (ak_nfc_wave.h): NFC by segments into the epoch's text, then the tile variant over it (NFC proof
+// bypassed, words in the tile, the carried base for close calls), then each row's ids to its
+// fallback slot; the rows it cannot take go on to the one-lane kernel (fb3).
 template <int FLAGS>
-__device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *nbuf, uint64_t *pairs, uint32_t *fb3, uint32_t *fb3_count,
-                             const uint32_t *H, const uint16_t *scode, const uint2 *fast, SpmWaveMem &M, NfcWaveMem &NM,
-                             uint32_t wave_gid, uint32_t nwaves) {
+__device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count, const uint32_t *H,
+                             const uint16_t *scode, const uint2 *fast, SpmWaveMem &M, NfcWaveMem &NM, uint32_t wave_gid,
+                             uint32_t nwaves) {
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
     PassClock pc;
     pc.init(false, M.passacc);
-    uint8_t *slot = nbuf + (uint64_t)wave_gid * NFC_SLOT;
-    uint64_t *pr = pairs + 2 * (uint64_t)wave_gid;
-    TileArgs tl = ta;
-    tl.fb_list = fb3;  // rows that fall back again
-    tl.fb_count = fb3_count;
-    tl.ra.in = nbuf;
-    for (uint32_t i = wave_gid; i < nl; i += nwaves) {
-        const uint64_t r = ta.fb_list[i];
-        const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
-        const int nb = len <= (uint64_t)NW_MAXB ? nfc_row_wave(ta.ra.in + o0, (int)len, slot, (int)NFC_SLOT - 16, NM, fast) : -1;
-        if (nb < 0) {
-            if (lane == 0) fb3[atomicAdd(fb3_count, 1u)] = (uint32_t)r;
-            continue;
-        }
+    const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
+    const TileArgs tl = nfc_epoch_args(ta, E);
+    for (uint32_t i = wave_gid; i < nl;) {
+        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, NM, fast, fb3, fb3_count);
+        if (v == 0) continue;
         if (lane == 0) {
-            pr[0] = (uint64_t)(slot - nbuf);
-            pr[1] = (uint64_t)(slot - nbuf) + (uint64_t)nb;
-        }
-#ifndef AK_HOST_EMU
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the NFC bytes and the pair have landed
-#endif
-        w_sync();
-        tl.ra.offs = (const uint64_t *)((uintptr_t)pr - (uintptr_t)r * sizeof(uint64_t));  // (bpe_nfc_wave)
-        if (lane == 0) {
-            M.unext = 2 * o0 + 2 * r;  // the row's fallback slot (SentencePiece: 2 offs[r] + 2 r)
+            M.unext = 0;
             M.ufbm = 0;
         }
         w_sync();
-        (void)spm_tile<FLAGS, SpmWaveMem, true>(tl, r, r + 1, H, scode, M, nullptr, pc, true);
+        for (uint32_t r = 0; r < v;) {
+            const uint64_t sb = M.unext;
+            const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
+            const int took = spm_tile<FLAGS, SpmWaveMem, true>(tl, r, re, H, scode, M, nullptr, pc, true);
+            const bool in = lane < took;
+            nfc_epoch_runs(NM, r, took, sb, in && M.fb[lane], in ? M.rowfirst[lane] : 0u, in ? M.rowcnt[lane] : 0u);
+            r += (uint32_t)took;
+        }
+        nfc_epoch_finish(ta, E, NM, v, 2u, fb3, fb3_count);
     }
 }
 

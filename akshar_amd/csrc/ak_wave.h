@@ -95,6 +95,9 @@ inline uint32_t atomicAdd(uint32_t *p, uint32_t v) {
 inline uint32_t atomicSub(uint32_t *p, uint32_t v) {
     return reinterpret_cast<std::atomic<uint32_t> *>(p)->fetch_sub(v, std::memory_order_relaxed);
 }
+inline uint32_t atomicExch(uint32_t *p, uint32_t v) {
+    return reinterpret_cast<std::atomic<uint32_t> *>(p)->exchange(v, std::memory_order_relaxed);
+}
 inline unsigned long long atomicOr(unsigned long long *p, unsigned long long v) {
     return reinterpret_cast<std::atomic<unsigned long long> *>(p)->fetch_or(v, std::memory_order_relaxed);
 }

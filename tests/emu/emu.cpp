@@ -308,20 +308,19 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     if (err) return -1;
     g_last_fb = fbn;
     if (getenv("AK_EMU_DUMP_FB")) { for (uint32_t i = 0; i < fbn; ++i) fprintf(stderr, "fb row %u\n", fbl[i]); }
-    // fallback rows as k_bpe_nfc: a wave per row, NFC then the tile pipeline with the NFC proof
-    // bypassed, into the row's slot; the rows it cannot take go on in fb3
-    std::vector<uint32_t> fb3(n), runlen(n + 1);
+    // fallback rows as k_bpe_nfc: the waves' epochs (NFC, then the tile pipeline with the NFC proof
+    // bypassed, then the rows' slots); the rows it cannot take go on in fb3
+    std::vector<uint32_t> fb3(n);
     uint32_t fb3n = 0;
     if (!getenv("AK_NO_NFC_WAVE")) {
-        std::vector<uint8_t> nbuf((size_t)g_waves * (NFC_SLOT + 16) + 64);
-        uint64_t *pairs = (uint64_t *)(nbuf.data() + (size_t)g_waves * NFC_SLOT);
+        std::vector<uint8_t> ebuf((size_t)g_waves * NE_BYTES);
         std::vector<NfcWaveMem> NM(g_waves);
         TileArgs tn = ta;
         tn.ra.out = stage.data() + half;
         tn.ra.cap = half;
         run_waves([&](int w) {
-            bpe_nfc_wave<3>(tn, nbuf.data(), pairs, runlen.data(), fb3.data(), &fb3n, hot_tab, sfast.data(), fast, M[w],
-                            NM[w], (uint32_t)w, (uint32_t)g_waves);
+            bpe_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, sfast.data(), fast, M[w], NM[w], (uint32_t)w,
+                            (uint32_t)g_waves);
         });
         if (err) return -1;
         g_last_nfc = fbn - fb3n;
@@ -433,18 +432,17 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         run_waves([&](int w) { spm_redo_wave<3>(tr, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
     }
     const uint32_t tile_fb = fbn;  // the tile kernel's fallback rows (last_fallback_rows)
-    if (!getenv("AK_NO_NFC_WAVE")) {  // as k_spm_nfc: the fallback rows a wave each, NFC then the tile
+    if (!getenv("AK_NO_NFC_WAVE")) {  // as k_spm_nfc: the waves' epochs, NFC then the tile
         static uint2 sfastp[FAST_N];
         for (uint32_t i = 0; i < FAST_N; ++i) sfastp[i] = prop_global(i);
-        std::vector<uint8_t> nbuf((size_t)g_waves * (NFC_SLOT + 16) + 64);
-        uint64_t *pairs = (uint64_t *)(nbuf.data() + (size_t)g_waves * NFC_SLOT);
+        std::vector<uint8_t> ebuf((size_t)g_waves * NE_BYTES);
         std::vector<NfcWaveMem> NM(g_waves);
         std::vector<uint32_t> fb3(n);
         uint32_t fb3n = 0;
         TileArgs tn = ta;
         tn.ra.out = stage.data() + half;
         run_waves([&](int w) {
-            spm_nfc_wave<3>(tn, nbuf.data(), pairs, fb3.data(), &fb3n, hot_tab, scode, sfastp, M[w], NM[w], (uint32_t)w,
+            spm_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, scode, sfastp, M[w], NM[w], (uint32_t)w,
                             (uint32_t)g_waves);
         });
         if (err) return -1;

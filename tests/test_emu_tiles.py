@@ -205,3 +205,22 @@ def test_fallback_rows_through_the_wave_nfc(golden, bpe_model, monkeypatch):
     ids, oo, _ = emu.bpe_tiles(m, buf, offs, rows=8)
     assert emu.last_nfc_rows() == 0
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_wave_nfc_rows_that_nfc_lengthens(bpe_model, spm_model):
+    """Fallback rows whose NFC is longer than the row (composition exclusions: U+1D15E -> U+1D157
+    U+1D165, 4 -> 8 bytes; U+0F73 -> U+0F71 U+0F72; U+0958 -> U+0915 U+093C), back to back: they go
+    on to the one-lane kernel (with a byte-level model their ids could pass the row's slot and
+    overwrite the neighbour's; the test models' merges keep them inside), and every row equals the
+    oracle (BPE and SentencePiece)."""
+    rng = np.random.default_rng(7)
+    parts = ["\U0001D15E", "ཱི", "क̴़", "á", " ", "x", "क"]
+    texts = ["".join(rng.choice(parts, size=int(rng.integers(1, 9)))) for _ in range(300)]
+    buf, offs = O.pack(texts)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    ids, oo, _ = emu.bpe_tiles(emu.Model(bpe=bpe_model), buf, offs, rows=8)
+    assert emu.last_nfc_rows() > 0
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
