@@ -272,8 +272,8 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
                              uint32_t nwaves) {
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
-    PassClock pc;
-    pc.init(false, M.passacc);
+    PassClock pc;  // (profiling level 2: the epochs' NFC and slot copies count as "loop")
+    pc.init(ta.passprof != nullptr, M.passacc);
     uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_CAP;
     if (lane < POOL_NCLASS) {
         M.phead[lane] = 0;
@@ -284,6 +284,7 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
     const TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nl;) {
         const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, NM, fast, fb3, fb3_count);
+        pc.mark(TP_LOOP);
         if (v == 0) continue;
         if (lane == 0) M.unext = 0;
         w_sync();
@@ -297,8 +298,11 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
             r += (uint32_t)took;
         }
         pool_drain(tl, M, pool, 1u, pc);  // every miss of the epoch merged
+        pc.mark(TP_FBE);
         nfc_epoch_finish(ta, E, NM, v, 1u, fb3, fb3_count);
+        pc.mark(TP_LOOP);
     }
+    pc.flush(ta.passprof);
 }
 
 }  // namespace ak

@@ -1031,7 +1031,7 @@ template <int FLAGS>
 __device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M, uint32_t wave_gid,
                               uint32_t nwaves) {
     PassClock pc;
-    pc.init(false, M.passacc);
+    pc.init(ta.passprof != nullptr, M.passacc);
     if (w_lane() < SP_NCLASS) {
         M.phead[w_lane()] = 0;
         M.pcnt[w_lane()] = 0;
@@ -1047,6 +1047,7 @@ __device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint1
         w_sync();
         (void)spm_tile<FLAGS, SpmWaveMem>(ta, r, r + 1, H, scode, M, nullptr, pc, true);
     }
+    pc.flush(ta.passprof);
 }
 
 // The SentencePiece kernel's fallback rows in a wave's epochs (k_spm_nfc), as bpe_nfc_wave
@@ -1059,12 +1060,13 @@ __device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
                              uint32_t nwaves) {
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
-    PassClock pc;
-    pc.init(false, M.passacc);
+    PassClock pc;  // (profiling level 2: the epochs' NFC and slot copies count as "loop")
+    pc.init(ta.passprof != nullptr, M.passacc);
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
     const TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nl;) {
         const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, NM, fast, fb3, fb3_count);
+        pc.mark(TP_LOOP);
         if (v == 0) continue;
         if (lane == 0) {
             M.unext = 0;
@@ -1080,7 +1082,9 @@ __device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
             r += (uint32_t)took;
         }
         nfc_epoch_finish(ta, E, NM, v, 2u, fb3, fb3_count);
+        pc.mark(TP_LOOP);
     }
+    pc.flush(ta.passprof);
 }
 
 }  // namespace ak

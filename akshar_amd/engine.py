@@ -485,14 +485,17 @@ def profile_read():
     return res
 
 
-def profile_tile_passes(dev=None):
-    """{pass name: fraction of tile-kernel wave-cycles} since the last call (profiling enabled)."""
+def profile_tile_passes(dev=None, raw=False):
+    """{pass name: fraction of tile-kernel wave-cycles} since the last call (profiling enabled);
+    raw: the wave-cycles themselves."""
     ws = workspace(dev)
     n = len(_lib.AK_TILE_PASSES)
     buf = (ctypes.c_uint64 * n)()
     k = _lib.lib().ak_profile_tile_passes(ws, buf, n)
     if k < 0:
         check(k, "ak_profile_tile_passes")
+    if raw:
+        return {name: int(buf[i]) for i, name in enumerate(_lib.AK_TILE_PASSES)} if k else {}
     tot = float(sum(buf)) or 1.0
     return {name: round(buf[i] / tot, 4) for i, name in enumerate(_lib.AK_TILE_PASSES)} if k else {}
 

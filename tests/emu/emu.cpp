@@ -316,6 +316,7 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
         std::vector<uint8_t> ebuf((size_t)g_waves * NE_BYTES);
         std::vector<NfcWaveMem> NM(g_waves);
         TileArgs tn = ta;
+        tn.passprof = nullptr;
         tn.ra.out = stage.data() + half;
         tn.ra.cap = half;
         run_waves([&](int w) {
@@ -428,6 +429,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     if (getenv("AK_EMU_DUMP_REDO")) { for (uint32_t i = 0; i < nredo; ++i) fprintf(stderr, "redo row %u\n", redo[i]); }
     {  // as k_spm_redo: the rows the word pool sent back, into their fallback slots
         TileArgs tr = ta;
+        tr.passprof = nullptr;
         tr.ra.out = stage.data() + half;
         run_waves([&](int w) { spm_redo_wave<3>(tr, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
     }
@@ -440,6 +442,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         std::vector<uint32_t> fb3(n);
         uint32_t fb3n = 0;
         TileArgs tn = ta;
+        tn.passprof = nullptr;
         tn.ra.out = stage.data() + half;
         run_waves([&](int w) {
             spm_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, scode, sfastp, M[w], NM[w], (uint32_t)w,
