@@ -1,23 +1,23 @@
-// ak_nfc_wave.h — NFC of one row by one wave: the first step of the tile path's fallback rows.
+// ak_nfc_wave.h — NFC of the tile path's fallback rows by waves: the first step of their epochs.
 //
 // A row the tile front end cannot prove NFC-identical (ak_tile.h nfc_trig and its exact clauses)
 // used to run the whole sequential pipeline in one lane (ak_rows.h process_row): decode, NFC,
-// normalize_text, the model, each step one code point at a time, ~0.5 ms for a 150-byte row. Here the
-// wave normalizes the row (normalize.py:13-18, unicodedata.normalize('NFC'), Unicode 13) and the
-// caller re-encodes the NFC text through the tile kernel with the NFC proof bypassed (ak_tile.h
+// normalize_text, the model, each step one code point at a time, ~0.5 ms for a 150-byte row. Here a
+// wave normalizes its rows (normalize.py:13-18, unicodedata.normalize('NFC'), Unicode 13) and
+// re-encodes the NFC text through the tile pipeline with the NFC proof bypassed (ak_tile.h
 // tile_front<.., NFCD = true>):
-//   decode   64 bytes per step: lead bytes by ballot, each lead decodes its char (branch-free
-//            decode_word), compacted into cps[]; the row is valid UTF-8 iff the leads' lengths sum
-//            to its bytes and every sequence decodes
+//   decode   a row at a time, 64 bytes per step: lead bytes by ballot, each lead decodes its char
+//            (branch-free decode_word), compacted into the batch's cps[]; the row is valid UTF-8 iff
+//            the leads' lengths sum to its bytes and every sequence decodes
 //   segment  NFC never looks across a stable char (ccc 0, NFC(c) = c, never a composition second):
-//            the row splits into segments [stable char, the non-stable chars after it), and NFC of
+//            a row splits into segments [stable char, the non-stable chars after it), and NFC of
 //            the row is the concatenation of NFC of its segments
-//   NFC      lane per segment: a lone char that does not decompose is itself; any other segment
-//            runs the exact sequential algorithm (ak_dev.h nfc_full: full canonical decomposition,
-//            stable ccc sort, canonical composition) on its few chars
+//   NFC      lane per segment, the segments of several rows together: a lone char that does not
+//            decompose is itself; any other segment runs the exact sequential algorithm (ak_dev.h
+//            nfc_full: full canonical decomposition, stable ccc sort, canonical composition)
 //   encode   UTF-8 byte counts per lane, a scan, and each lane writes its bytes
-// Rows over NW_MAXB bytes, a segment whose NFC passes NW_DCAP code points, or invalid UTF-8 return
-// -1: the caller keeps the one-lane path for those.
+// Rows over NW_MAXB bytes, a segment whose NFC passes NW_DCAP code points, or invalid UTF-8 go on
+// to the one-lane path.
 #pragma once
 #include "ak_tile.h"
 
@@ -31,26 +31,30 @@ constexpr uint32_t NE_TCAP = 8192;  // their NFC text, bytes
 constexpr uint32_t NE_VMAX = 128;   // rows
 
 struct NfcWaveMem {
-    alignas(16) uint8_t bytes[NW_MAXB + 32];  // the row's UTF-8 (+ slack: decode reads 4-byte windows)
-    uint32_t cps[NW_MAXB];                     // its chars
-    uint16_t seg[NW_MAXB + 1];                 // segment starts (+ the end)
+    alignas(16) uint8_t bytes[NW_MAXB + 32];  // a row's UTF-8 (+ slack: decode reads 4-byte windows)
+    uint32_t cps[NW_MAXB];                     // the batch's chars (several rows, back to back)
+    uint16_t seg[NW_MAXB + 1];                 // the batch's segment starts (+ the end)
+    uint8_t segrow[NW_MAXB];                   // ... each one's virtual row
     uint32_t dec[64 * NW_DCAP];                // lane l's segment output at [l * NW_DCAP ...); after the
                                                // epoch's NFC: its rows' runs (nfc_epoch_finish)
     uint32_t vrow[NE_VMAX];                    // the epoch's rows (virtual row v -> row)
+    uint32_t vbytes[NE_VMAX];                  // ... their NFC bytes
+    uint8_t vfail[NE_VMAX];                    // ... a segment's NFC failed (the row goes on to fb3)
     __device__ uint32_t *vstart() { return dec; }  // virtual row v's run in the epoch's id region
     __device__ uint32_t *vlen() { return dec + NE_VMAX; }  // ... its length (0xFFFFFFFF: the tile sent it on)
 };
+static_assert(NE_VMAX <= 256, "segrow is a byte");
 static_assert(64 * NW_DCAP >= 2 * NE_VMAX, "the epoch's runs overlay dec");
 
-// NFC of the row in[0..len) (global) into out[0..out_cap) (global). Returns its byte length or -1.
-__device__ __forceinline__ int nfc_row_wave(const uint8_t *in, int len, uint8_t *out, int out_cap, NfcWaveMem &W,
-                                            const uint2 *fast) {
+// Decode the row in[0..len) (global) into the batch: its chars at W.cps[nc ...), its segments (its
+// first char and every NFC-stable char) at W.seg[ns ...) with virtual row v. Returns false for
+// invalid UTF-8 (nc, ns unchanged: the row goes on); else advances nc and ns.
+__device__ __forceinline__ bool nfc_decode_row(const uint8_t *in, int len, uint32_t v, NfcWaveMem &W, int &nc, int &ns,
+                                               const uint2 *fast) {
     const int lane = w_lane();
-    if (len > NW_MAXB) return -1;
     for (int i = lane; i < len + 8; i += 64) W.bytes[i] = i < len ? in[i] : 0u;
     w_sync();
-    // decode
-    int nc = 0;
+    int c = nc;
     uint32_t tot_len = 0;
     bool bad = false;
     for (int base = 0; base < len; base += 64) {
@@ -61,28 +65,41 @@ __device__ __forceinline__ int nfc_row_wave(const uint8_t *in, int len, uint8_t 
         const uint32_t cp = lead ? decode_word(lds_word(W.bytes, p), p, len) : 0u;
         bad = bad || (lead && cp == 0xFFFFFFFFu);
         const uint64_t LM = w_ballot(lead);
-        if (lead) W.cps[nc + (int)w_rank(LM)] = cp;
+        if (lead) W.cps[c + (int)w_rank(LM)] = cp;
         uint32_t t;
         (void)w_exscan(lead && cp != 0xFFFFFFFFu ? (uint32_t)utf8_len(cp) : 0u, &t);
         tot_len += t;
-        nc += w_popc(LM);
+        c += w_popc(LM);
     }
-    if (w_ballot(bad) || tot_len != (uint32_t)len) return -1;  // invalid or stray continuation bytes
+    if (w_ballot(bad) || tot_len != (uint32_t)len) return false;  // invalid or stray continuation bytes
     w_sync();
-    // segment starts: the row start and every stable char
-    int ns = 0;
-    for (int base = 0; base < nc; base += 64) {
+    int s = ns;
+    for (int base = nc; base < c; base += 64) {
         const int i = base + lane;
-        const bool st = i < nc && (i == 0 || p_stable(prop(fast, W.cps[i])));
+        const bool st = i < c && (i == nc || p_stable(prop(fast, W.cps[i])));
         const uint64_t SM = w_ballot(st);
-        if (st) W.seg[ns + (int)w_rank(SM)] = (uint16_t)i;
-        ns += w_popc(SM);
+        if (st) {
+            W.seg[s + (int)w_rank(SM)] = (uint16_t)i;
+            W.segrow[s + (int)w_rank(SM)] = (uint8_t)v;
+        }
+        s += w_popc(SM);
     }
+    nc = c;
+    ns = s;
+    w_sync();
+    return true;
+}
+
+// NFC of the batch's segments, a lane each (64 per round, whatever rows they belong to): a lone char
+// that does not decompose is itself, any other segment runs the exact sequential nfc_full; its
+// UTF-8 goes to out[tout ...) (segments in order, so rows stay back to back), its byte count to its
+// row's vbytes. A segment whose NFC passes NW_DCAP code points marks its row failed (vfail). Empties
+// the batch.
+__device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, int &nc, int &ns, uint8_t *out, uint32_t &tout,
+                                                uint32_t out_cap, const uint2 *fast) {
+    const int lane = w_lane();
     if (lane == 0) W.seg[ns] = (uint16_t)nc;
     w_sync();
-    // lane per segment: its NFC, its UTF-8 bytes
-    uint32_t pos = 0;
-    bool fail = false;
     uint32_t *dec = W.dec + lane * NW_DCAP;
     for (int base = 0; base < ns; base += 64) {
         const int j = base + lane;
@@ -98,30 +115,32 @@ __device__ __forceinline__ int nfc_row_wave(const uint8_t *in, int len, uint8_t 
                 w = nfc_full<NF_UCD>(W.cps + s, dec, e - s, NW_DCAP, fast);
             }
         }
-        fail = fail || w < 0;
         uint32_t nb = 0;
         for (int k = 0; k < w; ++k) nb += (uint32_t)utf8_len(dec[k]);
         uint32_t t;
-        const uint32_t at = pos + w_exscan(nb, &t);
-        if (at + nb > (uint32_t)out_cap) fail = true;
-        if (!fail) {
+        const uint32_t at = tout + w_exscan(nb, &t);
+        if (act && w >= 0) {
             uint32_t o = at;
             for (int k = 0; k < w; ++k) {
                 uint32_t by[4];
                 const uint32_t cl = utf8_bytes_of(dec[k], by);
-                for (uint32_t q = 0; q < cl; ++q) out[o + q] = (uint8_t)by[q];
+                for (uint32_t q = 0; q < cl; ++q)
+                    if (o + q < out_cap) out[o + q] = (uint8_t)by[q];  // (never short: the caller reserves 3 bytes per byte)
                 o += cl;
             }
+            if (nb) atomicAdd(&W.vbytes[W.segrow[j]], nb);
         }
-        pos += t;
+        if (act && w < 0) W.vfail[W.segrow[j]] = 1;  // (it writes nothing: its row goes on, the text stays intact)
+        tout += t;
+        w_sync();
     }
-    if (w_ballot(fail)) return -1;
-    return (int)pos;
+    nc = 0;
+    ns = 0;
 }
 
 // The fallback kernels' waves (k_bpe_nfc, k_spm_nfc) take the tile kernel's fallback rows
 // i = wave_gid, + nwaves, ... of ta.fb_list in epochs: each row NFC-normalized by the wave
-// (nfc_row_wave) into the epoch's text, back to back, as virtual rows 0..v-1 (their offsets
+// (nfc_decode_row, nfc_flush_batch) into the epoch's text, back to back, as virtual rows 0..v-1 (their offsets
 // E.voffs, their rows NM.vrow); then the tile pipeline with the NFC proof bypassed
 // (tile_front<.., NFCD = true>) encodes the virtual rows R at a time, ids into the epoch's id region
 // (a BPE epoch's pooled merges drained at its end); then each row's ids go to its fallback slot
@@ -178,15 +197,16 @@ __device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint
 }
 
 // The next epoch from fallback-list index i (advanced past the rows taken): returns its rows v.
+// Rows are decoded one at a time into the batch (nfc_decode_row) and its segments normalized
+// together whenever the next row's chars might not fit (nfc_flush_batch), so the lanes stay busy
+// across short rows; the rows' offsets are the scan of their byte counts.
 __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_t &i, uint32_t nl, uint32_t nwaves,
                                                      const NfcEpoch &E, NfcWaveMem &NM, const uint2 *fast, uint32_t *fb3,
                                                      uint32_t *fb3_count) {
     const int lane = w_lane();
-    uint32_t v = 0, tpos = 0;
-    if (lane == 0) {
-        E.voffs[0] = 0;
-        atomicExch(E.vfbc, 0u);  // (ordered with the tile's atomics on it)
-    }
+    uint32_t v = 0, tout = 0, reserve = 0;
+    int nc = 0, ns = 0;
+    if (lane == 0) atomicExch(E.vfbc, 0u);  // (ordered with the tile's atomics on it)
     for (; i < nl && v < NE_VMAX; i += nwaves) {
         const uint64_t r = ta.fb_list[i];
         const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
@@ -194,19 +214,32 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             nfc_fb3(fb3, fb3_count, r);
             continue;
         }
-        if (tpos + 3 * len + 16 > NE_TCAP) break;  // (an empty epoch takes any row: 3 NW_MAXB + 16 < NE_TCAP)
-        const int nb = nfc_row_wave(ta.ra.in + o0, (int)len, E.text + tpos, (int)(NE_TCAP - tpos), NM, fast);
-        if (nb < 0) {
+        if (reserve + 3 * len + 16 > NE_TCAP) break;  // (an empty epoch takes any row: 3 NW_MAXB + 16 < NE_TCAP)
+        if (nc + (int)len > NW_MAXB) nfc_flush_batch(NM, nc, ns, E.text, tout, NE_TCAP, fast);
+        if (lane == 0) {
+            NM.vbytes[v] = 0;
+            NM.vfail[v] = 0;
+        }
+        if (!nfc_decode_row(ta.ra.in + o0, (int)len, v, NM, nc, ns, fast)) {
             nfc_fb3(fb3, fb3_count, r);
             continue;
         }
-        tpos += (uint32_t)nb;
-        if (lane == 0) {
-            NM.vrow[v] = (uint32_t)r;
-            E.voffs[v + 1] = tpos;
-        }
+        reserve += 3 * (uint32_t)len;
+        if (lane == 0) NM.vrow[v] = (uint32_t)r;
         ++v;
     }
+    nfc_flush_batch(NM, nc, ns, E.text, tout, NE_TCAP, fast);
+    // offsets: the scan of the rows' bytes
+    uint32_t pos = 0;
+    for (uint32_t b = 0; b < v; b += 64) {
+        const uint32_t k = b + (uint32_t)lane;
+        const uint32_t nb = k < v ? NM.vbytes[k] : 0u;
+        uint32_t t;
+        const uint32_t at = pos + w_exscan(nb, &t);
+        if (k < v) E.voffs[k] = at;
+        pos += t;
+    }
+    if (lane == 0) E.voffs[v] = pos;
 #ifndef AK_HOST_EMU
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the text and offsets have landed (the tile reads them)
 #endif
@@ -242,7 +275,7 @@ __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEp
         const uint32_t rl = NM.vlen()[j];
         const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
         const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : load_l2(E.vcnt + j);
-        if (rl == 0xFFFFFFFFu || (uint64_t)cnt > mul * len + 2) {
+        if (rl == 0xFFFFFFFFu || NM.vfail[j] || (uint64_t)cnt > mul * len + 2) {
             nfc_fb3(fb3, fb3_count, r);
             continue;
         }
