@@ -52,15 +52,14 @@ __global__ __launch_bounds__(TILE_BLOCK, AK_BPE_TILE_WPE) void k_bpe_tiles(TileA
 // to its fallback slot (ta.ra.out is the second staging half). A row this cannot take (invalid
 // UTF-8, over NW_MAXB bytes, a segment past NW_DCAP, a fallback again in the tile: HF's NFKC changes
 // the text, or ids past its slot) goes on to k_tile_fb through the second list (fb3).
-constexpr int NFC_BLOCK = 256;
+constexpr int NFC_BLOCK = 512;  // 8 waves share the tables (NfcWaveLds: 16.5 KB each)
 
 template <int FLAGS>
 __global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t sfast[SFAST_N];
     __shared__ uint2 fast[FAST_N];
-    __shared__ TileWaveMem wm[NFC_BLOCK / 64];
-    __shared__ NfcWaveMem nm[NFC_BLOCK / 64];
+    __shared__ NfcWaveLds<TileWaveMem> wl[NFC_BLOCK / 64];
     const uint32_t nl = *ta.fb_count;
     if (nl == 0) return;  // uniform: the common case
     for (uint32_t i = threadIdx.x; i < HOT_N; i += NFC_BLOCK) hot_tab[i] = hot_word(hot_cp(i));
@@ -68,7 +67,7 @@ __global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *ebu
         sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     stage_tables(fast, nullptr, nullptr, false);  // (syncs the block)
     const uint32_t wave = threadIdx.x >> 6;
-    bpe_nfc_wave<FLAGS>(ta, ebuf, fb3, fb3_count, hot_tab, sfast, fast, wm[wave], nm[wave],
+    bpe_nfc_wave<FLAGS>(ta, ebuf, fb3, fb3_count, hot_tab, sfast, fast, wl[wave],
                         blockIdx.x * (NFC_BLOCK / 64) + wave, gridDim.x * (NFC_BLOCK / 64));
 }
 

@@ -67,15 +67,14 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_redo(TileArgs ta) {
 
 // the tile kernel's fallback rows in each wave's epochs (ak_tile_spm.h spm_nfc_wave): NFC, the tile
 // variant over the NFC text, the ids to the rows' fallback slots; the rest go on in fb3 (k_spm_tile_fb)
-constexpr int SPM_NFC_BLOCK = 256;
+constexpr int SPM_NFC_BLOCK = 512;  // 8 waves (NfcWaveLds)
 template <int FLAGS>
 __global__ __launch_bounds__(SPM_NFC_BLOCK) void k_spm_nfc(TileArgs ta, uint8_t *ebuf, uint32_t *fb3,
                                                           uint32_t *fb3_count) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
     __shared__ uint2 fast[FAST_N];
-    __shared__ SpmWaveMem wm[SPM_NFC_BLOCK / 64];
-    __shared__ NfcWaveMem nm[SPM_NFC_BLOCK / 64];
+    __shared__ NfcWaveLds<SpmWaveMem> wl[SPM_NFC_BLOCK / 64];
     if (*ta.fb_count == 0) return;  // uniform: the common case
     for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_NFC_BLOCK) {
         const uint32_t cp = hot_cp(i);
@@ -85,7 +84,7 @@ __global__ __launch_bounds__(SPM_NFC_BLOCK) void k_spm_nfc(TileArgs ta, uint8_t 
     }
     stage_tables(fast, nullptr, nullptr, false);  // (syncs the block)
     const uint32_t wave = threadIdx.x >> 6;
-    spm_nfc_wave<FLAGS>(ta, ebuf, fb3, fb3_count, hot_tab, scode, fast, wm[wave], nm[wave],
+    spm_nfc_wave<FLAGS>(ta, ebuf, fb3, fb3_count, hot_tab, scode, fast, wl[wave],
                         blockIdx.x * (SPM_NFC_BLOCK / 64) + wave, gridDim.x * (SPM_NFC_BLOCK / 64));
 }
 

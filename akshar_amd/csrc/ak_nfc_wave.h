@@ -30,18 +30,30 @@ constexpr int NW_DCAP = 32;      // code points of one segment's NFC
 constexpr uint32_t NE_TCAP = 8192;  // their NFC text, bytes
 constexpr uint32_t NE_VMAX = 128;   // rows
 
-struct NfcWaveMem {
+struct NfcWaveMem {  // the NFC scratch: free once an epoch's text is written (the tile's LDS overlays it)
     alignas(16) uint8_t bytes[NW_MAXB + 32];  // a row's UTF-8 (+ slack: decode reads 4-byte windows)
     uint32_t cps[NW_MAXB];                     // the batch's chars (several rows, back to back)
     uint16_t seg[NW_MAXB + 1];                 // the batch's segment starts (+ the end)
     uint8_t segrow[NW_MAXB];                   // ... each one's virtual row
-    uint32_t dec[64 * NW_DCAP];                // lane l's segment output at [l * NW_DCAP ...); after the
-                                               // epoch's NFC: its rows' runs (nfc_epoch_finish)
-    uint32_t vrow[NE_VMAX];                    // the epoch's rows (virtual row v -> row)
-    uint32_t vbytes[NE_VMAX];                  // ... their NFC bytes
-    uint8_t vfail[NE_VMAX];                    // ... a segment's NFC failed (the row goes on to fb3)
-    __device__ uint32_t *vstart() { return dec; }  // virtual row v's run in the epoch's id region
-    __device__ uint32_t *vlen() { return dec + NE_VMAX; }  // ... its length (0xFFFFFFFF: the tile sent it on)
+    uint32_t dec[64 * NW_DCAP];                // lane l's segment output at [l * NW_DCAP ...)
+};
+struct NfcRows {              // the epoch's rows, through its three phases
+    uint32_t vrow[NE_VMAX];   // virtual row v -> row
+    uint32_t vbytes[NE_VMAX]; // its NFC bytes
+    uint32_t vstart[NE_VMAX]; // its run in the epoch's id region
+    uint32_t vlen[NE_VMAX];   // ... and length (0xFFFFFFFF: the tile sent it on)
+    uint8_t vfail[NE_VMAX];   // a segment's NFC failed (the row goes on to fb3)
+};
+// A fallback wave's LDS: the NFC scratch and the tile's buffers in one place (the phases alternate:
+// every tile field is set again at each epoch's first tile), the rows beside them. 16.5 KB for BPE
+// instead of 20 KB: eight waves per CU (one 512-thread block) where four fitted.
+template <class TM>
+struct NfcWaveLds {
+    union {
+        NfcWaveMem n;
+        TM t;
+    };
+    NfcRows rows;
 };
 static_assert(NE_VMAX <= 256, "segrow is a byte");
 static_assert(64 * NW_DCAP >= 2 * NE_VMAX, "the epoch's runs overlay dec");
@@ -95,7 +107,7 @@ __device__ __forceinline__ bool nfc_decode_row(const uint8_t *in, int len, uint3
 // UTF-8 goes to out[tout ...) (segments in order, so rows stay back to back), its byte count to its
 // row's vbytes. A segment whose NFC passes NW_DCAP code points marks its row failed (vfail). Empties
 // the batch.
-__device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, int &nc, int &ns, uint8_t *out, uint32_t &tout,
+__device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &nc, int &ns, uint8_t *out, uint32_t &tout,
                                                 uint32_t out_cap, const uint2 *fast) {
     const int lane = w_lane();
     if (lane == 0) W.seg[ns] = (uint16_t)nc;
@@ -128,9 +140,9 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, int &nc, int &ns,
                     if (o + q < out_cap) out[o + q] = (uint8_t)by[q];  // (never short: the caller reserves 3 bytes per byte)
                 o += cl;
             }
-            if (nb) atomicAdd(&W.vbytes[W.segrow[j]], nb);
+            if (nb) atomicAdd(&R.vbytes[W.segrow[j]], nb);
         }
-        if (act && w < 0) W.vfail[W.segrow[j]] = 1;  // (it writes nothing: its row goes on, the text stays intact)
+        if (act && w < 0) R.vfail[W.segrow[j]] = 1;  // (it writes nothing: its row goes on, the text stays intact)
         tout += t;
         w_sync();
     }
@@ -141,7 +153,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, int &nc, int &ns,
 // The fallback kernels' waves (k_bpe_nfc, k_spm_nfc) take the tile kernel's fallback rows
 // i = wave_gid, + nwaves, ... of ta.fb_list in epochs: each row NFC-normalized by the wave
 // (nfc_decode_row, nfc_flush_batch) into the epoch's text, back to back, as virtual rows 0..v-1 (their offsets
-// E.voffs, their rows NM.vrow); then the tile pipeline with the NFC proof bypassed
+// E.voffs, their rows NfcRows::vrow); then the tile pipeline with the NFC proof bypassed
 // (tile_front<.., NFCD = true>) encodes the virtual rows R at a time, ids into the epoch's id region
 // (a BPE epoch's pooled merges drained at its end); then each row's ids go to its fallback slot
 // (ta.ra.out: the second staging half; BPE offs[r] + 2 r, len + 2 entries; SentencePiece
@@ -201,7 +213,7 @@ __device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint
 // together whenever the next row's chars might not fit (nfc_flush_batch), so the lanes stay busy
 // across short rows; the rows' offsets are the scan of their byte counts.
 __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_t &i, uint32_t nl, uint32_t nwaves,
-                                                     const NfcEpoch &E, NfcWaveMem &NM, const uint2 *fast, uint32_t *fb3,
+                                                     const NfcEpoch &E, NfcWaveMem &NM, NfcRows &R, const uint2 *fast, uint32_t *fb3,
                                                      uint32_t *fb3_count) {
     const int lane = w_lane();
     uint32_t v = 0, tout = 0, reserve = 0;
@@ -215,25 +227,25 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             continue;
         }
         if (reserve + 3 * len + 16 > NE_TCAP) break;  // (an empty epoch takes any row: 3 NW_MAXB + 16 < NE_TCAP)
-        if (nc + (int)len > NW_MAXB) nfc_flush_batch(NM, nc, ns, E.text, tout, NE_TCAP, fast);
+        if (nc + (int)len > NW_MAXB) nfc_flush_batch(NM, R, nc, ns, E.text, tout, NE_TCAP, fast);
         if (lane == 0) {
-            NM.vbytes[v] = 0;
-            NM.vfail[v] = 0;
+            R.vbytes[v] = 0;
+            R.vfail[v] = 0;
         }
         if (!nfc_decode_row(ta.ra.in + o0, (int)len, v, NM, nc, ns, fast)) {
             nfc_fb3(fb3, fb3_count, r);
             continue;
         }
         reserve += 3 * (uint32_t)len;
-        if (lane == 0) NM.vrow[v] = (uint32_t)r;
+        if (lane == 0) R.vrow[v] = (uint32_t)r;
         ++v;
     }
-    nfc_flush_batch(NM, nc, ns, E.text, tout, NE_TCAP, fast);
+    nfc_flush_batch(NM, R, nc, ns, E.text, tout, NE_TCAP, fast);
     // offsets: the scan of the rows' bytes
     uint32_t pos = 0;
     for (uint32_t b = 0; b < v; b += 64) {
         const uint32_t k = b + (uint32_t)lane;
-        const uint32_t nb = k < v ? NM.vbytes[k] : 0u;
+        const uint32_t nb = k < v ? R.vbytes[k] : 0u;
         uint32_t t;
         const uint32_t at = pos + w_exscan(nb, &t);
         if (k < v) E.voffs[k] = at;
@@ -250,12 +262,12 @@ static_assert(3 * NW_MAXB + 16 < NE_TCAP, "an empty epoch takes any row the wave
 
 // Virtual rows [r, r + took) of one tile: their runs in the region (lane l: row r + l; sb: the tile's
 // first position; first: the row's run from there, n: its length; fb: the tile sent the row on).
-__device__ __forceinline__ void nfc_epoch_runs(NfcWaveMem &NM, uint32_t r, int took, uint64_t sb, bool fb, uint32_t first,
+__device__ __forceinline__ void nfc_epoch_runs(NfcRows &R, uint32_t r, int took, uint64_t sb, bool fb, uint32_t first,
                                                uint32_t n) {
     const int lane = w_lane();
     if (lane < took) {
-        NM.vstart()[r + lane] = (uint32_t)sb + (fb ? 0u : first);
-        NM.vlen()[r + lane] = fb ? 0xFFFFFFFFu : n;
+        R.vstart[r + lane] = (uint32_t)sb + (fb ? 0u : first);
+        R.vlen[r + lane] = fb ? 0xFFFFFFFFu : n;
     }
     w_sync();
 }
@@ -263,7 +275,7 @@ __device__ __forceinline__ void nfc_epoch_runs(NfcWaveMem &NM, uint32_t r, int t
 // Each encoded virtual row's ids (its run without STAGE_DEAD entries) -> its fallback slot and count,
 // if they fit the slot; else -> fb3. BPE: slot = offs[r] + 2 r, len + 2 entries (mul 1); SentencePiece
 // 2 offs[r] + 2 r, 2 len + 2 (mul 2).
-__device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEpoch &E, NfcWaveMem &NM, uint32_t v,
+__device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEpoch &E, NfcRows &R, uint32_t v,
                                                  uint32_t mul, uint32_t *fb3, uint32_t *fb3_count) {
     const int lane = w_lane();
 #ifndef AK_HOST_EMU
@@ -271,16 +283,16 @@ __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEp
 #endif
     uint32_t *stage = (uint32_t *)ta.ra.out;
     for (uint32_t j = 0; j < v; ++j) {
-        const uint64_t r = NM.vrow[j];
-        const uint32_t rl = NM.vlen()[j];
+        const uint64_t r = R.vrow[j];
+        const uint32_t rl = R.vlen[j];
         const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
         const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : load_l2(E.vcnt + j);
-        if (rl == 0xFFFFFFFFu || NM.vfail[j] || (uint64_t)cnt > mul * len + 2) {
+        if (rl == 0xFFFFFFFFu || R.vfail[j] || (uint64_t)cnt > mul * len + 2) {
             nfc_fb3(fb3, fb3_count, r);
             continue;
         }
         const uint64_t s0 = mul * o0 + 2 * r;
-        const uint32_t b0 = NM.vstart()[j];
+        const uint32_t b0 = R.vstart[j];
         uint32_t d = 0;
         for (uint32_t k0 = 0; k0 < rl; k0 += 64) {
             const uint32_t k = k0 + (uint32_t)lane;
@@ -301,41 +313,47 @@ __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEp
 // epoch's end (its entries point into the region).
 template <int FLAGS>
 __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count, const uint32_t *H,
-                             const uint16_t *sfast, const uint2 *fast, TileWaveMem &M, NfcWaveMem &NM, uint32_t wave_gid,
+                             const uint16_t *sfast, const uint2 *fast, NfcWaveLds<TileWaveMem> &L, uint32_t wave_gid,
                              uint32_t nwaves) {
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
-    PassClock pc;  // (profiling level 2: the epochs' NFC and slot copies count as "loop")
-    pc.init(ta.passprof != nullptr, M.passacc);
+    TileWaveMem &M = L.t;
+    const bool prof = ta.passprof != nullptr;  // (profiling level 2: the NFC and the slot copies count as "loop")
     uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_CAP;
-    if (lane < POOL_NCLASS) {
-        M.phead[lane] = 0;
-        M.pcnt[lane] = 0;
-    }
-    w_sync();
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
     const TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nl;) {
-        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, NM, fast, fb3, fb3_count);
-        pc.mark(TP_LOOP);
+        const uint64_t g0 = prof ? clock64() : 0;
+        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, L.n, L.rows, fast, fb3, fb3_count);
         if (v == 0) continue;
-        if (lane == 0) M.unext = 0;
+        // the tile's buffers over the NFC scratch: its lasting fields set again (the pool is empty)
+        PassClock pc;
+        pc.init(prof, M.passacc);
+        if (lane < POOL_NCLASS) {
+            M.phead[lane] = 0;
+            M.pcnt[lane] = 0;
+        }
+        if (lane == 0) {
+            M.unext = 0;
+            M.ufbm = 0;
+            if (prof) M.passacc[TP_LOOP] = pc.last - g0;
+        }
         w_sync();
         for (uint32_t r = 0; r < v;) {
             const uint64_t sb = M.unext;
             const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
             const int took = bpe_tile<FLAGS, true>(tl, r, re, H, sfast, M, pool, pc);
             const bool in = lane < took;
-            nfc_epoch_runs(NM, r, took, sb, in && M.fb[lane], in ? M.rowop[lane] : 0u,
+            nfc_epoch_runs(L.rows, r, took, sb, in && M.fb[lane], in ? M.rowop[lane] : 0u,
                            in ? M.rowop[lane + 1] - M.rowop[lane] : 0u);
             r += (uint32_t)took;
         }
         pool_drain(tl, M, pool, 1u, pc);  // every miss of the epoch merged
         pc.mark(TP_FBE);
-        nfc_epoch_finish(ta, E, NM, v, 1u, fb3, fb3_count);
+        nfc_epoch_finish(ta, E, L.rows, v, 1u, fb3, fb3_count);
         pc.mark(TP_LOOP);
+        pc.flush(ta.passprof);
     }
-    pc.flush(ta.passprof);
 }
 
 }  // namespace ak

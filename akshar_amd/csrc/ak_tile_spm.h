@@ -1056,21 +1056,24 @@ __device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint1
 // fallback slot; the rows it cannot take go on to the one-lane kernel (fb3).
 template <int FLAGS>
 __device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count, const uint32_t *H,
-                             const uint16_t *scode, const uint2 *fast, SpmWaveMem &M, NfcWaveMem &NM, uint32_t wave_gid,
+                             const uint16_t *scode, const uint2 *fast, NfcWaveLds<SpmWaveMem> &L, uint32_t wave_gid,
                              uint32_t nwaves) {
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
-    PassClock pc;  // (profiling level 2: the epochs' NFC and slot copies count as "loop")
-    pc.init(ta.passprof != nullptr, M.passacc);
+    SpmWaveMem &M = L.t;
+    const bool prof = ta.passprof != nullptr;  // (profiling level 2: the NFC and the slot copies count as "loop")
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
     const TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nl;) {
-        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, NM, fast, fb3, fb3_count);
-        pc.mark(TP_LOOP);
+        const uint64_t g0 = prof ? clock64() : 0;
+        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, L.n, L.rows, fast, fb3, fb3_count);
         if (v == 0) continue;
+        PassClock pc;  // (the tile's buffers over the NFC scratch: its lasting fields set again)
+        pc.init(prof, M.passacc);
         if (lane == 0) {
             M.unext = 0;
             M.ufbm = 0;
+            if (prof) M.passacc[TP_LOOP] = pc.last - g0;
         }
         w_sync();
         for (uint32_t r = 0; r < v;) {
@@ -1078,13 +1081,13 @@ __device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
             const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
             const int took = spm_tile<FLAGS, SpmWaveMem, true>(tl, r, re, H, scode, M, nullptr, pc, true);
             const bool in = lane < took;
-            nfc_epoch_runs(NM, r, took, sb, in && M.fb[lane], in ? M.rowfirst[lane] : 0u, in ? M.rowcnt[lane] : 0u);
+            nfc_epoch_runs(L.rows, r, took, sb, in && M.fb[lane], in ? M.rowfirst[lane] : 0u, in ? M.rowcnt[lane] : 0u);
             r += (uint32_t)took;
         }
-        nfc_epoch_finish(ta, E, NM, v, 2u, fb3, fb3_count);
+        nfc_epoch_finish(ta, E, L.rows, v, 2u, fb3, fb3_count);
         pc.mark(TP_LOOP);
+        pc.flush(ta.passprof);
     }
-    pc.flush(ta.passprof);
 }
 
 }  // namespace ak

@@ -314,13 +314,13 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     uint32_t fb3n = 0;
     if (!getenv("AK_NO_NFC_WAVE")) {
         std::vector<uint8_t> ebuf((size_t)g_waves * NE_BYTES);
-        std::vector<NfcWaveMem> NM(g_waves);
+        std::vector<NfcWaveLds<TileWaveMem>> NL(g_waves);
         TileArgs tn = ta;
         tn.passprof = nullptr;
         tn.ra.out = stage.data() + half;
         tn.ra.cap = half;
         run_waves([&](int w) {
-            bpe_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, sfast.data(), fast, M[w], NM[w], (uint32_t)w,
+            bpe_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, sfast.data(), fast, NL[w], (uint32_t)w,
                             (uint32_t)g_waves);
         });
         if (err) return -1;
@@ -438,14 +438,14 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         static uint2 sfastp[FAST_N];
         for (uint32_t i = 0; i < FAST_N; ++i) sfastp[i] = prop_global(i);
         std::vector<uint8_t> ebuf((size_t)g_waves * NE_BYTES);
-        std::vector<NfcWaveMem> NM(g_waves);
+        std::vector<NfcWaveLds<SpmWaveMem>> NL(g_waves);
         std::vector<uint32_t> fb3(n);
         uint32_t fb3n = 0;
         TileArgs tn = ta;
         tn.passprof = nullptr;
         tn.ra.out = stage.data() + half;
         run_waves([&](int w) {
-            spm_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, scode, sfastp, M[w], NM[w], (uint32_t)w,
+            spm_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, scode, sfastp, NL[w], (uint32_t)w,
                             (uint32_t)g_waves);
         });
         if (err) return -1;
