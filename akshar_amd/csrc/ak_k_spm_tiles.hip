@@ -46,14 +46,15 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
                                 gridDim.x * (SPM_TILE_BLOCK / 64));
 }
 
-// rows the word pool sent back (ak_tile_spm.h spm_redo_wave): wave per row, same LDS as k_spm_tiles
+// rows the word pool sent back (ak_tile_spm.h spm_redo_wave): the waves' epochs, the tile variant
+constexpr int SPM_REDO_BLOCK = 512;  // 8 waves: the grid's waves = k_spm_nfc's (the same epoch buffers)
 template <int FLAGS>
-__global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_redo(TileArgs ta) {
+__global__ __launch_bounds__(SPM_REDO_BLOCK) void k_spm_redo(TileArgs ta, uint8_t *ebuf) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
-    __shared__ SpmWaveMem wm[SPM_TILE_BLOCK / 64];
+    __shared__ SpmRedoLds wm[SPM_REDO_BLOCK / 64];
     if (*ta.redo_count == 0) return;  // uniform: the common case
-    for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_REDO_BLOCK) {
         const uint32_t cp = hot_cp(i);
         hot_tab[i] = hot_word(cp);
         const uint32_t c = spm_code(ta.ra.spm, cp);
@@ -61,8 +62,8 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_redo(TileArgs ta) {
     }
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
-    spm_redo_wave<FLAGS>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
-                         gridDim.x * (SPM_TILE_BLOCK / 64));
+    spm_redo_wave<FLAGS>(ta, ebuf, hot_tab, scode, wm[wave], blockIdx.x * (SPM_REDO_BLOCK / 64) + wave,
+                         gridDim.x * (SPM_REDO_BLOCK / 64));
 }
 
 // the tile kernel's fallback rows in each wave's epochs (ak_tile_spm.h spm_nfc_wave): NFC, the tile
@@ -286,18 +287,19 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     TileArgs tfb = ta;
     tfb.ra.out = w->stage + half;
     tfb.ra.cap = half;
-    k_spm_redo<3><<<(unsigned)num_cus() * (unsigned)bpc, SPM_TILE_BLOCK, 0, st>>>(tfb);
+    static_assert(SPM_REDO_BLOCK == SPM_NFC_BLOCK, "k_spm_redo and k_spm_nfc share the epoch buffers");
+    const unsigned ngrid = (unsigned)num_cus();
+    const uint64_t nw = (uint64_t)ngrid * (SPM_NFC_BLOCK / 64);
+    if (w->cap_nfc < nw) {
+        (void)hipFree(w->nfc_buf);
+        w->nfc_buf = nullptr;
+        w->cap_nfc = 0;
+        HIP_TRY(hipMalloc(&w->nfc_buf, nw * NE_BYTES));
+        w->cap_nfc = nw;
+    }
+    k_spm_redo<3><<<ngrid, SPM_REDO_BLOCK, 0, st>>>(tfb, w->nfc_buf);
     HIP_TRY(hipGetLastError());
     if (!getenv("AK_NO_NFC_WAVE")) {  // (development aid: the one-lane path for every fallback row)
-        const unsigned ngrid = (unsigned)num_cus();
-        const uint64_t nw = (uint64_t)ngrid * (SPM_NFC_BLOCK / 64);
-        if (w->cap_nfc < nw) {
-            (void)hipFree(w->nfc_buf);
-            w->nfc_buf = nullptr;
-            w->cap_nfc = 0;
-            HIP_TRY(hipMalloc(&w->nfc_buf, nw * NE_BYTES));
-            w->cap_nfc = nw;
-        }
         if (w->cap_fb3 < a0.n) {
             (void)hipFree(w->fb3);
             w->fb3 = nullptr;

@@ -260,6 +260,40 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
 }
 static_assert(3 * NW_MAXB + 16 < NE_TCAP, "an empty epoch takes any row the wave normalizes");
 
+// The same epoch for rows that need no NFC (SentencePiece's send-backs, k_spm_redo): list[i], +
+// nwaves, ... copied back to back (a row over NW_MAXB bytes, which no tile buffer holds, goes
+// straight to fbl).
+__device__ __forceinline__ uint32_t copy_epoch_gather(const TileArgs &ta, const uint32_t *list, uint32_t &i, uint32_t nl,
+                                                      uint32_t nwaves, const NfcEpoch &E, NfcRows &R, uint32_t *fbl,
+                                                      uint32_t *fbc) {
+    const int lane = w_lane();
+    uint32_t v = 0, tpos = 0;
+    if (lane == 0) atomicExch(E.vfbc, 0u);
+    for (; i < nl && v < NE_VMAX; i += nwaves) {
+        const uint64_t r = list[i];
+        const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
+        if (len > (uint64_t)NW_MAXB) {
+            nfc_fb3(fbl, fbc, r);
+            continue;
+        }
+        if (tpos + len + 16 > NE_TCAP) break;
+        for (uint32_t k = (uint32_t)lane; k < (uint32_t)len; k += 64) E.text[tpos + k] = ta.ra.in[o0 + k];
+        if (lane == 0) {
+            R.vrow[v] = (uint32_t)r;
+            R.vfail[v] = 0;
+            E.voffs[v] = tpos;
+        }
+        tpos += (uint32_t)len;
+        ++v;
+    }
+    if (lane == 0) E.voffs[v] = tpos;
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    w_sync();
+    return v;
+}
+
 // Virtual rows [r, r + took) of one tile: their runs in the region (lane l: row r + l; sb: the tile's
 // first position; first: the row's run from there, n: its length; fb: the tile sent the row on).
 __device__ __forceinline__ void nfc_epoch_runs(NfcRows &R, uint32_t r, int took, uint64_t sb, bool fb, uint32_t first,

@@ -1022,30 +1022,45 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
     pc.flush(ta.passprof);
 }
 
-// Rows a pooled word's margin test sent back (k_spm_redo): each is encoded again as a tile of its own
-// with the pool off, so its words run in the tile, the close call triggers pass V2 and the row is
-// solved from the carried base; the ids go to the row's fallback slot (ta.ra.out is the second
-// staging half) and its count replaces the one pass F wrote. Its span in the unit run is left as it
-// was (k_unit_copy_spm steps over it).
+// Rows a pooled word's margin test sent back (k_spm_redo), in the wave's epochs (ak_nfc_wave.h):
+// copied back to back (copy_epoch_gather), encoded by the tile variant R rows at a time (every word
+// solved in its tile, the carried base for close calls) into the epoch's id region, then each row's
+// ids to its fallback slot; a row the tile variant cannot take (over its buffer) joins the fallback
+// list (k_spm_nfc and the one-lane kernel read it next).
+struct SpmRedoLds {
+    SpmWaveMem t;
+    NfcRows rows;
+};
+
 template <int FLAGS>
-__device__ void spm_redo_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, SpmWaveMem &M, uint32_t wave_gid,
-                              uint32_t nwaves) {
+__device__ void spm_redo_wave(const TileArgs &ta, uint8_t *ebuf, const uint32_t *H, const uint16_t *scode, SpmRedoLds &L,
+                              uint32_t wave_gid, uint32_t nwaves) {
+    const int lane = w_lane();
+    SpmWaveMem &M = L.t;
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
-    if (w_lane() < SP_NCLASS) {
-        M.phead[w_lane()] = 0;
-        M.pcnt[w_lane()] = 0;
-    }
-    w_sync();
     const uint32_t nredo = *ta.redo_count;
-    for (uint32_t i = wave_gid; i < nredo; i += nwaves) {
-        const uint64_t r = ta.redo_list[i];
-        if (w_lane() == 0) {
-            M.unext = 2 * ta.ra.offs[r] + 2 * r;
+    const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
+    const TileArgs tl = nfc_epoch_args(ta, E);
+    for (uint32_t i = wave_gid; i < nredo;) {
+        const uint32_t v = copy_epoch_gather(ta, ta.redo_list, i, nredo, nwaves, E, L.rows, ta.fb_list, ta.fb_count);
+        pc.mark(TP_LOOP);
+        if (v == 0) continue;
+        if (lane == 0) {
+            M.unext = 0;
             M.ufbm = 0;
         }
         w_sync();
-        (void)spm_tile<FLAGS, SpmWaveMem>(ta, r, r + 1, H, scode, M, nullptr, pc, true);
+        for (uint32_t r = 0; r < v;) {
+            const uint64_t sb = M.unext;
+            const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
+            const int took = spm_tile<FLAGS, SpmWaveMem>(tl, r, re, H, scode, M, nullptr, pc, true);
+            const bool in = lane < took;
+            nfc_epoch_runs(L.rows, r, took, sb, in && M.fb[lane], in ? M.rowfirst[lane] : 0u, in ? M.rowcnt[lane] : 0u);
+            r += (uint32_t)took;
+        }
+        nfc_epoch_finish(ta, E, L.rows, v, 2u, ta.fb_list, ta.fb_count);
+        pc.mark(TP_LOOP);
     }
     pc.flush(ta.passprof);
 }

@@ -427,11 +427,13 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     }
     g_last_redo = nredo;
     if (getenv("AK_EMU_DUMP_REDO")) { for (uint32_t i = 0; i < nredo; ++i) fprintf(stderr, "redo row %u\n", redo[i]); }
-    {  // as k_spm_redo: the rows the word pool sent back, into their fallback slots
+    {  // as k_spm_redo: the rows the word pool sent back, the waves' epochs, into their fallback slots
         TileArgs tr = ta;
         tr.passprof = nullptr;
         tr.ra.out = stage.data() + half;
-        run_waves([&](int w) { spm_redo_wave<3>(tr, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
+        std::vector<uint8_t> ebuf((size_t)g_waves * NE_BYTES);
+        std::vector<SpmRedoLds> RL(g_waves);
+        run_waves([&](int w) { spm_redo_wave<3>(tr, ebuf.data(), hot_tab, scode, RL[w], (uint32_t)w, (uint32_t)g_waves); });
     }
     const uint32_t tile_fb = fbn;  // the tile kernel's fallback rows (last_fallback_rows)
     if (!getenv("AK_NO_NFC_WAVE")) {  // as k_spm_nfc: the waves' epochs, NFC then the tile
