@@ -58,48 +58,16 @@ struct NfcWaveLds {
 static_assert(NE_VMAX <= 256, "segrow is a byte");
 static_assert(64 * NW_DCAP >= 2 * NE_VMAX, "the epoch's runs overlay dec");
 
-// Decode the row in[0..len) (global) into the batch: its chars at W.cps[nc ...), its segments (its
-// first char and every NFC-stable char) at W.seg[ns ...) with virtual row v. Returns false for
-// invalid UTF-8 (nc, ns unchanged: the row goes on); else advances nc and ns.
-__device__ __forceinline__ bool nfc_decode_row(const uint8_t *in, int len, uint32_t v, NfcWaveMem &W, int &nc, int &ns,
-                                               const uint2 *fast) {
-    const int lane = w_lane();
-    for (int i = lane; i < len + 8; i += 64) W.bytes[i] = i < len ? in[i] : 0u;
-    w_sync();
-    int c = nc;
-    uint32_t tot_len = 0;
-    bool bad = false;
-    for (int base = 0; base < len; base += 64) {
-        const int p = base + lane;
-        const bool inb = p < len;
-        const uint32_t b = inb ? W.bytes[p] : 0u;
-        const bool lead = inb && (b & 0xC0u) != 0x80u;
-        const uint32_t cp = lead ? decode_word(lds_word(W.bytes, p), p, len) : 0u;
-        bad = bad || (lead && cp == 0xFFFFFFFFu);
-        const uint64_t LM = w_ballot(lead);
-        if (lead) W.cps[c + (int)w_rank(LM)] = cp;
-        uint32_t t;
-        (void)w_exscan(lead && cp != 0xFFFFFFFFu ? (uint32_t)utf8_len(cp) : 0u, &t);
-        tot_len += t;
-        c += w_popc(LM);
+// The last lane j whose key[j] <= p (keys nondecreasing over the lanes, key[0] <= p): a binary
+// search over the lanes by shuffles (every lane active).
+__device__ __forceinline__ int w_last_le(uint32_t key, uint32_t p) {
+    int lo = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t k = w_shfl(key, lo + step);
+        if (k <= p) lo += step;
     }
-    if (w_ballot(bad) || tot_len != (uint32_t)len) return false;  // invalid or stray continuation bytes
-    w_sync();
-    int s = ns;
-    for (int base = nc; base < c; base += 64) {
-        const int i = base + lane;
-        const bool st = i < c && (i == nc || p_stable(prop(fast, W.cps[i])));
-        const uint64_t SM = w_ballot(st);
-        if (st) {
-            W.seg[s + (int)w_rank(SM)] = (uint16_t)i;
-            W.segrow[s + (int)w_rank(SM)] = (uint8_t)v;
-        }
-        s += w_popc(SM);
-    }
-    nc = c;
-    ns = s;
-    w_sync();
-    return true;
+    return lo;
 }
 
 // NFC of the batch's segments, a lane each (64 per round, whatever rows they belong to): a lone char
@@ -118,7 +86,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
         const bool act = j < ns;
         const int s = act ? (int)W.seg[j] : 0, e = act ? (int)W.seg[j + 1] : 0;
         int w = 0;
-        if (act) {
+        if (act && !R.vfail[W.segrow[j]]) {  // (a row found invalid while decoding has no text)
             const uint32_t c0 = W.cps[s];
             if (e - s == 1 && !p_decomp(prop(fast, c0)) && c0 - H_SBASE >= H_SCOUNT) {
                 dec[0] = c0;
@@ -209,38 +177,111 @@ __device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint
 }
 
 // The next epoch from fallback-list index i (advanced past the rows taken): returns its rows v.
-// Rows are decoded one at a time into the batch (nfc_decode_row) and its segments normalized
-// together whenever the next row's chars might not fit (nfc_flush_batch), so the lanes stay busy
-// across short rows; the rows' offsets are the scan of their byte counts.
+// Batches of rows are taken 64 list entries at a time: lane k loads entry i + k nwaves and its
+// offsets (one latency for 64 rows), scans give each row its place in the batch's bytes, and the
+// longest prefix that fits the batch (NW_MAXB bytes), the epoch's rows and its text reserve joins
+// (a row over NW_MAXB bytes goes to fb3). The batch's bytes are copied lane per byte (each byte's row
+// by a search over the lanes), decoded 64 at a time (a lead byte's row sums its sequence lengths: a
+// row is valid UTF-8 iff they sum to its bytes and every sequence decodes), its chars tagged with
+// their row and cut into segments, and the segments normalized together (nfc_flush_batch). The
+// rows' offsets in the epoch's text are the scan of their NFC byte counts.
 __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_t &i, uint32_t nl, uint32_t nwaves,
-                                                     const NfcEpoch &E, NfcWaveMem &NM, NfcRows &R, const uint2 *fast, uint32_t *fb3,
-                                                     uint32_t *fb3_count) {
+                                                     const NfcEpoch &E, NfcWaveMem &S, NfcRows &R, const uint2 *fast,
+                                                     uint32_t *fb3, uint32_t *fb3_count) {
     const int lane = w_lane();
     uint32_t v = 0, tout = 0, reserve = 0;
-    int nc = 0, ns = 0;
     if (lane == 0) atomicExch(E.vfbc, 0u);  // (ordered with the tile's atomics on it)
-    for (; i < nl && v < NE_VMAX; i += nwaves) {
-        const uint64_t r = ta.fb_list[i];
-        const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
-        if (len > (uint64_t)NW_MAXB) {
-            nfc_fb3(fb3, fb3_count, r);
-            continue;
+    while (i < nl && v < NE_VMAX) {
+        const uint64_t idx = (uint64_t)i + (uint64_t)lane * nwaves;
+        const bool valid = idx < nl;
+        uint64_t r = 0, o0 = 0, len = 0;
+        if (valid) {
+            r = ta.fb_list[idx];
+            o0 = ta.ra.offs[r];
+            len = ta.ra.offs[r + 1] - o0;
         }
-        if (reserve + 3 * len + 16 > NE_TCAP) break;  // (an empty epoch takes any row: 3 NW_MAXB + 16 < NE_TCAP)
-        if (nc + (int)len > NW_MAXB) nfc_flush_batch(NM, R, nc, ns, E.text, tout, NE_TCAP, fast);
-        if (lane == 0) {
-            R.vbytes[v] = 0;
-            R.vfail[v] = 0;
+        const bool longrow = valid && len > (uint64_t)NW_MAXB;
+        const uint32_t a = valid && !longrow ? (uint32_t)len : 0u;
+        const uint32_t c = valid && !longrow ? 1u : 0u;
+        uint32_t tt;
+        const uint32_t B = w_exscan(a, &tt) + a;  // inclusive: bytes, rows
+        const uint32_t C = w_exscan(c, &tt) + c;
+        const bool ok = valid && (longrow || (B <= (uint32_t)NW_MAXB && v + C <= NE_VMAX && reserve + 3 * B + 16 <= NE_TCAP));
+        const uint64_t OK = w_ballot(ok);
+        const uint32_t kstop = ~OK ? (uint32_t)__builtin_ctzll(~OK) : 64u;  // the prefix taken
+        if (kstop == 0) break;  // the epoch is full (an empty one takes any row)
+        const bool take = (uint32_t)lane < kstop;
+        const uint64_t LM = w_ballot(take && longrow);
+        if (LM) {  // rows no tile buffer holds
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(fb3_count, (uint32_t)w_popc(LM));
+            base = w_bcast(base, 0);
+            if (take && longrow) fb3[base + w_rank(LM)] = (uint32_t)r;
         }
-        if (!nfc_decode_row(ta.ra.in + o0, (int)len, v, NM, nc, ns, fast)) {
-            nfc_fb3(fb3, fb3_count, r);
-            continue;
+        const bool row_in = take && !longrow;
+        const uint32_t vi = v + C - 1;  // the row's virtual row
+        const uint32_t start = B - a;   // ... and its first byte in the batch
+        const uint32_t key = take ? start : 0xFFFFFFFFu;
+        const uint32_t nrows = w_bcast(C, (int)kstop - 1), blen = w_bcast(B, (int)kstop - 1);
+        if (row_in) {
+            R.vrow[vi] = (uint32_t)r;
+            R.vbytes[vi] = 0;
+            R.vfail[vi] = 0;
         }
-        reserve += 3 * (uint32_t)len;
-        if (lane == 0) R.vrow[v] = (uint32_t)r;
-        ++v;
+        // the batch's bytes (+ zero slack: decode reads 4-byte windows)
+        for (uint32_t base = 0; base < blen + 8; base += 64) {
+            const uint32_t p = base + (uint32_t)lane;
+            const int j = w_last_le(key, p < blen ? p : 0u);
+            const uint64_t src = w_shfl(o0, j) + (uint64_t)(p - w_shfl(start, j));
+            if (p < blen) S.bytes[p] = ta.ra.in[src];
+            else if (p < (uint32_t)NW_MAXB + 32) S.bytes[p] = 0;
+        }
+        w_sync();
+        // decode: chars tagged with their virtual row (bits 24-30) and row start (bit 31)
+        int nc = 0;
+        for (uint32_t base = 0; base < blen; base += 64) {
+            const uint32_t p = base + (uint32_t)lane;
+            const bool inb = p < blen;
+            const uint32_t b = inb ? S.bytes[p] : 0u;
+            const bool lead = inb && (b & 0xC0u) != 0x80u;
+            const uint32_t cp = lead ? decode_word(lds_word(S.bytes, p), (int)p, (int)blen) : 0u;
+            const int j = w_last_le(key, inb ? p : 0u);
+            const uint32_t rv = w_shfl(vi, j), rs = w_shfl(start, j);
+            if (lead) {
+                if (cp == 0xFFFFFFFFu) R.vfail[rv] = 1;
+                else atomicAdd(&R.vbytes[rv], (uint32_t)utf8_len(cp));
+            }
+            const uint64_t LMk = w_ballot(lead);
+            if (lead)
+                S.cps[nc + (int)w_rank(LMk)] = (cp == 0xFFFFFFFFu ? 0xFFFDu : cp) | (rv << 24) | (p == rs ? 0x80000000u : 0u);
+            nc += w_popc(LMk);
+        }
+        w_sync();
+        if (row_in && R.vbytes[vi] != a) R.vfail[vi] = 1;  // stray continuation bytes, a sequence past the row
+        w_sync();
+        if (row_in) R.vbytes[vi] = 0;  // (from here: the row's NFC bytes)
+        // segments: a row's first char and every NFC-stable char
+        int ns = 0;
+        for (int base = 0; base < nc; base += 64) {
+            const int ci = base + lane;
+            const bool in = ci < nc;
+            const uint32_t x = in ? S.cps[ci] : 0u;
+            const uint32_t cp = x & 0xFFFFFFu;
+            const bool st = in && ((x >> 31) || p_stable(prop(fast, cp)));
+            const uint64_t SM = w_ballot(st);
+            if (st) {
+                S.seg[ns + (int)w_rank(SM)] = (uint16_t)ci;
+                S.segrow[ns + (int)w_rank(SM)] = (uint8_t)((x >> 24) & 0x7Fu);
+            }
+            if (in) S.cps[ci] = cp;
+            ns += w_popc(SM);
+        }
+        w_sync();
+        nfc_flush_batch(S, R, nc, ns, E.text, tout, NE_TCAP, fast);
+        v += nrows;
+        reserve += 3 * blen;
+        i += kstop * nwaves;
     }
-    nfc_flush_batch(NM, R, nc, ns, E.text, tout, NE_TCAP, fast);
     // offsets: the scan of the rows' bytes
     uint32_t pos = 0;
     for (uint32_t b = 0; b < v; b += 64) {

@@ -224,3 +224,29 @@ def test_wave_nfc_rows_that_nfc_lengthens(bpe_model, spm_model):
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
     ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_wave_nfc_batches_with_invalid_rows(bpe_model, spm_model):
+    """The fallback waves decode several rows' bytes as one batch: invalid rows (a sequence cut at
+    the row's end, stray continuation bytes, bytes no sequence has) side by side with rows NFC changes,
+    empty rows and rows starting with a combining mark, in random order: the invalid ones go on to
+    the one-lane kernel, whatever their neighbours, and every row equals the oracle (BPE and
+    SentencePiece), statuses included."""
+    rng = np.random.default_rng(11)
+    good = ["Ḳ́x", "ạ́b", "é ऩि", "́lead mark", "", "क़ ড় x", "Ạ̊", "ok ḍ̇",
+            "क़़", "x" * 70 + "́"]
+    bad = [b"\xe0\xa4", b"\x80lead", b"\xc3(", b"ok \xe0", b"\xff\xfeabc", b"a\x80b", b"\xe0\xa4\x95\x80",
+           b"mid\xf4\x90\x80\x80end"]
+    raw = []
+    for _ in range(400):
+        raw.append(bad[rng.integers(len(bad))] if rng.random() < 0.3 else good[rng.integers(len(good))].encode())
+    buf, offs = _raw_rows(raw)
+    ids, oo, st = emu.bpe_tiles(emu.Model(bpe=bpe_model), buf, offs, rows=8)
+    assert emu.last_nfc_rows() > 100
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)
+    ref_st = [1 if isinstance(x, bytes) and x in bad else 0 for x in raw]
+    assert st.tolist() == ref_st
+    ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)
