@@ -70,6 +70,82 @@ __device__ __forceinline__ int w_last_le(uint32_t key, uint32_t p) {
     return lo;
 }
 
+// NFC of one segment (its chars in[0..n), a lane's own) into dec[0..NW_DCAP): the result of ak_dev.h
+// nfc_full<NF_UCD> (canonical decomposition, stable ccc sort, canonical composition) with each
+// char's properties looked up once (its ccc and "second of a primary composite" bit kept beside it:
+// cp | second << 22 | ccc << 24) and the composition table (a binary search in global memory) asked
+// only when the starter is a composition first and the char a second, unblocked — the pairs the
+// table holds (tools/gen_tables.py: comp_first / comp_second, Hangul L, LV, V, T). Inlined, so its
+// LDS accesses stay LDS accesses. Returns the length, or -1 past NW_DCAP.
+__device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n, const uint2 *fast) {
+    constexpr uint32_t CP = 0x1FFFFFu, SECOND = 1u << 22;
+    auto ent = [&](uint32_t cp, uint2 pr) { return cp | (p_second(pr) ? SECOND : 0u) | ((uint32_t)p_ccc(pr) << 24); };
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const uint32_t cp = in[i];
+        if (cp - H_SBASE < H_SCOUNT) {  // Hangul syllable: L V (T), algorithmically
+            const uint32_t x = cp - H_SBASE;
+            if (m + 3 > NW_DCAP) return -1;
+            dec[m++] = H_LBASE + x / H_NCOUNT;
+            dec[m++] = (H_VBASE + (x % H_NCOUNT) / H_TCOUNT) | SECOND;
+            if (x % H_TCOUNT) dec[m++] = (H_TBASE + x % H_TCOUNT) | SECOND;
+            continue;
+        }
+        const uint2 pr = prop(fast, cp);
+        const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
+        if (m + (int)(len ? len : 1) > NW_DCAP) return -1;
+        if (!len) {
+            dec[m++] = ent(cp, pr);
+        } else {
+            for (uint32_t k = 0; k < len; ++k) {
+                const uint32_t d = AK_UT_DECOMP[idx + k];
+                dec[m++] = ent(d, prop(fast, d));
+            }
+        }
+    }
+    for (int i = 1; i < m; ++i) {  // canonical ordering: stable insertion sort of non-starter runs
+        const uint32_t x = dec[i];
+        const uint32_t c = x >> 24;
+        if (c == 0) continue;
+        int j = i;
+        while (j > 0 && (dec[j - 1] >> 24) > c) {
+            dec[j] = dec[j - 1];
+            --j;
+        }
+        dec[j] = x;
+    }
+    int starter = -1, w = 0;
+    uint32_t st = 0, lastc = 0;
+    bool first = false;  // st is the first char of some primary composite
+    for (int i = 0; i < m; ++i) {
+        const uint32_t x = dec[i];
+        const uint32_t ch = x & CP, c = x >> 24;
+        if (starter >= 0 && first && (x & SECOND) && (lastc < c || lastc == 0)) {
+            const uint32_t comp = compose_pair<NF_UCD>(st, ch);
+            if (comp) {
+                st = comp;
+                dec[starter] = comp;
+                first = comp - H_SBASE < H_SCOUNT ? (comp - H_SBASE) % H_TCOUNT == 0 : ((prop(fast, comp).x >> 23) & 1u);
+                continue;
+            }
+        }
+        if (i == 0 && c != 0) {
+            lastc = 256;  // a leading non-starter blocks composition
+            dec[w++] = ch;
+            continue;
+        }
+        if (c == 0) {
+            starter = w;
+            st = ch;
+            first = ch - H_SBASE < H_SCOUNT ? (ch - H_SBASE) % H_TCOUNT == 0
+                                            : (ch - H_LBASE < H_LCOUNT || ((prop(fast, ch).x >> 23) & 1u));
+        }
+        lastc = c;
+        dec[w++] = ch;
+    }
+    return w;
+}
+
 // NFC of the batch's segments, a lane each (64 per round, whatever rows they belong to): a lone char
 // that does not decompose is itself, any other segment runs the exact sequential nfc_full; its
 // UTF-8 goes to out[tout ...) (segments in order, so rows stay back to back), its byte count to its
@@ -92,7 +168,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
                 dec[0] = c0;
                 w = 1;
             } else {
-                w = nfc_full<NF_UCD>(W.cps + s, dec, e - s, NW_DCAP, fast);
+                w = nfc_seg(W.cps + s, dec, e - s, fast);
             }
         }
         uint32_t nb = 0;
@@ -176,6 +252,21 @@ __device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint
     if (w_lane() == 0) fb3[atomicAdd(fb3_count, 1u)] = (uint32_t)r;
 }
 
+#ifndef AK_NFC_SPLIT
+#define AK_NFC_SPLIT 0  // development aid (a build variant): the gather's phases' wave-cycles into the
+#endif              // tile counters (profiling level 2; the waves' own pass clocks off)
+#if AK_NFC_SPLIT
+#define NFC_SPLIT_MARK(k)                                                                                  \
+    do {                                                                                                   \
+        const uint64_t now_ = clock64();                                                                   \
+        if (ta.passprof && lane == 0) atomicAdd((unsigned long long *)(ta.passprof + T_NPASS + (k)),       \
+                                                (unsigned long long)(now_ - split_t));                     \
+        split_t = now_;                                                                                    \
+    } while (0)
+#else
+#define NFC_SPLIT_MARK(k) do {} while (0)
+#endif
+
 // The next epoch from fallback-list index i (advanced past the rows taken): returns its rows v.
 // Batches of rows are taken 64 list entries at a time: lane k loads entry i + k nwaves and its
 // offsets (one latency for 64 rows), scans give each row its place in the batch's bytes, and the
@@ -190,6 +281,9 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
                                                      uint32_t *fb3, uint32_t *fb3_count) {
     const int lane = w_lane();
     uint32_t v = 0, tout = 0, reserve = 0;
+#if AK_NFC_SPLIT
+    uint64_t split_t = clock64();
+#endif
     if (lane == 0) atomicExch(E.vfbc, 0u);  // (ordered with the tile's atomics on it)
     while (i < nl && v < NE_VMAX) {
         const uint64_t idx = (uint64_t)i + (uint64_t)lane * nwaves;
@@ -228,6 +322,7 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             R.vbytes[vi] = 0;
             R.vfail[vi] = 0;
         }
+        NFC_SPLIT_MARK(0);
         // the batch's bytes (+ zero slack: decode reads 4-byte windows)
         for (uint32_t base = 0; base < blen + 8; base += 64) {
             const uint32_t p = base + (uint32_t)lane;
@@ -237,6 +332,7 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             else if (p < (uint32_t)NW_MAXB + 32) S.bytes[p] = 0;
         }
         w_sync();
+        NFC_SPLIT_MARK(1);
         // decode: chars tagged with their virtual row (bits 24-30) and row start (bit 31)
         int nc = 0;
         for (uint32_t base = 0; base < blen; base += 64) {
@@ -260,6 +356,7 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
         if (row_in && R.vbytes[vi] != a) R.vfail[vi] = 1;  // stray continuation bytes, a sequence past the row
         w_sync();
         if (row_in) R.vbytes[vi] = 0;  // (from here: the row's NFC bytes)
+        NFC_SPLIT_MARK(2);
         // segments: a row's first char and every NFC-stable char
         int ns = 0;
         for (int base = 0; base < nc; base += 64) {
@@ -277,7 +374,9 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             ns += w_popc(SM);
         }
         w_sync();
+        NFC_SPLIT_MARK(3);
         nfc_flush_batch(S, R, nc, ns, E.text, tout, NE_TCAP, fast);
+        NFC_SPLIT_MARK(4);
         v += nrows;
         reserve += 3 * blen;
         i += kstop * nwaves;
@@ -393,7 +492,7 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
     TileWaveMem &M = L.t;
-    const bool prof = ta.passprof != nullptr;  // (profiling level 2: the NFC and the slot copies count as "loop")
+    const bool prof = !AK_NFC_SPLIT && ta.passprof != nullptr;  // (level 2: the NFC and the slot copies count as "loop")
     uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_CAP;
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
     const TileArgs tl = nfc_epoch_args(ta, E);

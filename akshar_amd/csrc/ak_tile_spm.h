@@ -1076,7 +1076,7 @@ __device__ void spm_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
     const uint32_t nl = *ta.fb_count;
     const int lane = w_lane();
     SpmWaveMem &M = L.t;
-    const bool prof = ta.passprof != nullptr;  // (profiling level 2: the NFC and the slot copies count as "loop")
+    const bool prof = !AK_NFC_SPLIT && ta.passprof != nullptr;  // (level 2: the NFC and the slot copies count as "loop")
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
     const TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nl;) {

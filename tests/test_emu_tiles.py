@@ -250,3 +250,34 @@ def test_wave_nfc_batches_with_invalid_rows(bpe_model, spm_model):
     ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
     assert rows_ints(ids, oo) == rows_ints(ref, ro)
+
+
+def test_wave_nfc_compositions(bpe_model, spm_model):
+    """Segments whose NFC composes, reorders or decomposes, through the fallback waves' NFC
+    (ak_nfc_wave.h nfc_seg: properties looked up once, the composition table asked only for a
+    first + second pair): Hangul jamo L V T runs and syllables + T, Latin letters with random marks
+    (reordered by ccc, blocked or composed), two-part vowel signs (Kannada, Malayalam, Bengali,
+    Tamil, Tibetan), nukta letters, singletons (U+212B, U+2126) and chained compositions; every row
+    equals the oracle (BPE and SentencePiece)."""
+    rng = np.random.default_rng(21)
+    starters = ["a", "e", "o", "u", "A", "O", "s", "ஒ", "ெ", "ಕ", "ೆ", "ക", "െ", "ে", "क", "ড", "ཀ",
+                "ᄀ", "ᄒ", "가", "각", "Å", "Ω", "ṩ", "x", " "]
+    marks = ["̀", "́", "̂", "̃", "̈", "̣", "̧", "̨", "̛",
+             "ͅ", "͂", "̓", "़", "्", "া", "ৗ", "ೂ", "ೕ",
+             "ാ", "ൗ", "ா", "ௗ", "ཱ", "ི", "ྀ", "ᅡ", "ᅵ",
+             "ᆨ", "ᇂ", "̴", "่"]
+    texts = []
+    for _ in range(500):
+        parts = []
+        for _ in range(int(rng.integers(1, 6))):
+            parts.append(starters[rng.integers(len(starters))])
+            parts += [marks[j] for j in rng.integers(len(marks), size=int(rng.integers(0, 4)))]
+        texts.append("".join(parts))
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(emu.Model(bpe=bpe_model), buf, offs, rows=8)
+    assert emu.last_nfc_rows() > 200
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)

@@ -22,13 +22,15 @@ def split(model, gb, go):
     torch.cuda.synchronize()
     engine.profile_enable(True, passes=True)
     engine.profile_tile_passes()
+    engine.profile_tile_counters()
     engine.profile_reset()
     model.encode_batch(gb, go)
     torch.cuda.synchronize()
     prof = engine.profile_read()
     passes = engine.profile_tile_passes(raw=True)
+    ctr = engine.profile_tile_counters()
     engine.profile_enable(False)
-    return {"ms": {k: round(v[0], 3) for k, v in prof.items() if v[1]}, "passes": passes,
+    return {"ms": {k: round(v[0], 3) for k, v in prof.items() if v[1]}, "passes": passes, "counters": ctr,
             "detail": engine.fallback_detail()}
 
 
