@@ -6,11 +6,12 @@
 #   trace    rocprofv3 kernel trace + stats of the cfg4 bench command
 #   pmc      PMC passes over the cfg4 (10 M-row BPE) and cfg5 (25 M-row SPM) launch shapes (tools/pmc_op.sh)
 #   fallback tools/fallback_realism.py
+#   waves    tools/wave_split.py (the fallback waves' per-pass split, fuzz / alphabet sets)
 #   tools/measure.sh TAG [STEP...]      (no steps: all of them, in this order)
 set -e
 TAG=${1:?tag}
 shift || true
-STEPS=${*:-tests smoke bench nccl trace pmc fallback}
+STEPS=${*:-tests smoke bench nccl trace pmc fallback waves}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -30,6 +31,7 @@ for s in $STEPS; do
     pmc) bash tools/pmc_op.sh $OUT/pmc_cfg4 bpe 10000000
          bash tools/pmc_op.sh $OUT/pmc_cfg5 spm 25000000 ;;
     fallback) timeout -k 10 400 python -u tools/fallback_realism.py > $OUT/fallback_realism.json 2> $OUT/fallback_realism.err ;;
+    waves) timeout -k 10 300 python -u tools/wave_split.py > $OUT/wave_split.jsonl 2> $OUT/wave_split.err ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
