@@ -72,6 +72,7 @@ struct AkWs {
     uint64_t cap_redo = 0;
     uint32_t *fb3 = nullptr;        // tile BPE: fallback rows k_bpe_nfc could not take (k_tile_fb)
     uint64_t cap_fb3 = 0;
+    uint4 *comp_hash = nullptr;     // fallback waves: the composition pairs' hash (ak_nfc_wave.h), built once
     uint8_t *nfc_buf = nullptr;     // k_bpe_nfc / k_spm_nfc: per-wave epochs (ak_nfc_wave.h NE_BYTES each)
     uint64_t cap_nfc = 0;           // ... waves
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)

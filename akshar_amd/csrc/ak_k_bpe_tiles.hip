@@ -505,6 +505,13 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
             HIP_TRY(hipMalloc(&w->nfc_buf, nw * NE_BYTES));
             w->cap_nfc = nw;
         }
+        if (!w->comp_hash) {  // built once per workspace
+            HIP_TRY(hipMalloc(&w->comp_hash, CH_SLOTS * sizeof(uint4)));
+            HIP_TRY(hipMemsetAsync(w->comp_hash, 0, CH_SLOTS * sizeof(uint4), st));
+            k_comp_hash_build<><<<(AK_UT_NCOMP + 255) / 256, 256, 0, st>>>(w->comp_hash);
+            HIP_TRY(hipGetLastError());
+        }
+        tfb.comp_hash = w->comp_hash;
         HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
         if (w->cap_bpool < nw * POOL_CAP) return set_error(AK_ERR_HIP, "internal: merge pools smaller than k_bpe_nfc's grid");
         k_bpe_nfc<3><<<ngrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);

@@ -297,8 +297,10 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
         HIP_TRY(hipMalloc(&w->nfc_buf, nw * NE_BYTES));
         w->cap_nfc = nw;
     }
-    k_spm_redo<3><<<ngrid, SPM_REDO_BLOCK, 0, st>>>(tfb, w->nfc_buf);
-    HIP_TRY(hipGetLastError());
+    if (ta.ra.spm.pool_ok) {  // (only the pooled variant sends rows back: a small launch skips it)
+        k_spm_redo<3><<<ngrid, SPM_REDO_BLOCK, 0, st>>>(tfb, w->nfc_buf);
+        HIP_TRY(hipGetLastError());
+    }
     if (!getenv("AK_NO_NFC_WAVE")) {  // (development aid: the one-lane path for every fallback row)
         if (w->cap_fb3 < a0.n) {
             (void)hipFree(w->fb3);
@@ -306,6 +308,13 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
             HIP_TRY(hipMalloc(&w->fb3, a0.n * 4));
             w->cap_fb3 = a0.n;
         }
+        if (!w->comp_hash) {  // built once per workspace
+            HIP_TRY(hipMalloc(&w->comp_hash, CH_SLOTS * sizeof(uint4)));
+            HIP_TRY(hipMemsetAsync(w->comp_hash, 0, CH_SLOTS * sizeof(uint4), st));
+            k_comp_hash_build<><<<(AK_UT_NCOMP + 255) / 256, 256, 0, st>>>(w->comp_hash);
+            HIP_TRY(hipGetLastError());
+        }
+        tfb.comp_hash = w->comp_hash;
         HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
         k_spm_nfc<3><<<ngrid, SPM_NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
         HIP_TRY(hipGetLastError());

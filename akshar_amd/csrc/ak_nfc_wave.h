@@ -70,6 +70,51 @@ __device__ __forceinline__ int w_last_le(uint32_t key, uint32_t p) {
     return lo;
 }
 
+// The canonical composition pairs (ak_dev.h compose_pair's sorted AK_UT_COMP_KEY / VAL, a binary
+// search of ~10 dependent loads) as an open-addressing hash: a 16-byte slot {key lo, key hi,
+// composite, 0}, key = first << 21 | second, linear probing from a multiplicative hash, 4096 slots
+// for the 941 pairs (at most a few probes, one 16-byte load each). Built once per workspace by
+// k_comp_hash_build.
+constexpr uint32_t CH_SLOTS = 4096;
+static_assert(CH_SLOTS >= 4 * AK_UT_NCOMP && (CH_SLOTS & (CH_SLOTS - 1)) == 0, "a sparse power-of-two table");
+__device__ __forceinline__ uint32_t ch_hash(uint64_t key) {
+    return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 52);  // 12 bits
+}
+// slot i of the table: insert key i (one thread each; the table zeroed before)
+__device__ __forceinline__ void ch_insert(uint4 *ch, uint32_t i) {
+    const uint64_t key = AK_UT_COMP_KEY[i];
+    uint32_t h = ch_hash(key);
+    for (;;) {
+        unsigned long long *k = (unsigned long long *)&ch[h];
+        if (atomicCAS(k, 0ull, (unsigned long long)key) == 0ull) {
+            ch[h].z = AK_UT_COMP_VAL[i];
+            return;
+        }
+        h = (h + 1) & (CH_SLOTS - 1);
+    }
+}
+#ifndef AK_HOST_EMU
+template <int D = 0>  // (a template: each translation unit that launches it has its own copy)
+__global__ void k_comp_hash_build(uint4 *ch) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < (uint32_t)AK_UT_NCOMP) ch_insert(ch, i);
+}
+#endif
+// compose_pair<NF_UCD>(a, b) through the hash
+__device__ __forceinline__ uint32_t compose_hashed(const uint4 *ch, uint32_t a, uint32_t b) {
+    if (a - H_LBASE < H_LCOUNT && b - H_VBASE < H_VCOUNT)
+        return H_SBASE + ((a - H_LBASE) * H_VCOUNT + (b - H_VBASE)) * H_TCOUNT;
+    if (a - H_SBASE < H_SCOUNT && (a - H_SBASE) % H_TCOUNT == 0 && b > H_TBASE && b < H_TBASE + H_TCOUNT)
+        return a + (b - H_TBASE);
+    const uint64_t key = ((uint64_t)a << 21) | b;
+    for (uint32_t h = ch_hash(key);; h = (h + 1) & (CH_SLOTS - 1)) {  // (the table always has empty slots)
+        const uint4 e = ch[h];
+        const uint64_t k = (uint64_t)e.x | ((uint64_t)e.y << 32);
+        if (k == key) return e.z;
+        if (k == 0) return 0;
+    }
+}
+
 // NFC of one segment (its chars in[0..n), a lane's own) into dec[0..NW_DCAP): the result of ak_dev.h
 // nfc_full<NF_UCD> (canonical decomposition, stable ccc sort, canonical composition) with each
 // char's properties looked up once (its ccc and "second of a primary composite" bit kept beside it:
@@ -77,7 +122,7 @@ __device__ __forceinline__ int w_last_le(uint32_t key, uint32_t p) {
 // only when the starter is a composition first and the char a second, unblocked — the pairs the
 // table holds (tools/gen_tables.py: comp_first / comp_second, Hangul L, LV, V, T). Inlined, so its
 // LDS accesses stay LDS accesses. Returns the length, or -1 past NW_DCAP.
-__device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n, const uint2 *fast) {
+__device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n, const uint2 *fast, const uint4 *chash) {
     constexpr uint32_t CP = 0x1FFFFFu, SECOND = 1u << 22;
     auto ent = [&](uint32_t cp, uint2 pr) { return cp | (p_second(pr) ? SECOND : 0u) | ((uint32_t)p_ccc(pr) << 24); };
     int m = 0;
@@ -121,7 +166,7 @@ __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n,
         const uint32_t x = dec[i];
         const uint32_t ch = x & CP, c = x >> 24;
         if (starter >= 0 && first && (x & SECOND) && (lastc < c || lastc == 0)) {
-            const uint32_t comp = compose_pair<NF_UCD>(st, ch);
+            const uint32_t comp = compose_hashed(chash, st, ch);
             if (comp) {
                 st = comp;
                 dec[starter] = comp;
@@ -152,7 +197,7 @@ __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n,
 // row's vbytes. A segment whose NFC passes NW_DCAP code points marks its row failed (vfail). Empties
 // the batch.
 __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &nc, int &ns, uint8_t *out, uint32_t &tout,
-                                                uint32_t out_cap, const uint2 *fast) {
+                                                uint32_t out_cap, const uint2 *fast, const uint4 *chash) {
     const int lane = w_lane();
     if (lane == 0) W.seg[ns] = (uint16_t)nc;
     w_sync();
@@ -168,7 +213,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
                 dec[0] = c0;
                 w = 1;
             } else {
-                w = nfc_seg(W.cps + s, dec, e - s, fast);
+                w = nfc_seg(W.cps + s, dec, e - s, fast, chash);
             }
         }
         uint32_t nb = 0;
@@ -375,7 +420,7 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
         }
         w_sync();
         NFC_SPLIT_MARK(3);
-        nfc_flush_batch(S, R, nc, ns, E.text, tout, NE_TCAP, fast);
+        nfc_flush_batch(S, R, nc, ns, E.text, tout, NE_TCAP, fast, ta.comp_hash);
         NFC_SPLIT_MARK(4);
         v += nrows;
         reserve += 3 * blen;

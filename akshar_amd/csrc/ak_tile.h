@@ -91,6 +91,7 @@ struct TileArgs {
     uint32_t *redo_list;  // SentencePiece: rows a pooled word's margin test sent back (k_spm_redo)
     uint32_t *redo_count; // its length (zeroed before the launch)
     uint32_t *next_unit;  // the work queue: next unit to take (zeroed before the launch)
+    const uint4 *comp_hash = nullptr;  // fallback waves: the canonical composition pairs (ak_nfc_wave.h compose_hashed)
     uint64_t ntiles;
     int rows;             // R
 };

@@ -95,6 +95,10 @@ inline uint32_t atomicAdd(uint32_t *p, uint32_t v) {
 inline uint32_t atomicSub(uint32_t *p, uint32_t v) {
     return reinterpret_cast<std::atomic<uint32_t> *>(p)->fetch_sub(v, std::memory_order_relaxed);
 }
+inline unsigned long long atomicCAS(unsigned long long *p, unsigned long long cmp, unsigned long long v) {
+    reinterpret_cast<std::atomic<unsigned long long> *>(p)->compare_exchange_strong(cmp, v, std::memory_order_relaxed);
+    return cmp;
+}
 inline uint32_t atomicExch(uint32_t *p, uint32_t v) {
     return reinterpret_cast<std::atomic<uint32_t> *>(p)->exchange(v, std::memory_order_relaxed);
 }

@@ -22,6 +22,16 @@
 
 using namespace ak;
 
+// as k_comp_hash_build: the composition pairs' hash (ak_nfc_wave.h), built once
+static const uint4 *comp_hash_table() {
+    static std::vector<uint4> t;
+    if (t.empty()) {
+        t.assign(CH_SLOTS, uint4{0, 0, 0, 0});
+        for (uint32_t i = 0; i < (uint32_t)AK_UT_NCOMP; ++i) ch_insert(t.data(), i);
+    }
+    return t.data();
+}
+
 struct EmuModel {
     akb::BpeTables bpe;
     std::vector<uint32_t> ptc;  // pre-token result cache (ak_ptc.h)
@@ -317,6 +327,7 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
         std::vector<NfcWaveLds<TileWaveMem>> NL(g_waves);
         TileArgs tn = ta;
         tn.passprof = nullptr;
+        tn.comp_hash = comp_hash_table();
         tn.ra.out = stage.data() + half;
         tn.ra.cap = half;
         run_waves([&](int w) {
@@ -445,6 +456,7 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
         uint32_t fb3n = 0;
         TileArgs tn = ta;
         tn.passprof = nullptr;
+        tn.comp_hash = comp_hash_table();
         tn.ra.out = stage.data() + half;
         run_waves([&](int w) {
             spm_nfc_wave<3>(tn, ebuf.data(), fb3.data(), &fb3n, hot_tab, scode, sfastp, NL[w], (uint32_t)w,
