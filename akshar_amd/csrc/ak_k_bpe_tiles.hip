@@ -514,7 +514,9 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
         tfb.comp_hash = w->comp_hash;
         HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
         if (w->cap_bpool < nw * POOL_CAP) return set_error(AK_ERR_HIP, "internal: merge pools smaller than k_bpe_nfc's grid");
-        k_bpe_nfc<3><<<ngrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
+        // (no more waves than rows: a small call dispatches a block or two of the 156 KB kernel)
+        const unsigned lgrid = (unsigned)std::min<uint64_t>(ngrid, (a0.n + NFC_BLOCK / 64 - 1) / (NFC_BLOCK / 64));
+        k_bpe_nfc<3><<<lgrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
         HIP_TRY(hipGetLastError());
         tfb.fb_list = w->fb3;
         tfb.fb_count = w->tile_misc + 5;

@@ -316,7 +316,9 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
         }
         tfb.comp_hash = w->comp_hash;
         HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
-        k_spm_nfc<3><<<ngrid, SPM_NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
+        // (no more waves than rows: a small call dispatches a block or two of the 156 KB kernel)
+        const unsigned lgrid = (unsigned)std::min<uint64_t>(ngrid, (a0.n + SPM_NFC_BLOCK / 64 - 1) / (SPM_NFC_BLOCK / 64));
+        k_spm_nfc<3><<<lgrid, SPM_NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
         HIP_TRY(hipGetLastError());
         tfb.fb_list = w->fb3;
         tfb.fb_count = w->tile_misc + 5;
