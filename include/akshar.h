@@ -233,10 +233,11 @@ void ak_profile_reset(void);
  * kernels (NFC / HF-NFC quick check tripped, invalid UTF-8, or past the 768-byte tile buffer), and
  * how many of those needed the slow-tier pool buffers. Synchronizes the device. */
 int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
-/* The same launch in detail: [0] rows the tile kernel could not finish; [1] of those, rows the
- * tile path finished after all (BPE: NFC by the wave, k_bpe_nfc; SentencePiece: rows a pooled
- * word's margin test sent back, re-encoded from the carried base by k_spm_redo); [2] rows left to
- * the one-lane row pipeline; [3] of those, rows that needed the slow-tier buffers. Synchronizes. */
+/* The same launch in detail: [0] rows the tile kernel could not finish (SentencePiece: + the rows
+ * a pooled word's margin test sent back); [1] of those, rows the tile path finished after all (NFC
+ * by the fallback waves, k_bpe_nfc / k_spm_nfc; the send-backs re-encoded from the carried base by
+ * k_spm_redo); [2] rows left to the one-lane row pipeline; [3] of those, rows that needed the
+ * slow-tier buffers. Synchronizes. */
 int ak_ws_fallback_detail(ak_ws *ws, uint64_t detail[4]);
 
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each
