@@ -463,8 +463,8 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
         w->cap_fb3 = a0.n;
     }
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4 * 4, st));
-    HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 2 * 4, st));  // k_bpe_nfc's pass-on count; [6]: a BPE launch
+    // [0..3] as above, [4] (SentencePiece's), [5] k_bpe_nfc's pass-on count, [6] 0: a BPE launch
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 7 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit
@@ -512,7 +512,6 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
             HIP_TRY(hipGetLastError());
         }
         tfb.comp_hash = w->comp_hash;
-        HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
         if (w->cap_bpool < nw * POOL_CAP) return set_error(AK_ERR_HIP, "internal: merge pools smaller than k_bpe_nfc's grid");
         // (no more waves than rows: a small call dispatches a block or two of the 156 KB kernel)
         const unsigned lgrid = (unsigned)std::min<uint64_t>(ngrid, (a0.n + NFC_BLOCK / 64 - 1) / (NFC_BLOCK / 64));

@@ -255,12 +255,10 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.ntiles = ntiles;
     ta.rows = R;
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count, the
-    // unit queue, the word pool's redo count
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 5 * 4, st));
-    {  // [6]: this launch is SentencePiece (ak_ws_fallback_detail)
-        static const uint32_t one = 1;
-        HIP_TRY(hipMemcpyAsync(w->tile_misc + 6, &one, 4, hipMemcpyHostToDevice, st));
-    }
+    // unit queue, the word pool's redo count, k_spm_nfc's pass-on count; [6] 1: this launch is
+    // SentencePiece (ak_ws_fallback_detail). (A memset, not a copy from pageable host memory.)
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 6 * 4, st));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w->tile_misc + 6), 1, 1, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = SPM_TILE_BLOCK / 64;
     int bpc = g_spm_blocks_per_cu.load(std::memory_order_relaxed);
@@ -315,7 +313,6 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
             HIP_TRY(hipGetLastError());
         }
         tfb.comp_hash = w->comp_hash;
-        HIP_TRY(hipMemsetAsync(w->tile_misc + 5, 0, 4, st));
         // (no more waves than rows: a small call dispatches a block or two of the 156 KB kernel)
         const unsigned lgrid = (unsigned)std::min<uint64_t>(ngrid, (a0.n + SPM_NFC_BLOCK / 64 - 1) / (SPM_NFC_BLOCK / 64));
         k_spm_nfc<3><<<lgrid, SPM_NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);

@@ -650,3 +650,52 @@ def test_spm_fallback_rows_through_the_wave_nfc(golden, eng, spm_model, monkeypa
     monkeypatch.setenv("AK_NO_NFC_WAVE", "1")
     ids2, oo2 = m.encode_batch(gb, go)
     assert torch.equal(oo2, oo) and torch.equal(ids2, ids)
+
+
+def _composition_rows(n, seed):
+    """Rows whose NFC composes, reorders or decomposes (tests/test_emu_tiles.py
+    test_wave_nfc_compositions's generator), and raw invalid rows between them."""
+    rng = np.random.default_rng(seed)
+    starters = ["a", "e", "o", "u", "A", "O", "s", "ஒ", "ெ", "ಕ", "ೆ", "ക", "െ", "ে", "क", "ড", "ཀ",
+                "ᄀ", "ᄒ", "가", "각", "Å", "Ω", "ṩ", "x", " "]
+    marks = ["̀", "́", "̂", "̃", "̈", "̣", "̧", "̨", "̛", "ͅ", "͂", "̓", "़",
+             "्", "া", "ৗ", "ೂ", "ೕ", "ാ", "ൗ", "ா", "ௗ", "ཱ", "ི", "ྀ", "ᅡ", "ᅵ",
+             "ᆨ", "ᇂ", "̴", "่"]
+    bad = [b"\xe0\xa4", b"\x80lead", b"\xc3(", b"ok \xe0", b"\xff\xfeabc", b"a\x80b"]
+    raw = []
+    for _ in range(n):
+        if rng.random() < 0.1:
+            raw.append(bad[rng.integers(len(bad))])
+            continue
+        parts = []
+        for _ in range(int(rng.integers(1, 6))):
+            parts.append(starters[rng.integers(len(starters))])
+            parts += [marks[j] for j in rng.integers(len(marks), size=int(rng.integers(0, 4)))]
+        raw.append("".join(parts).encode())
+    offs = np.zeros(len(raw) + 1, dtype=np.int64)
+    np.cumsum([len(r) for r in raw], out=offs[1:])
+    return np.frombuffer(b"".join(raw), dtype=np.uint8).copy(), offs
+
+
+def test_wave_nfc_compositions_on_device(eng, bpe_model, spm_model):
+    """The fallback waves' NFC on the device (nfc_seg with the hashed composition pairs, batches
+    mixing valid and invalid rows): 20 k rows of compositions, reorderings, Hangul jamo and two-part
+    vowel signs with invalid rows between them equal the oracle row by row, statuses included, for
+    BPE and SentencePiece."""
+    buf, offs = _composition_rows(20000, 5)
+    gb, go = _to_dev(eng, buf, offs)
+    for model, oracle in ((eng.BPE(bpe_model), O.OracleBPE(bpe_model)), (eng.SPM(spm_model), O.OracleSPM(spm_model))):
+        st = torch.zeros(len(offs) - 1, dtype=torch.uint8, device=gb.device)
+        ids, oo = model.encode_batch(gb, go, row_status=st)
+        d = eng.fallback_detail()
+        assert d["finished_in_tile_path"] > 5000, d
+        ref, ro = oracle.encode_batch(buf, offs.astype(np.uint64))
+        assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
+        bad = []
+        for r in range(len(offs) - 1):
+            try:
+                bytes(buf[offs[r]:offs[r + 1]]).decode("utf-8", "surrogatepass")
+                bad.append(0)
+            except UnicodeDecodeError:
+                bad.append(1)
+        assert [x & 1 for x in _cpu(st).tolist()] == bad  # AK_ROW_BAD_UTF8 exactly on the invalid rows
