@@ -505,7 +505,12 @@ __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEp
         const uint64_t r = R.vrow[j];
         const uint32_t rl = R.vlen[j];
         const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
-        const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : load_l2(E.vcnt + j);
+        // (an agent-scope load: pool_flush's atomicSub on the count ran at L2, past this CU's L1)
+#ifdef AK_HOST_EMU
+        const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : E.vcnt[j];
+#else
+        const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : __hip_atomic_load(E.vcnt + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         if (rl == 0xFFFFFFFFu || R.vfail[j] || (uint64_t)cnt > mul * len + 2) {
             nfc_fb3(fb3, fb3_count, r);
             continue;
@@ -515,7 +520,7 @@ __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEp
         uint32_t d = 0;
         for (uint32_t k0 = 0; k0 < rl; k0 += 64) {
             const uint32_t k = k0 + (uint32_t)lane;
-            const uint32_t x = k < rl ? load_l2(E.region + b0 + k) : STAGE_DEAD;
+            const uint32_t x = k < rl ? E.region[b0 + k] : STAGE_DEAD;  // (this wave's own stores: same-CU L1)
             const bool keep = x != STAGE_DEAD;
             const uint64_t KM = w_ballot(keep);
             if (keep) stage[s0 + d + w_rank(KM)] = x;
