@@ -464,8 +464,9 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     }
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
     // [0..3] as above, [4] (SentencePiece's), [5] k_bpe_nfc's pass-on count, [6] 0: a BPE launch
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 7 * 4, st));
-    HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
+    static_assert(CTR_N <= 256, "k_tile_init's first block clears the counters");
+    k_tile_init<><<<1, 256, 0, st>>>(w->tile_misc, 7, 0u, w->ctr, CTR_N, nullptr, 0);
+    HIP_TRY(hipGetLastError());
     const uint64_t waves_per_block = TILE_BLOCK / 64;
     // AK_TILE_BPC (development aid): resident blocks per CU below the occupancy limit
     int bpc = g_tile_blocks_per_cu.load(std::memory_order_relaxed);

@@ -206,8 +206,6 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
         HIP_TRY(hipMalloc(&w->row_span, a0.n * 4));
         w->cap_row_span = a0.n;
     }
-    // the units' fallback masks are OR-ed into (a pooled word may add a row to a finished unit)
-    HIP_TRY(hipMemsetAsync(w->unit_fb, 0, ntiles * 8, st));
     if (!w->tile_misc) {  // [0] fb count, [1] overflow flag, [2] fb2 count, [3] the unit queue
         HIP_TRY(hipMalloc(&w->tile_misc, 64 * 4));
         HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 64 * 4, st));
@@ -255,11 +253,12 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     ta.ntiles = ntiles;
     ta.rows = R;
     // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count, the
-    // unit queue, the word pool's redo count, k_spm_nfc's pass-on count; [6] 1: this launch is
-    // SentencePiece (ak_ws_fallback_detail). (A memset, not a copy from pageable host memory.)
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 6 * 4, st));
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(w->tile_misc + 6), 1, 1, st));
-    HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
+    // unit queue, the word pool's redo count, k_spm_nfc's pass-on count = 0; [6] = 1: this launch is
+    // SentencePiece (ak_ws_fallback_detail); the counters; the units' fallback masks, OR-ed into (a
+    // pooled word may add a row to a finished unit): one launch (k_tile_init)
+    static_assert(CTR_N <= 256, "k_tile_init's first block clears the counters");
+    k_tile_init<><<<tile_init_grid(ntiles), 256, 0, st>>>(w->tile_misc, 7, 1u, w->ctr, CTR_N, w->unit_fb, ntiles);
+    HIP_TRY(hipGetLastError());
     const uint64_t wpb = SPM_TILE_BLOCK / 64;
     int bpc = g_spm_blocks_per_cu.load(std::memory_order_relaxed);
     if (const char *e = getenv("AK_SPM_BPC")) bpc = std::max(1, std::min(bpc, atoi(e)));  // development aid

@@ -96,6 +96,24 @@ struct TileArgs {
     int rows;             // R
 };
 
+#ifndef AK_HOST_EMU
+// A tile launch's per-call state in one launch instead of three or four memsets (each a queued
+// operation of a few µs on a single call's critical path): misc[0..misc_n) = 0 but misc[6] = flag6,
+// ctr[0..ctr_n) = 0, unit_fb[0..nunits) = 0. (A template: every translation unit has its own copy.)
+template <int D = 0>
+__global__ void k_tile_init(uint32_t *misc, uint32_t misc_n, uint32_t flag6, uint32_t *ctr, uint32_t ctr_n, uint64_t *unit_fb,
+                            uint64_t nunits) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < misc_n) misc[i] = i == 6 ? flag6 : 0u;
+    if (i < ctr_n) ctr[i] = 0u;
+    for (uint64_t k = i; k < nunits; k += (uint64_t)gridDim.x * blockDim.x) unit_fb[k] = 0ull;
+}
+inline unsigned tile_init_grid(uint64_t nunits) {
+    const uint64_t b = (nunits + 255) / 256;
+    return (unsigned)(b < 1 ? 1 : b > 1024 ? 1024 : b);
+}
+#endif
+
 #ifndef AK_TILE_DYNAMIC
 #define AK_TILE_DYNAMIC 1
 #endif
