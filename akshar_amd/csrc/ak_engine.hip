@@ -740,11 +740,32 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const uint32_t *c, ui
     if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = sums[nb];
 }
 
+// n <= SCAN_TILE: the whole scan in one block, one launch (a single call's critical path)
+__global__ __launch_bounds__(SCAN_BLOCK) void k_scan_one(const uint32_t *c, uint64_t n, uint64_t *out) {
+    __shared__ uint64_t tmp[SCAN_BLOCK / 64 + 1];
+    const uint64_t base = (uint64_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    uint64_t s = 0;
+    for (int k = 0; k < SCAN_ITEMS; ++k) { v[k] = base + k < n ? c[base + k] : 0u; s += v[k]; }
+    uint64_t tot;
+    uint64_t x = block_exclusive_scan(s, tmp, tot);
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        if (base + k < n) out[base + k] = x;
+        x += v[k];
+    }
+    if (threadIdx.x == 0) out[n] = tot;
+}
+
 int ak::scan_counts(AkWs *w, uint64_t n, uint64_t *out_offs, hipStream_t st, const uint32_t *counts) {
     if (!counts) counts = w->counts;
     const uint64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     if (nb == 0) {
         HIP_TRY(hipMemsetAsync(out_offs, 0, 8, st));
+        return AK_OK;
+    }
+    if (nb == 1) {
+        k_scan_one<<<1, SCAN_BLOCK, 0, st>>>(counts, n, out_offs);
+        HIP_TRY(hipGetLastError());
         return AK_OK;
     }
     k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, st>>>(counts, n, w->block_sums);
