@@ -654,6 +654,9 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint
     w_sync();
 }
 
+#ifndef AK_SP_FLUSH_MIN
+#define AK_SP_FLUSH_MIN 64  // a ring runs a batch once it holds this many words (or a full batch)
+#endif
 // every ring holding a full batch (minc = 1 at the wave's end: every word), a batch at a time
 template <class MemT>
 __device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, MemT &M, uint4 *pool, bool all, PassClock &pc) {
@@ -662,7 +665,7 @@ __device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, MemT &M, uint
         const uint32_t bw = sp_batch(c);
         for (;;) {
             const uint32_t k = w_bcast(M.pcnt[c], 0);
-            if (k == 0 || (!all && k < bw)) break;
+            if (k == 0 || (!all && k < (bw < (uint32_t)AK_SP_FLUSH_MIN ? bw : (uint32_t)AK_SP_FLUSH_MIN))) break;
             if (c == (uint32_t)(SP_NCLASS - 1)) spm_pool_flush<32, SP_MAXL, MemT>(ta, M, pool, c, k < bw ? k : bw, pc);
             else spm_pool_flush<64, SP_SHORT, MemT>(ta, M, pool, c, k < bw ? k : bw, pc);
         }
