@@ -281,3 +281,35 @@ def test_wave_nfc_compositions(bpe_model, spm_model):
     ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_wave_nfc_epoch_edges(bpe_model, spm_model):
+    """The fallback waves' epoch and batch edges: 700 rows that NFC changes, padded to lengths
+    around the batch (768 bytes: 767, 768, 769 go straight on past it), the epoch's text reserve
+    (rows of 300–700 bytes fill 8 KB in a few rows) and its row count (runs of short rows: 128 per
+    epoch), with empty rows between; every row equals the oracle (BPE and SentencePiece)."""
+    rng = np.random.default_rng(31)
+    seeds = ["\u1100\u1161\u11a8", "a\u0301\u0323", "o\u0308\u0304\u0301", "\u1112\u1175 x", "a\u030a\u0323", "\u0bc6\u0bbe", "\u0cc6\u0cc2"]
+    texts = []
+    for i in range(700):
+        base = seeds[i % len(seeds)]
+        k = rng.random()
+        if k < 0.5:
+            target = int(rng.integers(1, 40))
+        elif k < 0.8:
+            target = int(rng.integers(300, 700))
+        else:
+            target = int(rng.choice([766, 767, 768, 769, 770]))
+        pad = target - len(base.encode())
+        t = base + ("x" * max(pad, 0))
+        texts.append(t)
+        if i % 97 == 0:
+            texts.append("")
+    buf, offs = O.pack(texts)
+    ids, oo, _ = emu.bpe_tiles(emu.Model(bpe=bpe_model), buf, offs, rows=8)
+    assert emu.last_nfc_rows() > 330
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+    ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
+    ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
