@@ -62,7 +62,11 @@ constexpr int SP_MAXL = SPM_POOL_MAXL;      // longest pooled word (chars, "▁"
 constexpr int SP_SHORT = 12;                // longest word of the 64-lane batches
 constexpr int SP_NCLASS = SP_SHORT;         // rings: lengths 2..SP_SHORT, then SP_SHORT+1..SP_MAXL
 constexpr uint32_t SP_RING = 320;           // a ring holds < 64 waiting + one tile's words (<= S_WORDS)
-constexpr uint32_t SP_CAP = SP_NCLASS * SP_RING;  // entries (uint4) per wave slot
+#ifndef AK_SP_RING_CODES
+#define AK_SP_RING_CODES 0  // 1: a pooled word's codes travel in its ring slot (4 x 16 B) instead of
+#endif                      // being parked in its reserved stage slots and read back by the batch
+constexpr uint32_t SP_SLOT = AK_SP_RING_CODES ? 4u : 1u;  // uint4 per ring slot
+constexpr uint32_t SP_CAP = SP_NCLASS * SP_RING * SP_SLOT;  // uint4 per wave slot
 static_assert(SP_RING >= 63 + 256, "a ring holds a batch - 1 waiting + a tile's words");
 __device__ __forceinline__ uint32_t sp_class(int L) { return L <= SP_SHORT ? (uint32_t)(L - 2) : (uint32_t)(SP_NCLASS - 1); }
 __device__ __forceinline__ uint32_t sp_batch(uint32_t c) { return c == (uint32_t)(SP_NCLASS - 1) ? 32u : 64u; }
@@ -576,9 +580,9 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint
 #ifndef AK_HOST_EMU
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's run / count / pool stores have landed
 #endif
-    uint4 *ring = pool + c * SP_RING;
     const uint32_t head = w_bcast(M.phead[c], 0);
-    const uint4 e = load_l2(ring + (head + (uint32_t)lane) % SP_RING);  // every lane: a slot in range
+    const uint4 *slot = pool + (uint64_t)(c * SP_RING + (head + (uint32_t)lane) % SP_RING) * SP_SLOT;  // every lane: in range
+    const uint4 e = load_l2(slot);
     const uint64_t dst = act ? (uint64_t)e.x | ((uint64_t)(e.y & 0xFFFFu) << 32) : 0ull;
     const int L = act ? (int)((e.y >> 16) & 0xFFu) : 0;
     const uint32_t R = act ? e.y >> 24 : 0u;
@@ -587,12 +591,13 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint
     // the batch's longest word bounds every per-position loop: a short ring's words all have
     // c + 2 chars, the long ring's up to SP_MAXL
     const int Lmax = c < (uint32_t)(SP_NCLASS - 1) ? (int)c + 2 : (int)w_max_u32((uint32_t)L);
-    // the codes back from the reserved slots (u16 pairs; dword-aligned 16-byte loads, the stage is
-    // padded past every run), into the position-major batch arrays; back slots 0..Lmax to BK_NONE
+    // the codes (u16 pairs) from the ring slot (AK_SP_RING_CODES: loads independent of the entry's)
+    // or back from the reserved slots (dword-aligned 16-byte loads, the stage is padded past every
+    // run), into the position-major batch arrays; back slots 0..Lmax to BK_NONE
 #pragma unroll
     for (int q = 0; q < (CAPL + 7) / 8; ++q) {
         if (8 * q < Lmax) {  // wave-uniform
-            const uint4 x = load_l2((const uint4 *)sp + q);
+            const uint4 x = AK_SP_RING_CODES ? load_l2(slot + 1 + q) : load_l2((const uint4 *)sp + q);
             const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (int h = 0; h < 8; ++h) {
@@ -919,9 +924,9 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         if (live && last_of_row) M.rowcnt[row] = P + c - M.rowfirst[row];  // a row's words are consecutive
         const int p1 = act ? (!last_of_row ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
         const bool pooled = live && M.wpool[j];
-        if (pooled) {  // reserve its c = R slots and park its W codes there (u16 pairs) for the batch
+        if (pooled) {  // reserve its c = R slots (and park its W codes there, u16 pairs, for the batch)
             if (P + c > scap) over = true;
-            else
+            else if (!AK_SP_RING_CODES)
                 for (int q = p0; q < p1; q += 2)
                     stage[P + (uint32_t)((q - p0) >> 1)] = (uint32_t)M.w[q] | (q + 1 < p1 ? (uint32_t)M.w[q + 1] << 16 : 0u);
         }
@@ -937,7 +942,20 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
                 const uint32_t cc = w_bcast(cls, __builtin_ctzll(CMs));
                 const uint64_t CM = w_ballot(cls == cc);
                 const uint32_t head = w_bcast(M.phead[cc], 0), k = w_bcast(M.pcnt[cc], 0);
-                if (cls == cc) pool[cc * SP_RING + (head + k + w_rank(CM)) % SP_RING] = ent;
+                if (cls == cc) {
+                    uint4 *se = pool + (uint64_t)(cc * SP_RING + (head + k + w_rank(CM)) % SP_RING) * SP_SLOT;
+                    se[0] = ent;
+                    if (AK_SP_RING_CODES) {  // the codes as u16 pairs: slots 1..3 (8 codes each)
+                        for (int q = 0; q < (L + 7) / 8; ++q) {
+                            uint32_t wv[4];
+                            for (int h = 0; h < 4; ++h) {
+                                const int a = p0 + 8 * q + 2 * h;
+                                wv[h] = (a < p1 ? (uint32_t)M.w[a] : 0u) | (a + 1 < p1 ? (uint32_t)M.w[a + 1] << 16 : 0u);
+                            }
+                            se[1 + q] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+                        }
+                    }
+                }
                 w_sync();
                 if (lane == 0) M.pcnt[cc] = k + (uint32_t)w_popc(CM);
                 w_sync();
