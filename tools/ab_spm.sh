@@ -11,7 +11,7 @@ fi
 for rep in 1 2; do
   for e in ${AB_ENVS:-X=1}; do
     for v in ${AB_VARIANTS:-default}; do
-      if [ "$v" = default ]; then env $e AB_TAG="$e" AB_DETAIL=1 timeout -k 10 300 python -u tools/ab_ops.py spm >> gpurun_out/$TAG/ab.jsonl
+      if [ "$v" = default ]; then env -u AK_LIB_VARIANT $e AB_TAG="$e" AB_DETAIL=1 timeout -k 10 300 python -u tools/ab_ops.py spm >> gpurun_out/$TAG/ab.jsonl
       else env $e AK_LIB_VARIANT=$v AB_TAG="$e" AB_DETAIL=1 timeout -k 10 300 python -u tools/ab_ops.py spm >> gpurun_out/$TAG/ab.jsonl; fi
     done
   done
