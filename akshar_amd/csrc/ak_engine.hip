@@ -509,11 +509,13 @@ extern "C" int ak_ws_fallback_detail(ak_ws *w, uint64_t detail[4]) {
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(h, w->tile_misc, sizeof(h), hipMemcpyDeviceToHost));
     // tile_misc: [0] fallback list, [2] slow tier, [4] SPM send-backs, [5] rows k_*_nfc passed on
-    // ([6]: 1 when the last launch was SPM, which leaves [5] alone)
+    // ([6]: 1 when the last launch was SPM; [7] the send-backs k_spm_redo passed on to the fallback
+    // list, which [0] and [4] both count)
     const bool spm = h[6] != 0;
     const uint64_t one_lane = std::min(h[0], h[5]);
-    detail[0] = spm ? (uint64_t)h[0] + h[4] : h[0];
-    detail[1] = (spm ? h[4] : 0u) + h[0] - one_lane;
+    const uint64_t dup = spm ? std::min(h[7], h[4]) : 0u;
+    detail[0] = spm ? (uint64_t)h[0] + h[4] - dup : h[0];
+    detail[1] = (spm ? h[4] : 0u) + h[0] - one_lane - dup;
     detail[2] = one_lane;
     detail[3] = h[2];
     return AK_OK;

@@ -249,6 +249,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     if (a0.n < ta.ra.spm.pool_rows || ta.ra.spm.wc) ta.ra.spm.pool_ok = 0;
     ta.redo_list = w->redo;
     ta.redo_count = w->tile_misc + 4;
+    ta.redo_passon = w->tile_misc + 7;
     ta.passprof = g_prof_passes ? w->tile_passprof : nullptr;
     ta.ntiles = ntiles;
     ta.rows = R;
@@ -257,7 +258,7 @@ int launch_spm_tiles(AkWs *w, const RowArgs &a0, uint64_t *out_offs, hipStream_t
     // SentencePiece (ak_ws_fallback_detail); the counters; the units' fallback masks, OR-ed into (a
     // pooled word may add a row to a finished unit): one launch (k_tile_init)
     static_assert(CTR_N <= 256, "k_tile_init's first block clears the counters");
-    k_tile_init<><<<tile_init_grid(ntiles), 256, 0, st>>>(w->tile_misc, 7, 1u, w->ctr, CTR_N, w->unit_fb, ntiles);
+    k_tile_init<><<<tile_init_grid(ntiles), 256, 0, st>>>(w->tile_misc, 8, 1u, w->ctr, CTR_N, w->unit_fb, ntiles);
     HIP_TRY(hipGetLastError());
     const uint64_t wpb = SPM_TILE_BLOCK / 64;
     int bpc = g_spm_blocks_per_cu.load(std::memory_order_relaxed);

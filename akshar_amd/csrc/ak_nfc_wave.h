@@ -293,8 +293,12 @@ __device__ __forceinline__ TileArgs nfc_epoch_args(const TileArgs &ta, const Nfc
     return tl;
 }
 
-__device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint64_t r) {
-    if (w_lane() == 0) fb3[atomicAdd(fb3_count, 1u)] = (uint32_t)r;
+// (also: a second counter of the rows passed on, SentencePiece's redo pass-ons, or null)
+__device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint64_t r, uint32_t *also = nullptr) {
+    if (w_lane() == 0) {
+        fb3[atomicAdd(fb3_count, 1u)] = (uint32_t)r;
+        if (also) atomicAdd(also, 1u);
+    }
 }
 
 #ifndef AK_NFC_SPLIT
@@ -402,14 +406,20 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
         w_sync();
         if (row_in) R.vbytes[vi] = 0;  // (from here: the row's NFC bytes)
         NFC_SPLIT_MARK(2);
-        // segments: a row's first char and every NFC-stable char
+        // segments: a row's first char and every NFC-stable char. The first char is the first whose
+        // row tag differs from the char before it, wherever its lead sits: a row that opens with
+        // continuation bytes (invalid, sent on) must not join the previous row's last segment.
         int ns = 0;
+        uint32_t carry_tag = 0xFFFFFFFFu;
         for (int base = 0; base < nc; base += 64) {
             const int ci = base + lane;
             const bool in = ci < nc;
             const uint32_t x = in ? S.cps[ci] : 0u;
             const uint32_t cp = x & 0xFFFFFFu;
-            const bool st = in && ((x >> 31) || p_stable(prop(fast, cp)));
+            const uint32_t tag = (x >> 24) & 0x7Fu;
+            const bool first = tag != w_prev(tag, carry_tag);
+            carry_tag = w_bcast(tag, 63);
+            const bool st = in && ((x >> 31) || first || p_stable(prop(fast, cp)));
             const uint64_t SM = w_ballot(st);
             if (st) {
                 S.seg[ns + (int)w_rank(SM)] = (uint16_t)ci;
@@ -450,7 +460,7 @@ static_assert(3 * NW_MAXB + 16 < NE_TCAP, "an empty epoch takes any row the wave
 // straight to fbl).
 __device__ __forceinline__ uint32_t copy_epoch_gather(const TileArgs &ta, const uint32_t *list, uint32_t &i, uint32_t nl,
                                                       uint32_t nwaves, const NfcEpoch &E, NfcRows &R, uint32_t *fbl,
-                                                      uint32_t *fbc) {
+                                                      uint32_t *fbc, uint32_t *also = nullptr) {
     const int lane = w_lane();
     uint32_t v = 0, tpos = 0;
     if (lane == 0) atomicExch(E.vfbc, 0u);
@@ -458,7 +468,7 @@ __device__ __forceinline__ uint32_t copy_epoch_gather(const TileArgs &ta, const 
         const uint64_t r = list[i];
         const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
         if (len > (uint64_t)NW_MAXB) {
-            nfc_fb3(fbl, fbc, r);
+            nfc_fb3(fbl, fbc, r, also);
             continue;
         }
         if (tpos + len + 16 > NE_TCAP) break;
@@ -495,7 +505,7 @@ __device__ __forceinline__ void nfc_epoch_runs(NfcRows &R, uint32_t r, int took,
 // if they fit the slot; else -> fb3. BPE: slot = offs[r] + 2 r, len + 2 entries (mul 1); SentencePiece
 // 2 offs[r] + 2 r, 2 len + 2 (mul 2).
 __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEpoch &E, NfcRows &R, uint32_t v,
-                                                 uint32_t mul, uint32_t *fb3, uint32_t *fb3_count) {
+                                                 uint32_t mul, uint32_t *fb3, uint32_t *fb3_count, uint32_t *also = nullptr) {
     const int lane = w_lane();
 #ifndef AK_HOST_EMU
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the region's ids, merges and counts have landed
@@ -512,7 +522,7 @@ __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEp
         const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : __hip_atomic_load(E.vcnt + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
         if (rl == 0xFFFFFFFFu || R.vfail[j] || (uint64_t)cnt > mul * len + 2) {
-            nfc_fb3(fb3, fb3_count, r);
+            nfc_fb3(fb3, fb3_count, r, also);
             continue;
         }
         const uint64_t s0 = mul * o0 + 2 * r;

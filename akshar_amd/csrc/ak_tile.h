@@ -90,6 +90,7 @@ struct TileArgs {
     uint32_t *row_span;   // SentencePiece: per row, the entries it reserved in its unit's run (0: fallback row)
     uint32_t *redo_list;  // SentencePiece: rows a pooled word's margin test sent back (k_spm_redo)
     uint32_t *redo_count; // its length (zeroed before the launch)
+    uint32_t *redo_passon;// ... and how many of those k_spm_redo passed on to the fallback list (counted in both)
     uint32_t *next_unit;  // the work queue: next unit to take (zeroed before the launch)
     const uint4 *comp_hash = nullptr;  // fallback waves: the canonical composition pairs (ak_nfc_wave.h compose_hashed)
     uint64_t ntiles;

@@ -923,10 +923,13 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         w_sync();
         if (live && last_of_row) M.rowcnt[row] = P + c - M.rowfirst[row];  // a row's words are consecutive
         const int p1 = act ? (!last_of_row ? (int)starts[j + 1] : (int)M.rowpos[row + 1] - 1) : 0;
-        const bool pooled = live && M.wpool[j];
+        bool pooled = live && M.wpool[j];
+        if (pooled && P + c > scap) {  // (never: the slot bound) the tripwire, and no ring entry
+            over = true;               // whose flush would store past the stage
+            pooled = false;
+        }
         if (pooled) {  // reserve its c = R slots (and park its W codes there, u16 pairs, for the batch)
-            if (P + c > scap) over = true;
-            else if (!AK_SP_RING_CODES)
+            if (!AK_SP_RING_CODES)
                 for (int q = p0; q < p1; q += 2)
                     stage[P + (uint32_t)((q - p0) >> 1)] = (uint32_t)M.w[q] | (q + 1 < p1 ? (uint32_t)M.w[q + 1] << 16 : 0u);
         }
@@ -1064,7 +1067,8 @@ __device__ void spm_redo_wave(const TileArgs &ta, uint8_t *ebuf, const uint32_t 
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
     const TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nredo;) {
-        const uint32_t v = copy_epoch_gather(ta, ta.redo_list, i, nredo, nwaves, E, L.rows, ta.fb_list, ta.fb_count);
+        const uint32_t v = copy_epoch_gather(ta, ta.redo_list, i, nredo, nwaves, E, L.rows, ta.fb_list, ta.fb_count,
+                                             ta.redo_passon);
         pc.mark(TP_LOOP);
         if (v == 0) continue;
         if (lane == 0) {
@@ -1080,7 +1084,7 @@ __device__ void spm_redo_wave(const TileArgs &ta, uint8_t *ebuf, const uint32_t 
             nfc_epoch_runs(L.rows, r, took, sb, in && M.fb[lane], in ? M.rowfirst[lane] : 0u, in ? M.rowcnt[lane] : 0u);
             r += (uint32_t)took;
         }
-        nfc_epoch_finish(ta, E, L.rows, v, 2u, ta.fb_list, ta.fb_count);
+        nfc_epoch_finish(ta, E, L.rows, v, 2u, ta.fb_list, ta.fb_count, ta.redo_passon);
         pc.mark(TP_LOOP);
     }
     pc.flush(ta.passprof);

@@ -237,7 +237,8 @@ int ak_ws_fallback_rows(ak_ws *ws, uint64_t *rows, uint64_t *pool_rows);
  * a pooled word's margin test sent back); [1] of those, rows the tile path finished after all (NFC
  * by the fallback waves, k_bpe_nfc / k_spm_nfc; the send-backs re-encoded from the carried base by
  * k_spm_redo); [2] rows left to the one-lane row pipeline; [3] of those, rows that needed the
- * slow-tier buffers. Synchronizes. */
+ * slow-tier buffers. A send-back row k_spm_redo passes on to the fallback list counts once.
+ * Synchronizes. */
 int ak_ws_fallback_detail(ak_ws *ws, uint64_t detail[4]);
 
 /* Tile-kernel pass breakdown (profiling aid): device clock cycles summed over all waves for each

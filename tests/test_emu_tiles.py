@@ -235,9 +235,15 @@ def test_wave_nfc_batches_with_invalid_rows(bpe_model, spm_model):
     rng = np.random.default_rng(11)
     good = ["Ḳ́x", "ạ́b", "é ऩि", "́lead mark", "", "क़ ড় x", "Ạ̊", "ok ḍ̇",
             "क़़", "x" * 70 + "́"]
+    # rows that open with continuation bytes before a char NFC does not keep alone (a combining
+    # mark, a nukta): their first char must open a segment of their own, not join the row before
     bad = [b"\xe0\xa4", b"\x80lead", b"\xc3(", b"ok \xe0", b"\xff\xfeabc", b"a\x80b", b"\xe0\xa4\x95\x80",
-           b"mid\xf4\x90\x80\x80end"]
+           b"mid\xf4\x90\x80\x80end", b"\x80\xcc\x81x", b"\xa4\xbc" + "़ि हिंदी".encode(),
+           b"\x95\xe0\xa4\xbc\xe0\xa4\xbf"]
     raw = []
+    for g in good:  # every bad row right after every good row, in one batch
+        for b in bad[-3:]:
+            raw += [g.encode(), b]
     for _ in range(400):
         raw.append(bad[rng.integers(len(bad))] if rng.random() < 0.3 else good[rng.integers(len(good))].encode())
     buf, offs = _raw_rows(raw)
