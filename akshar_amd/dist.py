@@ -30,25 +30,29 @@ def shard_rows(offs, world, rank):
     return cuts[rank], cuts[rank + 1]
 
 
-def gather_ids(ids, out_offs, group=None, out=None):
+def gather_ids(ids, out_offs, group=None, out=None, id_bound=None):
     """All-gather per-rank (ids, row offsets) into the whole batch's, in rank order.
 
     ids: int32 [n_ids]; out_offs: int64 [n_rows + 1] with out_offs[0] == 0. Returns
-    (all_ids int32, all_offs int64) identical on every rank.
+    (all_ids int32, all_offs int64) identical on every rank. id_bound: every id is below it (the
+    model's vocabulary size); at most 32,768, the ids cross the links as int16 (half the bytes;
+    the values are unchanged).
 
     Two collectives per call, whatever the world size:
       1. all_gather_into_tensor of the per-rank sizes (16 bytes each);
       2. ONE all_gather_into_tensor of a fixed-size record per rank, padded to the largest shard:
          [its row offsets rebased by the ids of the ranks before it (int64, as int32 pairs) |
-          its ids (int32)]. Shards are byte-balanced (shard_rows), so the padding is small.
-    The records are then compacted locally into the final buffers (one concatenation per output;
-    `out` = (all_ids, all_offs) preallocated by the caller receives them in place). With RCCL over
-    xGMI the data all-gather is one ring / direct collective on every link at once; per-rank
-    broadcasts would serialise on the communicator's stream.
+          its ids (int32, or int16 pairs)]. Shards are byte-balanced (shard_rows), so the padding
+         is small.
+    The records are then copied into the final buffers, one slice per rank (`out` = (all_ids,
+    all_offs) preallocated by the caller receives them in place; an int16 record widens in that
+    copy). With RCCL over xGMI the data all-gather is one ring / direct collective on every link at
+    once; per-rank broadcasts would serialise on the communicator's stream.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = ids.device
+    narrow = id_bound is not None and 0 < id_bound <= 32768 and ids.dtype == torch.int32
     sizes = torch.tensor([ids.numel(), out_offs.numel() - 1], dtype=torch.int64, device=dev)
     all_sizes = torch.empty(world * 2, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(all_sizes, sizes, group=group)
@@ -71,22 +75,30 @@ def gather_ids(ids, out_offs, group=None, out=None):
     max_rows = max(x[1] for x in sz)
     # int32 words per rank record: offsets first, and an even length, so every record's offsets
     # are 8-byte aligned and read as int64 in place
-    rec = 2 * max_rows + max_ids + (max_ids & 1)
+    id_words = (max_ids + 1) // 2 if narrow else max_ids
+    rec = 2 * max_rows + id_words + (id_words & 1)
     if rec == 0:
         return all_ids[:0], all_offs[:1]
     mine = torch.empty(rec, dtype=torch.int32, device=dev)
     n_ids, n_rows = sz[rank]
     if n_rows:
         torch.add(out_offs[1:], ib[rank], out=mine[:2 * max_rows].view(torch.int64)[:n_rows])
+    body = mine[2 * max_rows:].view(torch.int16) if narrow else mine[2 * max_rows:]
     if n_ids:
-        mine[2 * max_rows:2 * max_rows + n_ids].copy_(ids.view(torch.int32))
+        body[:n_ids].copy_(ids.view(torch.int32))
     gathered = torch.empty(world * rec, dtype=torch.int32, device=dev)
     dist.all_gather_into_tensor(gathered, mine, group=group)
     g = gathered.view(world, rec)
     g_offs = g[:, :2 * max_rows].view(torch.int64)
     g_ids = g[:, 2 * max_rows:]
-    if tot_rows:
-        torch.cat([g_offs[r, :sz[r][1]] for r in range(world)], out=all_offs[1:tot_rows + 1])
-    if tot_ids:
-        torch.cat([g_ids[r, :sz[r][0]] for r in range(world)], out=all_ids[:tot_ids].view(torch.int32))
+    if narrow:
+        g_ids = g_ids.view(torch.int16)  # (the last dimension is contiguous)
+    flat_ids = all_ids.view(torch.int32)
+    rb = 0
+    for r in range(world):
+        if sz[r][1]:
+            all_offs[1 + rb:1 + rb + sz[r][1]].copy_(g_offs[r, :sz[r][1]])
+        if sz[r][0]:
+            flat_ids[ib[r]:ib[r + 1]].copy_(g_ids[r, :sz[r][0]])
+        rb += sz[r][1]
     return all_ids[:tot_ids], all_offs[:tot_rows + 1]

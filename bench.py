@@ -17,7 +17,12 @@ Workloads (`--workload`):
                   step = encode of the shard + the gather (gather_ms reported separately).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg4|cfg5] [--rows R]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N, or plain
+         `python bench.py --gpus N`: with no RANK in the environment the script starts that launcher
+         itself as a child process (before any GPU call) and exits with its code.
+  At N > 1 cfg4 ends every step with gather_ids (the north star's all-gather that reassembles the
+  id streams on every rank, ids as int16 on the wire: the 24k vocabulary fits); --no-gather times
+  the encode alone.
 
 Rows are packed UTF-8 + int64 offsets already resident in HBM when the timed region starts. Prints
 ONE JSON line (rank 0): value = whole-job MB/s of raw UTF-8 input (max-over-ranks time), tokens/s,
@@ -54,7 +59,10 @@ def parse():
     ap.add_argument("--workload", choices=("cfg4", "cfg5"), default="cfg4")
     ap.add_argument("--rows", type=int, default=None, help="cfg4: rows per GPU (10 M); cfg5: rows of the batch (100 M)")
     ap.add_argument("--chunk-rows", type=int, default=25_000_000, help="cfg5: rows per encode call")
-    ap.add_argument("--gather", action="store_true", help="cfg4: also all-gather the id streams (RCCL)")
+    ap.add_argument("--gather", action="store_true", help="cfg4 at N = 1 (a world-1 group): also all-gather")
+    ap.add_argument("--no-gather", action="store_true", help="cfg4 at N > 1: time the encode alone")
+    ap.add_argument("--dry-run", action="store_true", help="launcher check: set up the process group, print the "
+                    "JSON line with the world size, no GPU work")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="CPU baseline: seconds per leg (up to 8 legs per model)")
     ap.add_argument("--cfg5-rows", type=int, default=25_000_000, help="N = 1: rows of the cfg5 SentencePiece launch block")
     ap.add_argument("--no-cfg5", action="store_true", help="N = 1: skip the cfg5 SentencePiece launch block")
@@ -405,9 +413,27 @@ def cfg5_block(args, dev):
     return res
 
 
+# ------------------------------------------------------------------------------------------ launcher
+def launch_workers(args):
+    """`--gpus N` (N > 1) without a launcher: run torch.distributed.run with N ranks on this node as
+    a CHILD process (nothing here has touched the GPU; never exec) and return its exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print("[bench] launching %d ranks: %s" % (args.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 # ------------------------------------------------------------------------------------------ main
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_workers(args))
     # a process group whenever launched by torch.distributed.run (even at world size 1: the RCCL
     # path then runs with one rank) or asked for N > 1
     dist = args.gpus > 1 or "RANK" in os.environ
@@ -418,6 +444,14 @@ def main():
         world = int(os.environ["WORLD_SIZE"])
         local = int(os.environ.get("LOCAL_RANK", rank))
         backend = os.environ.get("AK_BENCH_BACKEND", "nccl")  # gloo: rehearse N ranks on one GPU
+        if args.dry_run:
+            tdist.init_process_group("gloo")
+            if rank == 0:
+                print(json.dumps({"dry_run": True, "n_gpus": tdist.get_world_size(), "world_size": tdist.get_world_size(),
+                                  "requested_gpus": args.gpus, "backend": backend}), flush=True)
+            tdist.barrier()
+            tdist.destroy_process_group()
+            return
         if backend == "nccl":
             torch.cuda.set_device(local)
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -478,16 +512,27 @@ def main():
         offs_all = torch.empty(rows + 1, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     gather_s = [0.0]
+    # every id is below the vocabulary size: at <= 32,768 the gather moves them as int16
+    id_bound = len(model.model.pieces) if cfg5 else model.model.vocab_size
+    do_gather = dist and (args.gather or (world > 1 and not args.no_gather))
+    gloo = dist and tdist.get_backend() != "nccl"
+
+    def gather(ids, oo):
+        from akshar_amd import dist as adist
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        if gloo:  # the one-GPU rehearsal: gloo gathers host tensors
+            adist.gather_ids(ids.cpu(), oo.cpu(), id_bound=id_bound)
+        else:
+            adist.gather_ids(ids, oo, id_bound=id_bound)
+        torch.cuda.synchronize()
+        gather_s[0] += time.perf_counter() - tg
 
     def step():
         if not cfg5:
             ids, oo = model.encode_batch(gbuf, goffs, cap=cap, nbytes=nbytes)
-            if dist and args.gather:
-                from akshar_amd import dist as adist
-                tg = time.perf_counter()
-                adist.gather_ids(ids, oo)
-                torch.cuda.synchronize()
-                gather_s[0] += time.perf_counter() - tg
+            if do_gather:
+                gather(ids, oo)
             return ids, oo
         pos = 0
         for c0, c1, b0, b1, co in chunks:
@@ -499,12 +544,7 @@ def main():
             pos += ids.numel()
         ids, oo = ids_all[:pos], offs_all
         if dist:
-            from akshar_amd import dist as adist
-            torch.cuda.synchronize()
-            tg = time.perf_counter()
-            adist.gather_ids(ids, oo)
-            torch.cuda.synchronize()
-            gather_s[0] += time.perf_counter() - tg
+            gather(ids, oo)
         return ids, oo
 
     for i in range(args.warmup):
@@ -594,12 +634,19 @@ def main():
             "scaling": "strong" if cfg5 else "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (akshar_amd.synth, seed %d)" % SEED, "tokens_per_s": round(toks, 1),
             "config": {"workload": wl, "rows_per_gpu": rows, "bytes_per_gpu": nbytes, "ids_per_gpu": n_ids,
-                       "parallelism": ("dp%d (byte-balanced row shards + all-gather)" if cfg5 else
+                       "parallelism": ("dp%d (byte-balanced row shards + all-gather)" if cfg5 or do_gather else
                                        "dp%d (row shards, no data-path collective)") % world},
             "roofline": roofline, "cpu_baseline": cpu,
         }
-        if cfg5 or args.gather:
+        if dist:
+            line["world_size"] = tdist.get_world_size()  # the ranks the process group (RCCL) saw
+            line["backend"] = tdist.get_backend()
+        if cfg5 or do_gather:
             line["gather_ms"] = round(gmax / args.steps * 1e3, 3)
+            line["gather"] = ("akshar_amd.dist.gather_ids inside every timed step: all-gather of the per-rank sizes, "
+                              "then ONE all_gather_into_tensor of the padded (offsets | ids) records, ids as %s" %
+                              ("int16" if id_bound <= 32768 else "int32"))
+            line["encode_only_mb_s"] = round(job_bytes * args.steps / max(elapsed - gmax, 1e-9) / 1e6, 2)
             line["shard_byte_imbalance"] = round(byte_imbalance, 5)
         if e2e:
             line["end_to_end"] = e2e

@@ -36,6 +36,10 @@ def _worker(rank, world, port, q):
         ids, oo = O.OracleBPE(BPEModel(BPE_PATH)).encode_batch(sub if len(sub) else np.zeros(1, np.uint8), sub_offs)
         all_ids, all_offs = adist.gather_ids(torch.from_numpy(ids.astype(np.int32)),
                                              torch.from_numpy(oo.astype(np.int64)))
+        # the same gather with the ids crossing as int16 (the 24k vocabulary fits): identical result
+        n_ids, n_offs = adist.gather_ids(torch.from_numpy(ids.astype(np.int32)),
+                                         torch.from_numpy(oo.astype(np.int64)), id_bound=32768)
+        assert torch.equal(n_ids, all_ids) and torch.equal(n_offs, all_offs)
         q.put((rank, r0, r1, all_ids.numpy(), all_offs.numpy()))
     finally:
         dist.destroy_process_group()
@@ -146,8 +150,10 @@ def _nccl_worker(port, q):
             gb, go = engine.to_device(pad, offs.astype(np.int64), dev=0)
             ids, oo = engine.SPM(SPM_PATH, dev=0).encode_batch(gb, go)
             all_ids, all_offs = adist.gather_ids(ids, oo)
+            n_ids, n_offs = adist.gather_ids(ids, oo, id_bound=32768)  # int16 on the wire
             torch.cuda.synchronize()
             ok = all_ids.is_cuda and torch.equal(all_ids, ids) and torch.equal(all_offs, oo)
+            ok = ok and torch.equal(n_ids, ids) and torch.equal(n_offs, oo)
             q.put(("ok" if ok else "mismatch", int(all_ids.numel())))
         finally:
             dist.destroy_process_group()
@@ -182,6 +188,8 @@ def _edge_worker(rank, world, port, q):
         if rank == 2:
             out = (torch.full((20,), -1, dtype=torch.int32), torch.full((10,), -1, dtype=torch.int64))
         all_ids, all_offs = adist.gather_ids(ids, offs, out=out)
+        n_ids, n_offs = adist.gather_ids(ids, offs, id_bound=32768)  # int16 on the wire (odd counts)
+        assert n_ids.tolist() == all_ids.tolist() and n_offs.tolist() == all_offs.tolist()
         q.put((rank, all_ids.tolist(), all_offs.tolist()))
     finally:
         dist.destroy_process_group()
@@ -189,7 +197,8 @@ def _edge_worker(rank, world, port, q):
 
 def test_gloo_world3_gather_uneven_and_empty_shards():
     """gather_ids with an empty rank and a caller-provided output: every rank gets the whole batch's
-    ids in rank order and offsets rebased across ranks (one size all-gather + exact-size broadcasts)."""
+    ids in rank order and offsets rebased across ranks (one size all-gather + one all-gather of the
+    padded per-rank records), with the ids as int32 and as int16 on the wire."""
     world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -661,7 +661,10 @@ def _composition_rows(n, seed):
     marks = ["̀", "́", "̂", "̃", "̈", "̣", "̧", "̨", "̛", "ͅ", "͂", "̓", "़",
              "्", "া", "ৗ", "ೂ", "ೕ", "ാ", "ൗ", "ா", "ௗ", "ཱ", "ི", "ྀ", "ᅡ", "ᅵ",
              "ᆨ", "ᇂ", "̴", "่"]
-    bad = [b"\xe0\xa4", b"\x80lead", b"\xc3(", b"ok \xe0", b"\xff\xfeabc", b"a\x80b"]
+    # (the last three open with continuation bytes before a mark / nukta: ak_nfc_wave.h must give
+    # their first char a segment of its own, not the previous row's)
+    bad = [b"\xe0\xa4", b"\x80lead", b"\xc3(", b"ok \xe0", b"\xff\xfeabc", b"a\x80b", b"\x80\xcc\x81x",
+           b"\xa4\xbc" + "\u093c\u093f \u0939\u093f\u0902".encode(), b"\x95\xe0\xa4\xbc\xe0\xa4\xbf"]
     raw = []
     for _ in range(n):
         if rng.random() < 0.1:
@@ -699,3 +702,47 @@ def test_wave_nfc_compositions_on_device(eng, bpe_model, spm_model):
             except UnicodeDecodeError:
                 bad.append(1)
         assert [x & 1 for x in _cpu(st).tolist()] == bad  # AK_ROW_BAD_UTF8 exactly on the invalid rows
+
+
+def test_fallback_waves_at_scale_on_fresh_fuzz_rows(eng, bpe_model, spm_model):
+    """The fallback waves at the scale they are tuned on, on DISTINCT rows: 1 M
+    fresh mixed-Unicode fuzz rows (synthetic kind 2, a seed no other test uses) in ONE launch each of
+    BPE, SentencePiece and the fused analyze op; every row equals the oracle (threaded, 16 row
+    ranges). About a third of the rows leave the tile kernel, so every fallback wave runs several
+    full epochs (an epoch holds 128 rows or 8 KB of NFC text, 3 bytes reserved per input byte)."""
+    n = 1_000_000
+    buf, offs = _synth(2, n, 777)
+    gb, go = _to_dev(eng, buf, offs)
+    for name, model, oracle in (("bpe", eng.BPE(bpe_model), O.OracleBPE(bpe_model)),
+                                ("spm", eng.SPM(spm_model), O.OracleSPM(spm_model))):
+        ids, oo = model.encode_batch(gb, go)
+        d = eng.fallback_detail()
+        ids, oo = _cpu(ids).astype(np.uint32), _cpu(oo).astype(np.int64)
+        waves = torch.cuda.get_device_properties(0).multi_processor_count * 8
+        # rows one epoch takes at most: its text reserve over the mean fallback-row bytes (~ all rows)
+        per_epoch = min(128, 8192 // max(1, 3 * int(offs[-1]) // n))
+        assert d["finished_in_tile_path"] > 2 * waves * per_epoch, (name, d, waves, per_epoch)
+        cuts, parts = _oracle_threads(lambda b, o: oracle.encode_batch(b, o), buf, offs, n)
+        for k, (ref, ro) in enumerate(parts):
+            a, b = cuts[k], cuts[k + 1]
+            assert np.array_equal(oo[a:b + 1] - oo[a], ro.astype(np.int64)), "%s offsets differ in rows %d..%d" % (name, a, b)
+            assert np.array_equal(ids[oo[a]:oo[b]], ref), "%s ids differ in rows %d..%d" % (name, a, b)
+    norm, no, cl, co, runs, labels, ro_ = eng.analyze_batch(gb, go)
+    norm, no, cl, co = _cpu(norm), _cpu(no).astype(np.int64), _cpu(cl).astype(np.uint32), _cpu(co).astype(np.int64)
+    runs, labels, ro_ = _cpu(runs).astype(np.uint32), _cpu(labels), _cpu(ro_).astype(np.int64)
+
+    def ref(b, o):
+        nb, nbo = O.normalize_batch(b, o, flags=3)
+        pad = np.zeros(len(nb) + 16, np.uint8)
+        pad[:len(nb)] = nb
+        return (nb, nbo) + O.segment_batch(pad, nbo, flags=-1) + O.switches_batch(pad, nbo, flags=-1)
+    cuts, parts = _oracle_threads(ref, buf, offs, n)
+    for k, (nb, nbo, ce, ceo, re_, rl, reo) in enumerate(parts):
+        a, b = cuts[k], cuts[k + 1]
+        assert np.array_equal(no[a:b + 1] - no[a], nbo.astype(np.int64)) and \
+            np.array_equal(norm[no[a]:no[b]], nb), "normalized rows differ in %d..%d" % (a, b)
+        assert np.array_equal(co[a:b + 1] - co[a], ceo.astype(np.int64)) and \
+            np.array_equal(cl[co[a]:co[b]], ce), "clusters differ in %d..%d" % (a, b)
+        assert np.array_equal(ro_[a:b + 1] - ro_[a], reo.astype(np.int64)) and \
+            np.array_equal(runs[ro_[a]:ro_[b]], re_) and np.array_equal(labels[ro_[a]:ro_[b]], rl), \
+            "runs differ in %d..%d" % (a, b)
