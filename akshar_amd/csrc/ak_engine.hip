@@ -176,6 +176,7 @@ struct ak_spm {
     uint32_t *d_wc = nullptr;     // the word cache (ak_swc.h), tile path only
     akb::SwcStats wc{};
     uint32_t wc_slots = 0;
+    uint16_t *d_scode = nullptr;  // the tile kernels' LDS code table, for the one-kernel per-call path
 };
 
 // The live handles: filled by ak_*_create (ak_*_load goes through them), cleared by ak_*_free, so
@@ -426,6 +427,10 @@ extern "C" int ak_spm_create(uint32_t n, const uint8_t *piece_bytes, const uint6
         const int rc = upload_dec(m->d_dec, m->dec, text, off, kind, bv);
         if (rc) { ak_spm_free(m); return rc; }
     }
+    {
+        const int rc = build_spm_scode(m->dev, &m->d_scode);
+        if (rc) { ak_spm_free(m); return rc; }
+    }
     live_add(m);
     *out = m;
     return AK_OK;
@@ -442,6 +447,7 @@ extern "C" void ak_spm_free(ak_spm *m) {
     (void)hipFree(m->d_byte_ids);
     (void)hipFree(m->d_dec);
     (void)hipFree(m->d_wc);
+    (void)hipFree(m->d_scode);
     delete m;
 }
 
@@ -581,6 +587,8 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->acounts);
     (void)hipFree(w->dev1);
     (void)hipHostFree(w->pin);
+    (void)hipHostFree(w->pin_small);
+    (void)hipFree(w->dev_small);
     delete w;
 }
 
@@ -942,6 +950,36 @@ __global__ void k_err_words(const uint32_t *ctr, const uint32_t *misc, uint32_t 
 // ak_*_encode_host: one row through pinned host staging. Device staging layout (16-byte aligned):
 // [offs 2 x u64 | bytes, padded | out_offs 2 x u64 | error words | ids dcap x u32]; the first two
 // travel host->device in one copy, the last three device->host in one copy.
+// The one-kernel path first (small(): ak_internal.h SmallCall) when the row fits a tile: the row
+// into fine-grained pinned memory, one launch, one synchronize, the ids read where the kernel wrote
+// them. A row the tile front end sends to the fallback kernels (status 1), or one no tile holds
+// (status 2), takes the batch sequence below.
+template <class Small>
+static int encode_small(ak_ws *w, const uint8_t *text, uint64_t len, int32_t *ids, uint64_t cap, uint64_t *n_ids,
+                        Small small, bool *done) {
+    *done = false;
+    if (len + 48 > SC_RES) return AK_OK;
+    int rc = small_call_reserve(w);
+    if (rc) return rc;
+    uint64_t *po = (uint64_t *)w->pin_small;
+    po[0] = 0;
+    po[1] = len;
+    if (len) memcpy(w->pin_small + 16, text, len);
+    memset(w->pin_small + 16 + len, 0, 32);
+    uint32_t status = 2;
+    if ((rc = small(&status))) return rc;
+    if (status != 0) return AK_OK;
+    const volatile uint32_t *res = (const volatile uint32_t *)(w->pin_small + SC_RES);
+    const uint32_t n = res[1], err = res[2], live = res[3];
+    if (err) return fail(AK_ERR_HIP, "tile staging slot overflow (a row produced more ids than bytes + 2)");
+    if (live != n) return fail(AK_ERR_HIP, "internal: the per-call kernel's count and ids disagree (engine bug)");
+    *n_ids = n;
+    if (n > cap) return fail(AK_ERR_NOMEM, "encode_host: ids buffer too small (*n_ids holds the count)");
+    if (n) memcpy(ids, (const void *)(res + 4), (size_t)n * 4);
+    *done = true;
+    return AK_OK;
+}
+
 template <class Enc>
 static int encode_host(ak_ws *w, const uint8_t *text, uint64_t len, int32_t *ids, uint64_t cap, uint64_t *n_ids,
                        uint64_t dcap, hipStream_t st, const char *who, Enc enc) {
@@ -1009,6 +1047,17 @@ extern "C" int ak_bpe_encode_host(const ak_bpe *m, ak_ws *w, int flags, const ui
     // the ids bound of the path that runs: bytes + 2 with clean_hinglish (BPE_MUL), 6 x bytes + 2 under
     // HF's full NFKC without it (BPE_NFKC_MUL, ak_k_bpe_f01.hip: U+FDFA is 3 bytes -> 18 code points)
     const uint64_t dcap = ((flags & AK_NORM_CLEAN) ? len : 6 * len) + 2 + 16;
+    if (w && n_ids && (text || !len) && (ids || !cap) && flags == 3 && m->tile_ok && w->bpe_path == 1 && !getenv("AK_NO_SMALL")) {
+        bool done = false;
+        RowArgs a = make_args(nullptr, nullptr, 1, nullptr, 0, nullptr);
+        a.bpe = m->dev;
+        a.single_fast = m->d_single_fast;
+        *n_ids = 0;
+        const int rc = encode_small(w, text, len, ids, cap, n_ids, [&](uint32_t *status) {
+            return small_call_bpe(w, a, len, (hipStream_t)stream, status);
+        }, &done);
+        if (rc || done) return rc;
+    }
     return encode_host(w, text, len, ids, cap, n_ids, dcap, (hipStream_t)stream, "ak_bpe_encode_host: null argument",
                        [&](const uint8_t *in, const uint64_t *offs, uint32_t *out, uint64_t c, uint64_t *oo) {
                            return ak_bpe_encode(m, w, flags, in, offs, 1, out, c, oo, nullptr, stream);
@@ -1018,6 +1067,16 @@ extern "C" int ak_bpe_encode_host(const ak_bpe *m, ak_ws *w, int flags, const ui
 extern "C" int ak_spm_encode_host(const ak_spm *m, ak_ws *w, int flags, const uint8_t *text, uint64_t len, int32_t *ids,
                                   uint64_t cap, uint64_t *n_ids, void *stream) {
     if (!m) return fail(AK_ERR_ARG, "ak_spm_encode_host: null model");
+    if (w && n_ids && (text || !len) && (ids || !cap) && flags == 3 && w->bpe_path == 1 && !getenv("AK_NO_SMALL")) {
+        bool done = false;
+        RowArgs a = make_args(nullptr, nullptr, 1, nullptr, 0, nullptr);
+        a.spm = m->dev;
+        *n_ids = 0;
+        const int rc = encode_small(w, text, len, ids, cap, n_ids, [&](uint32_t *status) {
+            return small_call_spm(w, a, m->d_scode, len, (hipStream_t)stream, status);
+        }, &done);
+        if (rc || done) return rc;
+    }
     return encode_host(w, text, len, ids, cap, n_ids, 3 * len + 4 + 16, (hipStream_t)stream,
                        "ak_spm_encode_host: null argument",
                        [&](const uint8_t *in, const uint64_t *offs, uint32_t *out, uint64_t c, uint64_t *oo) {

@@ -87,7 +87,27 @@ struct AkWs {
     uint64_t cap_pin = 0;
     uint8_t *dev1 = nullptr;        // device staging of one call: offsets, bytes, ids, offsets out
     uint64_t cap_dev1 = 0;
+    // the one-kernel per-call path (SmallCall: ak_*_encode_host of one row that fits a tile)
+    uint8_t *pin_small = nullptr;   // fine-grained (coherent) pinned host memory the kernel reads and writes
+    uint8_t *pin_small_dev = nullptr;  // ... its device address
+    uint8_t *dev_small = nullptr;   // device scratch: counters, the unit run, the merge pool, the hot table
 };
+
+// The one-kernel per-call path (ak_bpe_encode_host / ak_spm_encode_host of a row that fits one
+// tile): ONE wave reads the row straight from fine-grained pinned host memory, runs the tile
+// pipeline and its merges, and writes the ids and the count straight back there, so a call is one
+// launch and one synchronize instead of the batch sequence (init, tile kernel, fallback waves,
+// one-lane kernel, tiers, scan, copy, two copies). A row the tile front end sends to the fallback
+// kernels reports status 1 and the caller runs the batch sequence for it.
+constexpr uint64_t SC_PIN_BYTES = 16384;     // pinned: offs (16 B) | bytes (T_BCAP + 32) | results at SC_RES
+constexpr uint64_t SC_RES = 1024;            // res[0] status, [1] count, [2] error flags, [3] live entries; ids at +16
+constexpr uint64_t SC_STAGE = 4096;          // u32 entries of the device unit run
+constexpr uint64_t SC_DEV_BYTES = 64 * 4 + SC_STAGE * 4 + 1024 * 16 + 1024 * 4 + 16 + 1024;  // counters | run | pool | hot | offs | row
+int small_call_bpe(AkWs *w, const RowArgs &a, uint64_t len, hipStream_t st, uint32_t *status);
+int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, uint64_t len, hipStream_t st, uint32_t *status);
+// the SentencePiece tile kernels' LDS code table (HOT_N u16), built once per model for the small calls
+int build_spm_scode(const SpmDev &dev, uint16_t **out);
+int small_call_reserve(AkWs *w);
 
 // total bytes of a launch's rows (offs[n]): known to the host for a host-staged call, else one
 // 8-byte read-back

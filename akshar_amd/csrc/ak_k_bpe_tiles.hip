@@ -15,6 +15,7 @@
 
 #include "ak_internal.h"
 #include "ak_nfc_wave.h"
+#include "ak_small.h"
 #include "ak_tile.h"
 
 namespace ak {
@@ -476,7 +477,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     // the waves' merge pools: POOL_CAP entries per wave slot of the grid, and of k_bpe_nfc's grid
     // (num_cus() blocks of NFC_BLOCK / 64 waves, which a small launch's tile grid may not reach)
     const uint64_t pool_waves = std::max<uint64_t>((uint64_t)grid * waves_per_block, (uint64_t)num_cus() * (NFC_BLOCK / 64));
-    const uint64_t pool_entries = pool_waves * POOL_CAP;
+    const uint64_t pool_entries = pool_waves * POOL_U4;
     if (w->cap_bpool < pool_entries) {
         (void)hipFree(w->bpool);
         w->bpool = nullptr;
@@ -513,7 +514,7 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
             HIP_TRY(hipGetLastError());
         }
         tfb.comp_hash = w->comp_hash;
-        if (w->cap_bpool < nw * POOL_CAP) return set_error(AK_ERR_HIP, "internal: merge pools smaller than k_bpe_nfc's grid");
+        if (w->cap_bpool < nw * POOL_U4) return set_error(AK_ERR_HIP, "internal: merge pools smaller than k_bpe_nfc's grid");
         // (no more waves than rows: a small call dispatches a block or two of the 156 KB kernel)
         const unsigned lgrid = (unsigned)std::min<uint64_t>(ngrid, (a0.n + NFC_BLOCK / 64 - 1) / (NFC_BLOCK / 64));
         k_bpe_nfc<3><<<lgrid, NFC_BLOCK, 0, st>>>(tfb, w->nfc_buf, w->fb3, w->tile_misc + 5);
@@ -550,6 +551,73 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
     }
     AK_PROF(AK_PROF_COPY, true, st);
     return rc;
+}
+
+// One row (ta.ra.n == 1, at most T_BCAP bytes) through bpe_tile and the merge pool by ONE wave.
+__global__ __launch_bounds__(64) void k_bpe_small(TileArgs ta, uint8_t *dsmall, const uint8_t *hrow, uint64_t len, uint32_t *res) {
+    __shared__ uint32_t hot_tab[HOT_N];
+    __shared__ uint16_t sfast[SFAST_N];
+    __shared__ TileWaveMem M;
+    const SmallDev sd = small_dev(dsmall);
+    const int lane = w_lane();
+    small_stage_row(hrow, len, sd.row, sd.offs);
+    for (uint32_t i = lane; i < HOT_N; i += 64) hot_tab[i] = sd.hot[i];
+    for (uint32_t i = lane; i < SFAST_N; i += 64) sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
+    if (lane < POOL_NCLASS) {
+        M.phead[lane] = 0;
+        M.pcnt[lane] = 0;
+    }
+    if (lane == 0) {
+        M.unext = 0;
+        M.ufbm = 0;
+        sd.ctr[1] = 0;  // the fallback list's length (bpe_tile appends the row when it falls back)
+        sd.ctr[2] = 0;  // the slot-overflow flag
+    }
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (before bpe_tile's atomics on them)
+#endif
+    __syncthreads();
+    PassClock pc;
+    pc.init(false, M.passacc);
+    (void)bpe_tile<3>(ta, 0, 1, hot_tab, sfast, M, sd.pool, pc);
+    const bool fb = (w_bcast((uint32_t)M.ufbm, 0) & 1u) != 0u;
+    const uint64_t run_len = M.unext;
+    pool_drain(ta, M, sd.pool, 1u, pc);  // every miss merged
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t cnt = __hip_atomic_load(ta.counts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (pool atomics ran at L2)
+#else
+    const uint32_t cnt = ta.counts[0];
+#endif
+    small_finish(sd, run_len, fb, cnt, res);
+}
+
+int small_call_reserve(AkWs *w) {
+    if (w->pin_small) return AK_OK;
+    HIP_TRY(hipHostMalloc(&w->pin_small, SC_PIN_BYTES, hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void **)&w->pin_small_dev, w->pin_small, 0));
+    HIP_TRY(hipMalloc(&w->dev_small, SC_DEV_BYTES));
+    HIP_TRY(hipMemset(w->dev_small, 0, SC_DEV_BYTES));
+    k_hot_build<><<<(HOT_N + 255) / 256, 256>>>(small_dev(w->dev_small).hot);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    return AK_OK;
+}
+
+int small_call_bpe(AkWs *w, const RowArgs &a, uint64_t len, hipStream_t st, uint32_t *status) {
+    *status = 2;
+    if (len > (uint64_t)T_BCAP) return AK_OK;  // no tile buffer holds the row: the batch sequence
+    int rc = small_call_reserve(w);
+    if (rc) return rc;
+    TileArgs ta = small_args(w, a);
+    uint32_t *res = (uint32_t *)(w->pin_small_dev + SC_RES);
+    AK_PROF(AK_PROF_TILES, false, st);
+    k_bpe_small<<<1, 64, 0, st>>>(ta, w->dev_small, w->pin_small_dev + 16, len, res);
+    AK_PROF(AK_PROF_TILES, true, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    *status = ((volatile uint32_t *)(w->pin_small + SC_RES))[0];
+    return AK_OK;
 }
 
 int ws_stage_reserve(AkWs *w, uint64_t need, hipStream_t st) {

@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include "ak_internal.h"
+#include "ak_small.h"
 #include "ak_tile_spm.h"
 
 namespace ak {
@@ -44,6 +45,72 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     const uint32_t wave = threadIdx.x >> 6;
     spm_tiles_wave<FLAGS, MemT>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
                                 gridDim.x * (SPM_TILE_BLOCK / 64));
+}
+
+// The SentencePiece kernels' LDS code table entry of hot_cp(i): W_CODED | code for chars some piece
+// holds, else the code point.
+__device__ __forceinline__ uint16_t scode_of(const SpmDev &m, uint32_t cp) {
+    const uint32_t c = spm_code(m, cp);
+    return (c & SPM_CODED) ? (uint16_t)(W_CODED | (c & 0x7FFFu)) : (uint16_t)cp;
+}
+__global__ void k_scode_build(SpmDev m, uint16_t *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < HOT_N) out[i] = scode_of(m, hot_cp(i));
+}
+int build_spm_scode(const SpmDev &dev, uint16_t **out) {
+    *out = nullptr;
+    HIP_TRY(hipMalloc(out, HOT_N * sizeof(uint16_t)));
+    k_scode_build<<<(HOT_N + 255) / 256, 256>>>(dev, *out);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    return AK_OK;
+}
+
+// The per-call path (ak_internal.h SmallCall): one row of at most S_BCAP bytes through the tile
+// variant (every word solved in the tile, the carried base for close calls) by ONE wave; ids and the
+// count straight to pinned host memory (ak_small.h small_finish).
+__global__ __launch_bounds__(64) void k_spm_small(TileArgs ta, const uint16_t *scode_g, uint8_t *dsmall, const uint8_t *hrow,
+                                                 uint64_t len, uint32_t *res) {
+    __shared__ uint32_t hot_tab[HOT_N];
+    __shared__ uint16_t scode[HOT_N];
+    __shared__ SpmWaveMem M;
+    const SmallDev sd = small_dev(dsmall);
+    const int lane = w_lane();
+    small_stage_row(hrow, len, sd.row, sd.offs);
+    for (uint32_t i = lane; i < HOT_N; i += 64) {
+        hot_tab[i] = sd.hot[i];
+        scode[i] = scode_g[i];
+    }
+    if (lane == 0) {
+        M.unext = 0;
+        M.ufbm = 0;
+        sd.ctr[1] = 0;  // the fallback list's length
+        sd.ctr[2] = 0;  // the slot-overflow flag
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    PassClock pc;
+    pc.init(false, M.passacc);
+    (void)spm_tile<3, SpmWaveMem>(ta, 0, 1, hot_tab, scode, M, nullptr, pc, true);
+    const bool fb = (w_bcast((uint32_t)M.ufbm, 0) & 1u) != 0u;
+    small_finish(sd, M.unext, fb, w_bcast(M.rowcnt[0], 0), res);
+}
+
+int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, uint64_t len, hipStream_t st, uint32_t *status) {
+    *status = 2;
+    if (len > (uint64_t)SpmWaveMem::BC || !scode) return AK_OK;  // no tile buffer holds the row: the batch sequence
+    int rc = small_call_reserve(w);
+    if (rc) return rc;
+    TileArgs ta = small_args(w, a);
+    ta.ra.spm.pool_ok = 0;
+    uint32_t *res = (uint32_t *)(w->pin_small_dev + SC_RES);
+    AK_PROF(AK_PROF_SPM_TILES, false, st);
+    k_spm_small<<<1, 64, 0, st>>>(ta, scode, w->dev_small, w->pin_small_dev + 16, len, res);
+    AK_PROF(AK_PROF_SPM_TILES, true, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    *status = ((volatile uint32_t *)(w->pin_small + SC_RES))[0];
+    return AK_OK;
 }
 
 // rows the word pool sent back (ak_tile_spm.h spm_redo_wave): the waves' epochs, the tile variant

@@ -553,7 +553,7 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
     const int lane = w_lane();
     TileWaveMem &M = L.t;
     const bool prof = !AK_NFC_SPLIT && ta.passprof != nullptr;  // (level 2: the NFC and the slot copies count as "loop")
-    uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_CAP;
+    uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_U4;
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
     const TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nl;) {

@@ -753,6 +753,14 @@ __device__ __forceinline__ uint32_t ptc_probe(const BpeDev &m, bool cand, uint32
 constexpr int POOL_NCLASS = AK_POOL_NCLASS;    // 8: symbol counts 2, 3, 4, 5, 6, 7, 8-9, 10-15; 4: 2-3, 4-5, 6-8, 9-15
 constexpr uint32_t POOL_RING = 320;            // a class ring holds < 64 waiting + a tile's misses (T_SCAP)
 constexpr uint32_t POOL_CAP = POOL_NCLASS * POOL_RING;  // entries per wave slot
+#ifndef AK_POOL_INLINE
+#define AK_POOL_INLINE 0
+#endif
+// AK_POOL_INLINE: a miss's symbols travel in its ring entry (two more uint4 after the wave's POOL_CAP
+// headers: [headers | symbol pairs]), written by pass A from W with coalesced stores and read back
+// by the batch the same way, instead of read back from the unit run (a scattered 64-byte window
+// per miss)
+constexpr uint32_t POOL_U4 = POOL_CAP * (AK_POOL_INLINE ? 3u : 1u);  // uint4 per wave slot
 constexpr uint32_t STAGE_DEAD = 0xFFFFFFFFu;   // stage entry of a merged-away symbol (the copy drops it)
 static_assert(POOL_NCLASS == 1 || POOL_NCLASS == 4 || POOL_NCLASS == 8, "pool classes");
 __device__ __forceinline__ uint32_t pool_class(uint32_t n) {
@@ -844,6 +852,15 @@ __device__ __forceinline__ void merge_rounds(const BpeDev &m, uint16_t *sym, uin
     }
 }
 
+// AK_POOL_RB: the read-back skips a 16-byte chunk no lane of the batch needs; AK_POOL_WB: the
+// write-back stores each lane's tail chunk as ONE 3-, 2- or 1-dword store instead of up to three
+// dword stores (together -1 % on 4 M rows, profiles/r06c_ab_pool.jsonl)
+#ifndef AK_POOL_RB
+#define AK_POOL_RB 1
+#endif
+#ifndef AK_POOL_WB
+#define AK_POOL_WB 1
+#endif
 // One merge batch of the wave's pool: the first cnt (<= 64) entries, lane l the l-th. LDS: the
 // lanes' rank rows and symbol rows (64 x 32 B each) over the tile buffers, free between tiles.
 __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, uint4 *pool, uint32_t c, uint32_t cnt,
@@ -867,11 +884,24 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
     const uint32_t row = e.z;
     uint32_t *sp = (uint32_t *)ta.ra.out + dst;
     uint32_t p[WREG / 2];  // the symbols as u16 pairs (0xFFFF past n)
+#if AK_POOL_INLINE
+    {
+        const uint4 *sy = pool + POOL_CAP + 2 * (c * POOL_RING + (head + (uint32_t)lane) % POOL_RING);
+        const uint4 a = load_l2(sy), b = load_l2(sy + 1);
+        p[0] = a.x; p[1] = a.y; p[2] = a.z; p[3] = a.w; p[4] = b.x; p[5] = b.y; p[6] = b.z; p[7] = b.w;
+#pragma unroll
+        for (int k = 0; k < WREG / 2; ++k) {  // 0xFFFF past n (pass A stored the window as it was)
+            const int i = 2 * k;
+            p[k] = (i < n ? (p[k] & 0xFFFFu) : 0xFFFFu) | (i + 1 < n ? (p[k] & 0xFFFF0000u) : 0xFFFF0000u);
+        }
+    }
+#else
     {
         const uint4 *s4 = (const uint4 *)sp;  // dword-aligned 16-byte loads (the stage is padded past every run)
 #pragma unroll
         for (int k = 0; k < WREG / 4; ++k) {
-            const uint4 v = load_l2(s4 + k);
+            // (AK_POOL_RB: a chunk no lane of the batch needs is not loaded)
+            const uint4 v = (!AK_POOL_RB || k == 0 || w_ballot(4 * k < n)) ? load_l2(s4 + k) : make_uint4(0u, 0u, 0u, 0u);
             const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -880,6 +910,7 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
             }
         }
     }
+#endif
     uint32_t d[WREG / 2];
     // the batch's longest miss bounds the set-up: a pair no lane has is not looked up (each lookup
     // is a gather instruction, ~70 texture-path cycles whatever its active lanes)
@@ -921,6 +952,27 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
                 const uint32_t v = ((t < 2 ? w0 : w1) >> (16 * (t & 1))) & 0xFFFFu;
                 o[t] = (alive >> i) & 1u ? v : STAGE_DEAD;
             }
+#if AK_POOL_WB
+            // one store per lane and chunk: 4, 3, 2 or 1 dwords (a lane's tail is one access, not up
+            // to three)
+            const int rem = n - 4 * k;
+            if (rem >= 4) {
+                ((uint4 *)sp)[k] = make_uint4(o[0], o[1], o[2], o[3]);
+            } else if (rem == 3) {
+#ifdef AK_HOST_EMU
+                sp[4 * k] = o[0]; sp[4 * k + 1] = o[1]; sp[4 * k + 2] = o[2];
+#else
+                typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                u32x3 v3;
+                v3.x = o[0]; v3.y = o[1]; v3.z = o[2];
+                *(u32x3 *)(sp + 4 * k) = v3;
+#endif
+            } else if (rem == 2) {
+                *(uint2 *)(sp + 4 * k) = make_uint2(o[0], o[1]);
+            } else if (rem == 1) {
+                sp[4 * k] = o[0];
+            }
+#else
             if (4 * k + 3 < n) {
                 ((uint4 *)sp)[k] = make_uint4(o[0], o[1], o[2], o[3]);
             } else {
@@ -928,6 +980,7 @@ __device__ __forceinline__ void pool_flush(const TileArgs &ta, TileWaveMem &M, u
                 for (int t = 0; t < 3; ++t)
                     if (4 * k + t < n) sp[4 * k + t] = o[t];
             }
+#endif
         }
     }
     const uint32_t dead = (uint32_t)n - (uint32_t)__builtin_popcount(alive);
@@ -1282,12 +1335,40 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
         const uint32_t cls = ok ? pool_class(n) : 0xFFu;
         const uint64_t dst = sbase + (at & 0xFFFu);
         const uint4 ent = make_uint4((uint32_t)dst, (uint32_t)(dst >> 32) | (n << 16), (uint32_t)(r0 + (at >> 12)), 0u);
+#if AK_POOL_INLINE
+        // the miss's symbols (ids, WSTART cleared) from W: 9 aligned dwords + funnel shifts, as pass C
+        uint4 sa, sb;
+        {
+            const uint32_t *W32 = (const uint32_t *)M.w;
+            const int st = (int)(e & 1023u);
+            uint32_t wd[WREG / 2 + 1], pr[WREG / 2];
+#pragma unroll
+            for (int q = 0; q <= WREG / 2; ++q) wd[q] = W32[(st >> 1) + q];
+            const uint32_t sh = (uint32_t)(st & 1) * 16u;
+#pragma unroll
+            for (int q = 0; q < WREG / 2; ++q)
+#ifdef AK_HOST_EMU
+                pr[q] = (sh ? (wd[q] >> 16) | (wd[q + 1] << 16) : wd[q]) & 0x7FFF7FFFu;
+#else
+                pr[q] = __builtin_amdgcn_alignbit(wd[q + 1], wd[q], sh) & 0x7FFF7FFFu;
+#endif
+            sa = make_uint4(pr[0], pr[1], pr[2], pr[3]);
+            sb = make_uint4(pr[4], pr[5], pr[6], pr[7]);
+        }
+#endif
 #pragma unroll 1
         for (uint32_t c = 0; c < (uint32_t)POOL_NCLASS; ++c) {
             const uint64_t CM = w_ballot(cls == c);
             if (!CM) continue;
             const uint32_t head = w_bcast(M.phead[c], 0), k = w_bcast(M.pcnt[c], 0);
-            if (cls == c) pool[c * POOL_RING + (head + k + w_rank(CM)) % POOL_RING] = ent;
+            if (cls == c) {
+                const uint32_t slot = c * POOL_RING + (head + k + w_rank(CM)) % POOL_RING;
+                pool[slot] = ent;
+#if AK_POOL_INLINE
+                pool[POOL_CAP + 2 * slot] = sa;
+                pool[POOL_CAP + 2 * slot + 1] = sb;
+#endif
+            }
             w_sync();
             if (lane == 0) M.pcnt[c] = k + (uint32_t)w_popc(CM);
             w_sync();
@@ -1303,7 +1384,7 @@ __device__ __forceinline__ void bpe_tiles_wave(const TileArgs &ta, const uint32_
                                uint32_t wave_gid, uint32_t nwaves) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
-    uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_CAP;  // this wave's class rings
+    uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_U4;  // this wave's class rings
     if (w_lane() < POOL_NCLASS) {
         M.phead[w_lane()] = 0;
         M.pcnt[w_lane()] = 0;

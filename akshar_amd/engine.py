@@ -158,14 +158,30 @@ def decode_lists(model, rows, dev=None):
     return [b[o[i]:o[i + 1]].decode("utf-8", "surrogatepass") for i in range(n)]
 
 
+_TILING = {}  # workspace handle -> the (path, rows) it was last set to
+
+
+def set_tiling(ws, path):
+    """ak_ws_set_tiling, skipped when the workspace already holds the setting (the per-call path
+    runs it on every call)."""
+    t = (path, tile_rows())
+    if _TILING.get(ws.value) != t:
+        check(_lib.lib().ak_ws_set_tiling(ws, t[0], t[1]), "ak_ws_set_tiling")
+        _TILING[ws.value] = t
+
+
 def _encode_host(fn, name, h, dev, raw, flags, cap):
-    """One host string -> numpy int32 ids through ak_*_encode_host (pinned staging, one copy each
-    way, one synchronize)."""
-    ws = workspace(dev.index)
-    check(_lib.lib().ak_ws_set_tiling(ws, TILE_PATH, tile_rows()), "ak_ws_set_tiling")
+    """One host string -> numpy int32 ids through ak_*_encode_host: a row that fits one tile runs the
+    one-kernel path (one launch, the row and its ids in pinned host memory, one synchronize), any
+    other the host-staged batch sequence. The per-call Python work is kept to the lookups it needs."""
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ws = _WS.get((dev.index, stream))
+    if ws is None:
+        ws = workspace(dev.index)
+    set_tiling(ws, TILE_PATH)
     out = np.empty(max(cap, 1), dtype=np.int32)
     n = ctypes.c_uint64()
-    check(fn(h, ws, flags, raw, len(raw), out.ctypes.data, cap, ctypes.byref(n), _stream(dev)), name)
+    check(fn(h, ws, flags, raw, len(raw), out.ctypes.data, cap, ctypes.byref(n), ctypes.c_void_p(stream)), name)
     return out[:n.value]
 
 
@@ -198,7 +214,7 @@ def _run(fn_call, n, cap, make_out, dev, ws, out=None, out_offs=None):
 def _tiling(ws, path):
     """path 1 = tile-cooperative kernels for flags 3 (default), 0 = the one-lane-per-row kernels."""
     path = TILE_PATH if path is None else path
-    check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows()), "ak_ws_set_tiling")
+    set_tiling(ws, path)
 
 
 def normalize_batch(buf, offs, flags=3, row_status=None, path=None):
@@ -296,7 +312,8 @@ TILE_PATH = int(os.environ.get("AK_TILE_PATH", "1"))
 def tile_rows():
     """Rows per tile: tiles pack rows greedily up to their byte buffer, 16 rows at most;
     AK_TILE_ROWS overrides (development aid)."""
-    return int(os.environ.get("AK_TILE_ROWS", "16"))
+    v = os.environ.get("AK_TILE_ROWS")
+    return int(v) if v else 16
 
 
 class BPE:
@@ -377,7 +394,7 @@ class BPE:
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
         path = TILE_PATH if path is None else path
-        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows()), "ak_ws_set_tiling")
+        set_tiling(ws, path)
 
         def call(out, c, oo):
             check(_lib.lib().ak_bpe_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),
@@ -449,7 +466,7 @@ class SPM:
         if cap is None:
             cap = nbytes // 2 + 2 * n + 1024
         path = TILE_PATH if path is None else path
-        check(_lib.lib().ak_ws_set_tiling(ws, path, tile_rows()), "ak_ws_set_tiling")
+        set_tiling(ws, path)
 
         def call(out, c, oo):
             check(_lib.lib().ak_spm_encode(self.h, ws, flags, _ptr(buf), _ptr(offs), n, _ptr(out), c, _ptr(oo),

@@ -99,15 +99,19 @@ class aksharTokenizer:
             raise ValueError("need model for IDs")
         if self.model_type == "bpe":
             raw = text.encode("utf-8", "surrogatepass")
-            cuts_ok = not any(" " in c or "\n" in c for c, _ in self.model.model.added)  # no added token spans a cut
-            if len(raw) > longrows.LONG_ROW_BYTES and cuts_ok:  # one long row -> its exact pieces, stitched
+            if len(raw) > longrows.LONG_ROW_BYTES and self._cuts_ok():  # one long row -> its exact pieces, stitched
                 buf, offs = longrows.split_rows(raw)
                 gb, go = engine.to_device(buf, offs)
                 ids, oo = self.encode_packed(gb, go, nbytes=len(raw))
                 return [int(x) for x in longrows.stitch_bpe(ids.cpu().numpy(), oo.cpu().numpy())]
+            return self.model.encode_host(raw, self._flags).tolist()
         # SentencePiece: always one row (its lattice carries a float score across the whole row).
-        # One string: the host-staged single call (pinned staging, one copy each way, one sync)
+        # One string: the per-call path (one kernel for a row that fits a tile, else host staging)
         return self.model.encode_host(text.encode("utf-8", "surrogatepass"), self._flags).tolist()
+
+    def _cuts_ok(self):
+        """No added token spans a long-row cut point (' ' or '\n' inside one)."""
+        return not any(" " in c or "\n" in c for c, _ in self.model.model.added)
 
     def decode(self, ids: List[int]) -> str:
         """tokenizer.py:195-219, on the device (ak_bpe_decode / ak_spm_decode)."""

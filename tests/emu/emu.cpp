@@ -309,7 +309,7 @@ extern "C" int64_t emu_bpe_tiles(void *model, int flags, const uint8_t *in, cons
     std::vector<TileWaveMem> M(g_waves);
     std::vector<uint64_t> prof(T_NPROF, 0);
     ta.passprof = prof.data();  // the pass clocks read 0 here; the counters are real
-    std::vector<uint4> pool((size_t)g_waves * POOL_CAP);
+    std::vector<uint4> pool((size_t)g_waves * POOL_U4);
     std::vector<uint32_t> unit_len(nunits);
     ta.pool = pool.data();
     ta.unit_len = unit_len.data();

@@ -13,14 +13,17 @@ _L = None
 def lib():
     global _L
     if _L is None:
-        so = os.path.join(HERE, "_emu.so")
+        # AK_EMU_DEFINES="AK_POOL_WB=1,..." (development aid): a build of those variants, its own .so
+        defs = [d for d in os.environ.get("AK_EMU_DEFINES", "").split(",") if d]
+        so = os.path.join(HERE, "_emu%s.so" % ("_" + "_".join(d.replace("=", "") for d in defs) if defs else ""))
         srcs = [os.path.join(HERE, "emu.cpp")] + [os.path.join(HERE, "..", "..", "akshar_amd", "csrc", f) for f in
                                                    ("ak_dev.h", "ak_rows.h", "ak_model_build.h", "ak_host_emu.h", "ak_ptc.h", "ak_swc.h",
                                                     "ak_tile.h", "ak_tile_spm.h", "ak_tile_rows.h", "ak_wave.h", "ak_nfc_wave.h")]
         srcs.append(os.path.join(HERE, "..", "..", "include", "akshar.h"))
         if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
             subprocess.check_call(["g++", "-O2", "-std=c++20", "-pthread", "-fPIC", "-shared", "-I",
-                                   os.path.join(HERE, "..", "..", "include"), "-o", so, srcs[0]], cwd=HERE)
+                                   os.path.join(HERE, "..", "..", "include")] + ["-D" + d for d in defs] +
+                                  ["-o", so, srcs[0]], cwd=HERE)
         L = ctypes.CDLL(so)
         L.emu_bpe_create.restype = P
         L.emu_bpe_create.argtypes = [ctypes.c_uint32, P, P, ctypes.c_uint32, P, ctypes.c_uint32, ctypes.c_uint32]

@@ -222,3 +222,38 @@ def test_single_call_bpe_nfkc_expansion():
         got = [tk.encode(t) for t in texts]
         assert got == tk.encode_batch(texts), nr
         assert max(len(g) - len(t.encode()) for g, t in zip(got, texts)) > 0  # more ids than bytes
+
+
+@gpu
+def test_single_call_one_kernel_path_and_its_fallbacks(monkeypatch):
+    """encode(str) of a row that fits one tile runs ONE kernel (k_bpe_small / k_spm_small: the row
+    and its ids in fine-grained pinned memory); a row the tile front end cannot take (NFC changes
+    it, HF's NFKC changes it, it is over the tile buffer) reports back and takes the batch sequence.
+    Every case equals the batch path, the batch sequence alone (AK_NO_SMALL=1) and the oracle, for
+    both models: plain Hinglish, rows at and past the tile buffers (480 / 768 bytes), a pre-token of
+    >= 16 symbols (merged in the tile), many merge-pool misses, NFC / HF-NFKC / precomposed nukta
+    rows, lone surrogates (invalid UTF-8 after surrogatepass), empty and one-char rows."""
+    import numpy as np
+    from akshar_amd import engine
+    from akshar_amd.models import BPEModel, SPMModel
+    from oracle import oracle as O
+    texts = ["aaj मौसम बहुत अच्छा है yaar!!", "Heyyy यार kya HAAL hai", "", "x", "क",
+             "a" * 479, "a" * 480, "a b " * 120, "क्ष" * 85, "ख" * 256, "ख" * 257,
+             "supercalifragilisticexpialidocious antidisestablishmentarianism",
+             " ".join("कमलनयनपुष्प%d" % i for i in range(30)),
+             "café", "café", "Å ﬁ ① ™", "ज़िंदगी फ़िर", "क़ि", "ud800:\ud800 end",
+             "Ḳ́x ạ́b", "ok " * 200 + "́"]
+    oracle_bpe = O.OracleBPE(BPEModel(BPE_PATH))
+    oracle_spm = O.OracleSPM(SPMModel(SPM_PATH))
+    for mp, mt, orc in ((BPE_PATH, "bpe", oracle_bpe), (SPM_PATH, "sentencepiece", oracle_spm)):
+        tk = aksharTokenizer(model_path=mp, model_type=mt)
+        one = [tk.encode(t) for t in texts]
+        assert one == tk.encode_batch(texts), mt
+        for t, got in zip(texts, one):
+            raw = t.encode("utf-8", "surrogatepass")
+            b = np.frombuffer(raw + b"\0" * 16, dtype=np.uint8).copy()
+            ref, ro = orc.encode_batch(b, np.array([0, len(raw)], dtype=np.uint64))
+            assert got == [int(x) for x in ref], (mt, t[:40])
+        monkeypatch.setenv("AK_NO_SMALL", "1")
+        assert [tk.encode(t) for t in texts] == one, mt
+        monkeypatch.delenv("AK_NO_SMALL")

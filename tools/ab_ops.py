@@ -18,7 +18,10 @@ rows = int(os.environ.get("AB_ROWS", "1000000"))
 res = {"variant": os.environ.get("AK_LIB_VARIANT", "default"), "env": os.environ.get("AB_TAG", "")}
 spm = engine.SPM(os.path.join(ROOT, "models", "akshar.model"))
 bpe = engine.BPE(os.path.join(ROOT, "models", "akshar.json"))
-for kind, name in ((0, "deva"), (1, "hing")):
+kinds = [(0, "deva"), (1, "hing")]
+if os.environ.get("AB_KINDS"):  # e.g. "hing"
+    kinds = [k for k in kinds if k[1] in os.environ["AB_KINDS"].split(",")]
+for kind, name in kinds:
     buf, offs = synth.generate(kind, rows, seed=1241)
     pad = np.zeros(len(buf) + 32, np.uint8)
     pad[:len(buf)] = buf

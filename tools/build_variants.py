@@ -1,5 +1,6 @@
 """Development aid: build library variants for an A/B run on the GPU box (AK_LIB_VARIANT=<name>).
-  python tools/build_variants.py name:DEF1=1,DEF2=2[:nolicm] ..."""
+  python tools/build_variants.py name:DEF1=1,DEF2=2[:nolicm][:only=a.hip+b.hip] ...
+only=: compile just those TUs with the defines (the rest link the default build's objects)."""
 import os
 import sys
 
@@ -11,4 +12,5 @@ for spec in sys.argv[1:]:
     name = parts[0]
     defs = [d for d in (parts[1].split(",") if len(parts) > 1 and parts[1] else []) if d]
     flags = dict(_build.TU_FLAGS) if "licm" not in parts[2:] else {}
-    print(_build.build_variant(name, defs, flags))
+    only = next((p[5:].split("+") for p in parts[2:] if p.startswith("only=")), None)
+    print(_build.build_variant(name, defs, flags, only=only))
