@@ -575,6 +575,7 @@ extern "C" void ak_ws_free(ak_ws *w) {
     (void)hipFree(w->redo);
     (void)hipFree(w->fb3);
     (void)hipFree(w->nfc_buf);
+    (void)hipFree(w->rnfc_buf);
     (void)hipFree(w->comp_hash);
     (void)hipFree(w->counts);
     (void)hipFree(w->slow_list);

@@ -75,6 +75,8 @@ struct AkWs {
     uint4 *comp_hash = nullptr;     // fallback waves: the composition pairs' hash (ak_nfc_wave.h), built once
     uint8_t *nfc_buf = nullptr;     // k_bpe_nfc / k_spm_nfc: per-wave epochs (ak_nfc_wave.h NE_BYTES each)
     uint64_t cap_nfc = 0;           // ... waves
+    uint8_t *rnfc_buf = nullptr;    // k_rows_nfc: per-wave epochs (ak_tile_rows.h RE_BYTES each)
+    uint64_t cap_rnfc = 0;          // ... waves
     uint64_t *tile_passprof = nullptr;  // per-pass cycles (profiling only)
     int tile_rows = 16;
     int bpe_path = 1;               // 1 tile-cooperative, 0 one lane per row (staged row kernel)

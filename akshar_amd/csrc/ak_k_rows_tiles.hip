@@ -35,6 +35,29 @@ __global__ __launch_bounds__(RT_BLOCK) void k_rows_tiles(TileArgs ta, RowsOut o)
                          gridDim.x * (RT_BLOCK / 64));
 }
 
+// The tile kernel's fallback rows in the waves' epochs (ak_tile_rows.h rows_nfc_wave): NFC by
+// segments, rows_tile<OPS, NFCD> over the NFC text, the outputs to the rows' fallback slots; the
+// rows it cannot take go on to k_rows_tile_fb through fb3.
+constexpr int RT_NFC_BLOCK = 512;  // 8 waves (NfcWaveLds<RowsWaveMem>)
+template <int OPS>
+__global__ __launch_bounds__(RT_NFC_BLOCK) void k_rows_nfc(TileArgs ta, RowsOut ofb, uint8_t *ebuf, uint32_t *fb3,
+                                                           uint32_t *fb3_count) {
+    __shared__ uint32_t hot_tab[HOT_N];
+    __shared__ uint16_t sc_tab[HOT_N];
+    __shared__ uint2 fast[FAST_N];
+    __shared__ NfcWaveLds<RowsWaveMem> wl[RT_NFC_BLOCK / 64];
+    if (*ta.fb_count == 0) return;  // uniform: the common case
+    for (uint32_t i = threadIdx.x; i < HOT_N; i += RT_NFC_BLOCK) {
+        const uint32_t cp = hot_cp(i);
+        hot_tab[i] = hot_word(cp);
+        sc_tab[i] = seg_class_of(cp);
+    }
+    stage_tables(fast, nullptr, nullptr, false);  // (syncs the block)
+    const uint32_t wave = threadIdx.x >> 6;
+    rows_nfc_wave<OPS>(ta, ofb, ebuf, fb3, fb3_count, hot_tab, sc_tab, fast, wl[wave],
+                       blockIdx.x * (RT_NFC_BLOCK / 64) + wave, gridDim.x * (RT_NFC_BLOCK / 64));
+}
+
 // fallback rows with small buffers in LDS (private arrays would be scratch)
 constexpr int RT_FB_LANE_U32 = 10 * FAST_SEG;
 
@@ -127,8 +150,9 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     ta.ntiles = ntiles;
     ta.unit_fb = w->unit_fb;
     ta.rows = std::min(w->tile_rows, T_MAXR);
-    // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count
-    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 4 * 4, st));
+    // fallback count, overflow flag (ak_ws_check reports this call's), second fallback count, the
+    // unit queue, [5] the rows k_rows_nfc passes on; [6] = 0: not a SentencePiece launch
+    HIP_TRY(hipMemsetAsync(w->tile_misc, 0, 8 * 4, st));
     HIP_TRY(hipMemsetAsync(w->ctr, 0, CTR_N * 4, st));
     const uint64_t wpb = RT_BLOCK / 64;
     const unsigned grid = (unsigned)std::min<uint64_t>((ntiles + wpb - 1) / wpb, (uint64_t)num_cus() * g_rt_bpc[OPS]);
@@ -136,9 +160,44 @@ static int launch_ops(AkWs *w, const RowArgs &a0, const RowsOut &o0, const RowsO
     k_rows_tiles<OPS><<<grid, RT_BLOCK, 0, st>>>(ta, o0);
     AK_PROF(AK_PROF_ROW_TILES, true, st);
     HIP_TRY(hipGetLastError());
+    TileArgs tfb = ta;
+    if (!getenv("AK_NO_NFC_WAVE")) {  // (development aid: the one-lane path for every fallback row)
+        AK_PROF(AK_PROF_FALLBACK_WAVE, false, st);
+        const unsigned ngrid = (unsigned)num_cus();
+        const uint64_t nw = (uint64_t)ngrid * (RT_NFC_BLOCK / 64);
+        if (w->cap_rnfc < nw) {
+            (void)hipFree(w->rnfc_buf);
+            w->rnfc_buf = nullptr;
+            w->cap_rnfc = 0;
+            HIP_TRY(hipMalloc(&w->rnfc_buf, nw * RE_BYTES));
+            w->cap_rnfc = nw;
+        }
+        if (w->cap_fb3 < a0.n) {
+            (void)hipFree(w->fb3);
+            w->fb3 = nullptr;
+            HIP_TRY(hipMalloc(&w->fb3, a0.n * 4));
+            w->cap_fb3 = a0.n;
+        }
+        if (!w->comp_hash) {  // built once per workspace
+            HIP_TRY(hipMalloc(&w->comp_hash, CH_SLOTS * sizeof(uint4)));
+            HIP_TRY(hipMemsetAsync(w->comp_hash, 0, CH_SLOTS * sizeof(uint4), st));
+            k_comp_hash_build<><<<(AK_UT_NCOMP + 255) / 256, 256, 0, st>>>(w->comp_hash);
+            HIP_TRY(hipGetLastError());
+        }
+        tfb.comp_hash = w->comp_hash;
+        // (no more waves than rows: a small call dispatches a block or two)
+        const unsigned lgrid = (unsigned)std::min<uint64_t>(ngrid, (a0.n + RT_NFC_BLOCK / 64 - 1) / (RT_NFC_BLOCK / 64));
+        k_rows_nfc<OPS><<<lgrid, RT_NFC_BLOCK, 0, st>>>(tfb, ofb, w->rnfc_buf, w->fb3, w->tile_misc + 5);
+        HIP_TRY(hipGetLastError());
+        AK_PROF(AK_PROF_FALLBACK_WAVE, true, st);
+        tfb.fb_list = w->fb3;
+        tfb.fb_count = w->tile_misc + 5;
+    } else {  // every fallback row goes on (ak_ws_fallback_detail)
+        HIP_TRY(hipMemcpyAsync(w->tile_misc + 5, w->tile_misc, 4, hipMemcpyDeviceToDevice, st));
+    }
     AK_PROF(AK_PROF_EMIT_SLOW, false, st);
     static std::atomic<int> fb_bpc{0};
-    k_rows_tile_fb<OPS><<<resident_grid(k_rows_tile_fb<OPS>, RT_FB_BLOCK, fb_bpc), RT_FB_BLOCK, 0, st>>>(ta, ofb, w->ctr + CTR_ERR);
+    k_rows_tile_fb<OPS><<<resident_grid(k_rows_tile_fb<OPS>, RT_FB_BLOCK, fb_bpc), RT_FB_BLOCK, 0, st>>>(tfb, ofb, w->ctr + CTR_ERR);
     RowArgs ra = ta.ra;
     ra.err = w->ctr + CTR_ERR;
     k_rows_tile_tier<OPS><<<SLOW_THREADS / 64, 64, 0, st>>>(ra, ofb, slow_tier(w, w->fb2, ta.fb2_count));

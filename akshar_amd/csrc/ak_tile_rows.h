@@ -18,6 +18,7 @@
 // (never from normalize_text) goes to the fallback row kernels with the rows whose NFC quick check
 // trips or that hold invalid UTF-8.
 #pragma once
+#include "ak_nfc_wave.h"
 #include "ak_rows.h"
 #include "ak_tile.h"
 
@@ -80,13 +81,14 @@ __device__ __forceinline__ bool gcb_tile_ok(uint32_t cls) {
                             g == GCB_ZWJ || g == GCB_SPACINGMARK || g == GCB_PREPEND);
 }
 
-template <int OPS>
+// NFCD: the rows are NFC already (the fallback waves' epochs, ak_nfc_wave.h): no NFC proof
+template <int OPS, bool NFCD = false>
 __device__ int rows_tile(const TileArgs &ta, const RowsOut &o, uint64_t r0, uint64_t rend, const uint32_t *H,
                          const uint16_t *SC, RowsWaveMem &M, PassClock &pc) {
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<R_BCAP>(a, r0, rend, H, M);
+    const TileRows tr = tile_front<R_BCAP, RowsWaveMem, NFCD>(a, r0, rend, H, M);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
     pc.mark(TP_D);
@@ -350,6 +352,144 @@ __device__ void rows_tiles_wave(const TileArgs &ta, const RowsOut &o, const uint
         if (w_lane() == 0) ta.unit_fb[t] = M.ufbm;
     }
     pc.flush(ta.passprof);
+}
+
+// ---------------------------------------------------------------- fallback rows in the waves' epochs
+// The row tiles' fallback rows (k_rows_nfc, ak_k_rows_tiles.hip) as the BPE / SentencePiece ones
+// (ak_nfc_wave.h): each wave gathers an epoch of rows, NFC-normalizes them by segments back to back
+// into the epoch's text (nfc_epoch_gather), runs rows_tile<OPS, NFCD> over that text R rows at a
+// time into the epoch's output regions, then copies each row's normalized bytes, cluster ends and
+// run ends + labels to its fallback slots (RT_* slot rules) with its counts. A row the wave cannot
+// take (invalid UTF-8, over the tile buffer, a segment past NW_DCAP) or that the tile sends on again
+// (a grapheme class the tile path does not implement), or whose outputs pass its slots, goes on to
+// the one-lane kernel through fb3.
+constexpr uint64_t RE_TEXT_B = NE_TEXT_B, RE_OFFS_B = NE_OFFS_B;
+constexpr uint64_t RE_CNT_B = 3 * NE_VMAX * 4, RE_FB_B = NE_VMAX * 4 + 16;
+constexpr uint64_t RE_NORM_B = (2 * NE_TCAP + 2 * NE_VMAX + 256 + 15) / 16 * 16;  // normalized bytes
+constexpr uint64_t RE_END_N = NE_TCAP + 2 * NE_VMAX + 64;                         // cluster / run ends (u32)
+constexpr uint64_t RE_BYTES = (RE_TEXT_B + RE_OFFS_B + RE_CNT_B + RE_FB_B + RE_NORM_B + 2 * RE_END_N * 4 + RE_END_N +
+                               255) / 256 * 256;  // per wave
+
+struct RowsEpoch {
+    NfcEpoch e;                     // text, voffs, vfb, vfbc (nfc_epoch_gather / the tile's fallback list)
+    uint32_t *cnt;                  // [3][NE_VMAX]: norm bytes, cluster ends, runs per virtual row (~0: none)
+    uint8_t *norm, *labels;
+    uint32_t *seg, *runs;
+};
+__device__ __forceinline__ RowsEpoch rows_epoch(uint8_t *ebuf, uint32_t wave_gid) {
+    uint8_t *b = ebuf + (uint64_t)wave_gid * RE_BYTES;
+    RowsEpoch R;
+    R.e.text = b;
+    R.e.voffs = (uint64_t *)(b + RE_TEXT_B);
+    R.cnt = (uint32_t *)(b + RE_TEXT_B + RE_OFFS_B);
+    R.e.vcnt = R.cnt;
+    R.e.vfb = (uint32_t *)(b + RE_TEXT_B + RE_OFFS_B + RE_CNT_B);
+    R.e.vfbc = R.e.vfb + NE_VMAX;
+    R.e.region = nullptr;
+    uint8_t *q = b + RE_TEXT_B + RE_OFFS_B + RE_CNT_B + RE_FB_B;
+    R.norm = q;
+    R.seg = (uint32_t *)(q + RE_NORM_B);
+    R.runs = R.seg + RE_END_N;
+    R.labels = (uint8_t *)(R.runs + RE_END_N);
+    return R;
+}
+
+template <int OPS>
+__device__ __forceinline__ void rows_epoch_finish(const TileArgs &ta, const RowsOut &ofb, const RowsEpoch &E, NfcRows &R,
+                                                  uint32_t v, uint32_t *fb3, uint32_t *fb3_count) {
+    const int lane = w_lane();
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the regions' outputs and counts have landed (this wave's stores)
+#endif
+    uint64_t s0 = 0, s1 = 0, s2 = 0;  // the virtual row's first output in each region (rows that emitted, in order)
+    for (uint32_t j = 0; j < v; ++j) {
+        const uint64_t r = R.vrow[j];
+        const uint32_t c0 = (OPS & RT_NORM) ? E.cnt[j] : 0u;
+        const uint32_t c1 = (OPS & RT_SEG) ? E.cnt[NE_VMAX + j] : 0u;
+        const uint32_t c2 = (OPS & RT_SW) ? E.cnt[2 * NE_VMAX + j] : 0u;
+        const bool emitted = c0 != 0xFFFFFFFFu && c1 != 0xFFFFFFFFu && c2 != 0xFFFFFFFFu;
+        const uint64_t b = ta.ra.offs[r], len = ta.ra.offs[r + 1] - b;
+        const bool fits = (uint64_t)c0 <= RT_NORM_MUL * len + RT_NORM_ADD && (uint64_t)c1 <= RT_SEG_MUL * len + RT_SEG_ADD &&
+                          (uint64_t)c2 <= RT_SEG_MUL * len + RT_SEG_ADD;
+        if (!emitted || R.vfail[j] || !fits) {
+            nfc_fb3(fb3, fb3_count, r);
+        } else {
+            if constexpr ((OPS & RT_NORM) != 0) {
+                uint8_t *d = ofb.norm + RT_NORM_MUL * b + RT_NORM_ADD * r;
+                for (uint32_t k = (uint32_t)lane; k < c0; k += 64) d[k] = E.norm[s0 + k];
+            }
+            if constexpr ((OPS & RT_SEG) != 0) {
+                uint32_t *d = ofb.seg + RT_SEG_MUL * b + RT_SEG_ADD * r;
+                for (uint32_t k = (uint32_t)lane; k < c1; k += 64) d[k] = E.seg[s1 + k];
+            }
+            if constexpr ((OPS & RT_SW) != 0) {
+                uint32_t *d = ofb.runs + RT_SEG_MUL * b + RT_SEG_ADD * r;
+                uint8_t *dl = ofb.labels + RT_SEG_MUL * b + RT_SEG_ADD * r;
+                for (uint32_t k = (uint32_t)lane; k < c2; k += 64) {
+                    d[k] = E.runs[s2 + k];
+                    dl[k] = E.labels[s2 + k];
+                }
+            }
+            if (lane == 0) {
+                if constexpr ((OPS & RT_NORM) != 0) ofb.cnt_norm[r] = c0;
+                if constexpr ((OPS & RT_SEG) != 0) ofb.cnt_seg[r] = c1;
+                if constexpr ((OPS & RT_SW) != 0) ofb.cnt_runs[r] = c2;
+                if (ta.ra.row_status) ta.ra.row_status[r] = 0;
+            }
+        }
+        if (emitted) {  // (its outputs occupy the regions whether or not it fits its slots)
+            s0 += c0;
+            s1 += c1;
+            s2 += c2;
+        }
+    }
+}
+
+// a fallback wave of the row tiles: epochs as bpe_nfc_wave (ak_nfc_wave.h)
+template <int OPS>
+__device__ void rows_nfc_wave(const TileArgs &ta, const RowsOut &ofb, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count,
+                              const uint32_t *H, const uint16_t *SC, const uint2 *fast, NfcWaveLds<RowsWaveMem> &L,
+                              uint32_t wave_gid, uint32_t nwaves) {
+    const uint32_t nl = *ta.fb_count;
+    const int lane = w_lane();
+    RowsWaveMem &M = L.t;
+    const RowsEpoch E = rows_epoch(ebuf, wave_gid);
+    TileArgs tl = ta;
+    tl.ra.in = E.e.text;
+    tl.ra.offs = E.e.voffs;
+    tl.ra.row_status = nullptr;
+    tl.fb_list = E.e.vfb;
+    tl.fb_count = E.e.vfbc;
+    RowsOut eo = ofb;
+    eo.norm = E.norm;
+    eo.seg = E.seg;
+    eo.runs = E.runs;
+    eo.labels = E.labels;
+    eo.norm_cap = RE_NORM_B;
+    eo.seg_cap = RE_END_N;
+    eo.cnt_norm = E.cnt;
+    eo.cnt_seg = E.cnt + NE_VMAX;
+    eo.cnt_runs = E.cnt + 2 * NE_VMAX;
+    PassClock pc;
+    pc.init(false, M.passacc);
+    for (uint32_t i = wave_gid; i < nl;) {
+        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E.e, L.n, L.rows, fast, fb3, fb3_count);
+        if (v == 0) continue;
+        for (uint32_t k = (uint32_t)lane; k < 3 * NE_VMAX; k += 64) E.cnt[k] = 0xFFFFFFFFu;  // (a row the tile sends on keeps ~0)
+        if (lane == 0) {  // the tile's buffers over the NFC scratch: its lasting fields set again
+            M.un_norm = M.un_seg = M.un_runs = 0;
+            M.ufbm = 0;
+        }
+#ifndef AK_HOST_EMU
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        w_sync();
+        for (uint32_t r = 0; r < v;) {
+            const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
+            r += (uint32_t)rows_tile<OPS, true>(tl, eo, r, re, H, SC, M, pc);
+        }
+        rows_epoch_finish<OPS>(ta, ofb, E, L.rows, v, fb3, fb3_count);
+    }
 }
 
 }  // namespace ak

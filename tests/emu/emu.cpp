@@ -570,6 +570,26 @@ static int64_t rows_tiles_run(int matras, const uint8_t *in, const uint64_t *off
     delete M;
     if (err) return -1;
     g_last_fb = fbn;
+    // fallback rows as k_rows_nfc: the waves' epochs (NFC, rows_tile<OPS, NFCD>, the rows' slots);
+    // the rows it cannot take go on in fb3
+    if (!getenv("AK_NO_NFC_WAVE")) {
+        std::vector<uint32_t> fb3(n);
+        uint32_t fb3n = 0;
+        std::vector<uint8_t> ebuf((size_t)g_waves * RE_BYTES);
+        std::vector<NfcWaveLds<RowsWaveMem>> NL(g_waves);
+        TileArgs tn = ta;
+        tn.comp_hash = comp_hash_table();
+        run_waves([&](int w) {
+            rows_nfc_wave<OPS>(tn, ofb, ebuf.data(), fb3.data(), &fb3n, hot_tab, sc_tab, fast, NL[w], (uint32_t)w,
+                               (uint32_t)g_waves);
+        });
+        if (err) return -1;
+        g_last_nfc = fbn - fb3n;
+        fbl.assign(fb3.begin(), fb3.begin() + fb3n);
+        fbn = fb3n;
+    } else {
+        g_last_nfc = 0;
+    }
     uint64_t maxlen = 0;
     for (uint64_t r = 0; r < n; ++r) maxlen = std::max<uint64_t>(maxlen, offs[r + 1] - offs[r]);
     const uint64_t C = std::max<uint64_t>(SLOW_CAP, 3 * maxlen + 64);
