@@ -959,16 +959,13 @@ template <class Small>
 static int encode_small(ak_ws *w, const uint8_t *text, uint64_t len, int32_t *ids, uint64_t cap, uint64_t *n_ids,
                         Small small, bool *done) {
     *done = false;
-    if (len + 48 > SC_RES) return AK_OK;
-    int rc = small_call_reserve(w);
-    if (rc) return rc;
-    uint64_t *po = (uint64_t *)w->pin_small;
-    po[0] = 0;
-    po[1] = len;
-    if (len) memcpy(w->pin_small + 16, text, len);
-    memset(w->pin_small + 16 + len, 0, 32);
+    if (len + 16 > SC_ROW_B) return AK_OK;
+    SmallRow row;  // the row as the kernel's argument, zero slack after it
+    if (len) memcpy(row.b, text, len);
+    memset(row.b + len, 0, SC_ROW_B - len);
     uint32_t status = 2;
-    if ((rc = small(&status))) return rc;
+    int rc = small(row, &status);
+    if (rc) return rc;
     if (status != 0) return AK_OK;
     const volatile uint32_t *res = (const volatile uint32_t *)(w->pin_small + SC_RES);
     const uint32_t n = res[1], err = res[2], live = res[3];
@@ -1054,8 +1051,8 @@ extern "C" int ak_bpe_encode_host(const ak_bpe *m, ak_ws *w, int flags, const ui
         a.bpe = m->dev;
         a.single_fast = m->d_single_fast;
         *n_ids = 0;
-        const int rc = encode_small(w, text, len, ids, cap, n_ids, [&](uint32_t *status) {
-            return small_call_bpe(w, a, len, (hipStream_t)stream, status);
+        const int rc = encode_small(w, text, len, ids, cap, n_ids, [&](const SmallRow &row, uint32_t *status) {
+            return small_call_bpe(w, a, row, len, (hipStream_t)stream, status);
         }, &done);
         if (rc || done) return rc;
     }
@@ -1073,8 +1070,8 @@ extern "C" int ak_spm_encode_host(const ak_spm *m, ak_ws *w, int flags, const ui
         RowArgs a = make_args(nullptr, nullptr, 1, nullptr, 0, nullptr);
         a.spm = m->dev;
         *n_ids = 0;
-        const int rc = encode_small(w, text, len, ids, cap, n_ids, [&](uint32_t *status) {
-            return small_call_spm(w, a, m->d_scode, len, (hipStream_t)stream, status);
+        const int rc = encode_small(w, text, len, ids, cap, n_ids, [&](const SmallRow &row, uint32_t *status) {
+            return small_call_spm(w, a, m->d_scode, row, len, (hipStream_t)stream, status);
         }, &done);
         if (rc || done) return rc;
     }

@@ -93,6 +93,7 @@ struct AkWs {
     uint8_t *pin_small = nullptr;   // fine-grained (coherent) pinned host memory the kernel reads and writes
     uint8_t *pin_small_dev = nullptr;  // ... its device address
     uint8_t *dev_small = nullptr;   // device scratch: counters, the unit run, the merge pool, the hot table
+    uint32_t small_seq = 0;         // the small calls' sequence number (tags the status word)
 };
 
 // The one-kernel per-call path (ak_bpe_encode_host / ak_spm_encode_host of a row that fits one
@@ -101,12 +102,19 @@ struct AkWs {
 // launch and one synchronize instead of the batch sequence (init, tile kernel, fallback waves,
 // one-lane kernel, tiers, scan, copy, two copies). A row the tile front end sends to the fallback
 // kernels reports status 1 and the caller runs the batch sequence for it.
-constexpr uint64_t SC_PIN_BYTES = 16384;     // pinned: offs (16 B) | bytes (T_BCAP + 32) | results at SC_RES
-constexpr uint64_t SC_RES = 1024;            // res[0] status, [1] count, [2] error flags, [3] live entries; ids at +16
+constexpr uint64_t SC_PIN_BYTES = 16384;     // pinned: results at SC_RES (the ids the kernel writes)
+constexpr uint64_t SC_RES = 1024;            // res[0] seq << 2 | status, [1] count, [2] error flags, [3] live entries; ids at +16
+constexpr uint64_t SC_ROW_B = 784;           // the row travels as a kernel argument (T_BCAP + 16 bytes of zero slack)
+struct SmallRow {
+    alignas(16) uint8_t b[SC_ROW_B];
+};
 constexpr uint64_t SC_STAGE = 4096;          // u32 entries of the device unit run
 constexpr uint64_t SC_DEV_BYTES = 64 * 4 + SC_STAGE * 4 + 1024 * 16 + 1024 * 4 + 16 + 1024;  // counters | run | pool | hot | offs | row
-int small_call_bpe(AkWs *w, const RowArgs &a, uint64_t len, hipStream_t st, uint32_t *status);
-int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, uint64_t len, hipStream_t st, uint32_t *status);
+int small_call_bpe(AkWs *w, const RowArgs &a, const SmallRow &row, uint64_t len, hipStream_t st, uint32_t *status);
+int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, const SmallRow &row, uint64_t len, hipStream_t st,
+                   uint32_t *status);
+// waits for the small call's status word in pinned memory (a bounded spin, then the stream)
+int small_call_wait(AkWs *w, hipStream_t st, uint32_t seq, uint32_t *status);
 // the SentencePiece tile kernels' LDS code table (HOT_N u16), built once per model for the small calls
 int build_spm_scode(const SpmDev &dev, uint16_t **out);
 int small_call_reserve(AkWs *w);

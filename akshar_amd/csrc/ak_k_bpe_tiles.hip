@@ -554,13 +554,14 @@ int launch_bpe_tiles(int flags, AkWs *w, const RowArgs &a0, uint64_t *out_offs, 
 }
 
 // One row (ta.ra.n == 1, at most T_BCAP bytes) through bpe_tile and the merge pool by ONE wave.
-__global__ __launch_bounds__(64) void k_bpe_small(TileArgs ta, uint8_t *dsmall, const uint8_t *hrow, uint64_t len, uint32_t *res) {
+__global__ __launch_bounds__(64) void k_bpe_small(TileArgs ta, uint8_t *dsmall, SmallRow row, uint64_t len, uint32_t *res,
+                                                 uint32_t seq) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t sfast[SFAST_N];
     __shared__ TileWaveMem M;
     const SmallDev sd = small_dev(dsmall);
     const int lane = w_lane();
-    small_stage_row(hrow, len, sd.row, sd.offs);
+    small_stage_row(row, len, sd.row, sd.offs);
     for (uint32_t i = lane; i < HOT_N; i += 64) hot_tab[i] = sd.hot[i];
     for (uint32_t i = lane; i < SFAST_N; i += 64) sfast[i] = ta.ra.single_fast[i < 0x80u ? i : i - 0x80u + 0x900u];
     if (lane < POOL_NCLASS) {
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(64) void k_bpe_small(TileArgs ta, uint8_t *dsmall, 
 #else
     const uint32_t cnt = ta.counts[0];
 #endif
-    small_finish(sd, run_len, fb, cnt, res);
+    small_finish(sd, run_len, fb, cnt, res, seq);
 }
 
 int small_call_reserve(AkWs *w) {
@@ -604,19 +605,40 @@ int small_call_reserve(AkWs *w) {
     return AK_OK;
 }
 
-int small_call_bpe(AkWs *w, const RowArgs &a, uint64_t len, hipStream_t st, uint32_t *status) {
+int small_call_bpe(AkWs *w, const RowArgs &a, const SmallRow &row, uint64_t len, hipStream_t st, uint32_t *status) {
     *status = 2;
     if (len > (uint64_t)T_BCAP) return AK_OK;  // no tile buffer holds the row: the batch sequence
     int rc = small_call_reserve(w);
     if (rc) return rc;
     TileArgs ta = small_args(w, a);
     uint32_t *res = (uint32_t *)(w->pin_small_dev + SC_RES);
+    const uint32_t seq = small_next_seq(w);
     AK_PROF(AK_PROF_TILES, false, st);
-    k_bpe_small<<<1, 64, 0, st>>>(ta, w->dev_small, w->pin_small_dev + 16, len, res);
+    k_bpe_small<<<1, 64, 0, st>>>(ta, w->dev_small, row, len, res, seq);
     AK_PROF(AK_PROF_TILES, true, st);
     HIP_TRY(hipGetLastError());
+    return small_call_wait(w, st, seq, status);
+}
+
+// Spin (bounded) on the status word the kernel writes last (ak_small.h small_finish): done as soon
+// as it carries this call's sequence number, without the launch's completion signal and the cache
+// write-back of its end; past the bound, the stream's synchronize reports a fault or gives the
+// kernel the time it needs.
+int small_call_wait(AkWs *w, hipStream_t st, uint32_t seq, uint32_t *status) {
+    const volatile uint32_t *res = (const volatile uint32_t *)(w->pin_small + SC_RES);
+    for (int i = 0; i < 2000000; ++i) {
+        const uint32_t x = res[0];
+        if ((x >> 2) == (seq & 0x3FFFFFFFu)) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            *status = x & 3u;
+            return AK_OK;
+        }
+        if ((i & 1023) == 1023 && hipStreamQuery(st) == hipSuccess) break;  // (finished: re-read below)
+    }
     HIP_TRY(hipStreamSynchronize(st));
-    *status = ((volatile uint32_t *)(w->pin_small + SC_RES))[0];
+    const uint32_t x = res[0];
+    if ((x >> 2) != (seq & 0x3FFFFFFFu)) return set_error(AK_ERR_HIP, "internal: the per-call kernel wrote no status");
+    *status = x & 3u;
     return AK_OK;
 }
 

@@ -69,14 +69,14 @@ int build_spm_scode(const SpmDev &dev, uint16_t **out) {
 // The per-call path (ak_internal.h SmallCall): one row of at most S_BCAP bytes through the tile
 // variant (every word solved in the tile, the carried base for close calls) by ONE wave; ids and the
 // count straight to pinned host memory (ak_small.h small_finish).
-__global__ __launch_bounds__(64) void k_spm_small(TileArgs ta, const uint16_t *scode_g, uint8_t *dsmall, const uint8_t *hrow,
-                                                 uint64_t len, uint32_t *res) {
+__global__ __launch_bounds__(64) void k_spm_small(TileArgs ta, const uint16_t *scode_g, uint8_t *dsmall, SmallRow row,
+                                                 uint64_t len, uint32_t *res, uint32_t seq) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
-    __shared__ SpmWaveMem M;
+    __shared__ SpmWaveMemS M;  // (start-parallel walks: the call's latency is its dependent trie loads)
     const SmallDev sd = small_dev(dsmall);
     const int lane = w_lane();
-    small_stage_row(hrow, len, sd.row, sd.offs);
+    small_stage_row(row, len, sd.row, sd.offs);
     for (uint32_t i = lane; i < HOT_N; i += 64) {
         hot_tab[i] = sd.hot[i];
         scode[i] = scode_g[i];
@@ -91,12 +91,13 @@ __global__ __launch_bounds__(64) void k_spm_small(TileArgs ta, const uint16_t *s
     __syncthreads();
     PassClock pc;
     pc.init(false, M.passacc);
-    (void)spm_tile<3, SpmWaveMem>(ta, 0, 1, hot_tab, scode, M, nullptr, pc, true);
+    (void)spm_tile<3, SpmWaveMemS>(ta, 0, 1, hot_tab, scode, M, nullptr, pc, true);
     const bool fb = (w_bcast((uint32_t)M.ufbm, 0) & 1u) != 0u;
-    small_finish(sd, M.unext, fb, w_bcast(M.rowcnt[0], 0), res);
+    small_finish(sd, M.unext, fb, w_bcast(M.rowcnt[0], 0), res, seq);
 }
 
-int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, uint64_t len, hipStream_t st, uint32_t *status) {
+int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, const SmallRow &row, uint64_t len, hipStream_t st,
+                   uint32_t *status) {
     *status = 2;
     if (len > (uint64_t)SpmWaveMem::BC || !scode) return AK_OK;  // no tile buffer holds the row: the batch sequence
     int rc = small_call_reserve(w);
@@ -104,13 +105,12 @@ int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, uint64_t le
     TileArgs ta = small_args(w, a);
     ta.ra.spm.pool_ok = 0;
     uint32_t *res = (uint32_t *)(w->pin_small_dev + SC_RES);
+    const uint32_t seq = small_next_seq(w);
     AK_PROF(AK_PROF_SPM_TILES, false, st);
-    k_spm_small<<<1, 64, 0, st>>>(ta, scode, w->dev_small, w->pin_small_dev + 16, len, res);
+    k_spm_small<<<1, 64, 0, st>>>(ta, scode, w->dev_small, row, len, res, seq);
     AK_PROF(AK_PROF_SPM_TILES, true, st);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(st));
-    *status = ((volatile uint32_t *)(w->pin_small + SC_RES))[0];
-    return AK_OK;
+    return small_call_wait(w, st, seq, status);
 }
 
 // rows the word pool sent back (ak_tile_spm.h spm_redo_wave): the waves' epochs, the tile variant

@@ -34,13 +34,14 @@ __global__ void k_hot_build(uint32_t *hot) {
     if (i < HOT_N) hot[i] = hot_word(hot_cp(i));
 }
 
-// The row's bytes from pinned host memory into the device scratch (one PCIe round trip for the
-// whole row, every lane a 16-byte load) and its offsets [0, len] beside them: the tile front end
-// then reads device memory. Returns the device copy's base.
-__device__ __forceinline__ void small_stage_row(const uint8_t *hin, uint64_t len, uint8_t *drow, uint64_t *doffs) {
+// The row's bytes from the kernel argument (SmallRow: in the dispatch's kernarg segment, no PCIe
+// round trip) into the device scratch, every lane a 16-byte load, and its offsets [0, len] beside
+// them: the tile front end then reads device memory.
+static_assert(T_BCAP + 16 <= (int)SC_ROW_B, "a tile's row fits the kernel argument");
+__device__ __forceinline__ void small_stage_row(const SmallRow &row, uint64_t len, uint8_t *drow, uint64_t *doffs) {
     const int lane = w_lane();
     const uint64_t nblk = (len + 16 + 15) / 16;  // (+16: the zero slack the host wrote)
-    for (uint64_t b = (uint64_t)lane; b < nblk; b += 64) ((uint4 *)drow)[b] = ((const uint4 *)hin)[b];
+    for (uint64_t b = (uint64_t)lane; b < nblk && b < SC_ROW_B / 16; b += 64) ((uint4 *)drow)[b] = ((const uint4 *)row.b)[b];
     if (lane == 0) {
         doffs[0] = 0;
         doffs[1] = len;
@@ -53,7 +54,8 @@ __device__ __forceinline__ void small_stage_row(const uint8_t *hin, uint64_t len
 
 // The small call's live ids (the unit run without STAGE_DEAD) -> res + 4 in pinned host memory,
 // then res[1..3] and, last, res[0] = status (0: done, 1: the row needs the fallback kernels).
-__device__ __forceinline__ void small_finish(const SmallDev &sd, uint64_t run_len, bool fb, uint32_t cnt, uint32_t *res) {
+__device__ __forceinline__ void small_finish(const SmallDev &sd, uint64_t run_len, bool fb, uint32_t cnt, uint32_t *res,
+                                             uint32_t seq) {
     const int lane = w_lane();
 #ifndef AK_HOST_EMU
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stage and count stores have landed
@@ -69,7 +71,7 @@ __device__ __forceinline__ void small_finish(const SmallDev &sd, uint64_t run_le
             live += (uint32_t)w_popc(KM);
         }
     }
-    if (lane == 0) {  // (the host reads them after the launch completes: no ordering needed here)
+    if (lane == 0) {
         res[1] = cnt;
 #ifndef AK_HOST_EMU
         res[2] = __hip_atomic_load(sd.ctr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (set by an agent-scope store)
@@ -77,10 +79,27 @@ __device__ __forceinline__ void small_finish(const SmallDev &sd, uint64_t run_le
         res[2] = sd.ctr[2];
 #endif
         res[3] = live;
-        res[0] = fb ? 1u : 0u;
+        // the status word last, after a system-scope release: the host spins on it (small_call_wait)
+        // and reads the ids and the count once it carries this call's sequence number
+#ifndef AK_HOST_EMU
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(res, (seq << 2) | (fb ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+        res[0] = (seq << 2) | (fb ? 1u : 0u);
+#endif
     }
 }
 
+
+// the next call's sequence number: 30 bits, never 0 (the status word's initial value), and never the
+// previous call's (a status the previous kernel wrote must not pass for this call's)
+inline uint32_t small_next_seq(AkWs *w) {
+    uint32_t s;
+    do {
+        s = ++w->small_seq & 0x3FFFFFFFu;
+    } while (s == 0);
+    return s;
+}
 
 // The tile arguments of a small call: the row and its offsets in pinned host memory, the unit run
 // and counters in the device scratch.
@@ -89,7 +108,7 @@ inline TileArgs small_args(AkWs *w, const RowArgs &a0) {
     TileArgs ta;
     memset(&ta, 0, sizeof(ta));
     ta.ra = a0;
-    ta.ra.in = sd.row;  // (the kernel copies the row there from pinned memory first: small_stage_row)
+    ta.ra.in = sd.row;  // (the kernel copies the row there from its argument first: small_stage_row)
     ta.ra.offs = sd.offs;
     ta.ra.n = 1;
     ta.ra.out = sd.stage;

@@ -79,6 +79,7 @@ struct SpmWaveMem {
     static constexpr int BC = S_BCAP;        // staged bytes per tile
     static constexpr int WN = S_W;           // entries of W
     static constexpr bool PL = false;        // the tile solves its words (best / back below)
+    static constexpr bool ST = false;        // ... by word_dp_flat (SpmWaveMemS: by start-parallel walks)
     alignas(16) uint8_t bytes[S_BCAP + 32];  // staged bytes; after D2: word starts (u16)
     uint16_t v[S_E];                         // V; after pass W: nxt (u8 per W position)
     uint16_t w[S_W];                         // P (pass D1), then W
@@ -135,6 +136,7 @@ struct SpmWaveMemP {
     static constexpr int BC = SP_BCAP;
     static constexpr int WN = SP_W;
     static constexpr bool PL = true;
+    static constexpr bool ST = false;
     alignas(16) uint8_t bytes[SP_BCAP + 32];
     uint16_t v[SP_E];
     uint16_t w[SP_W];
@@ -423,6 +425,162 @@ __device__ __forceinline__ float word_dp_flat(SpmWaveMem &M, const SpmDev &m, in
     return minm;
 }
 #endif
+
+// The per-call path's tile (k_spm_small: one row, one wave, latency-bound): the lattice of every word
+// from start-parallel trie walks. word_dp_flat runs, per lane, one trie walk after another (about 3 L
+// dependent node loads for a word of L chars, the longest word setting the wave's time); here every
+// start of the tile walks at once on lanes that take the next start when done (spm_walk_starts: the
+// chain is about the longest single walk), the pieces go to an LDS pool indexed by start, and the
+// lattice runs over the pool in LDS (word_dp_starts). The same candidates in the same order (starts
+// ascending, each start's pieces by length, then its unk node if it has no single-char piece), so
+// the same float adds, decisions, margin and rebase as word_dp_flat. (Measured -40 % as the batch
+// kernel's pass V in round 3: there the lanes are full anyway and the pool costs issue slots and
+// occupancy; the per-call path has one wave and a dependent-load chain.)
+constexpr int S_POOL = 376;  // pieces a tile's starts may find (more: the tile solves its words by word_dp_flat)
+struct SpmWaveMemS : SpmWaveMem {
+    static constexpr bool ST = true;
+    uint2 pool[S_POOL];   // pieces found by the start walks {score bits, id << 8 | chars}
+    uint16_t sidx[S_W];   // per W position: first piece | count << 12 | single-char piece << 15
+};
+
+// Every start of the tile (W positions [0, wlen)) walks the trie, lanes taking the next start as soon
+// as their walk ends. A walk records up to 4 pieces (length order) and whether one is the start's
+// single char; at its end the lane appends them to the pool and indexes them by start (sidx). A walk
+// stops before the next word's "▁" (every "▁" is a forced boundary, checked at model load), at an
+// uncoded char and at a row sentinel. Returns false when a start has more than 4 pieces or the pool
+// is full (the tile then solves its words with word_dp_flat).
+__device__ __forceinline__ bool spm_walk_starts(SpmWaveMemS &M, const SpmDev &m, uint32_t wlen) {
+    const int lane = w_lane();
+    uint32_t next_item = 64, pool_n = 0;
+    uint32_t pos = (uint32_t)lane;
+    bool act = pos < wlen;
+    uint32_t v = M.w[act ? pos : 0];
+    bool walk = act && (v & W_CODED);
+    int k = (int)pos, node = 0, nb = m.root_base;
+    uint32_t c = 0;
+    bool hs = false, ovf = false;
+    uint2 q0 = make_uint2(0, 0), q1 = q0, q2 = q0, q3 = q0;
+    while (w_ballot(act)) {
+        const int t = walk ? nb + (int)(v & 0x7FFFu) : m.root_base;  // idle lanes read a node in range
+        const int4 e = m.trie[t];
+        const bool ok = walk && e.x == node;
+        const bool hv = ok && e.z >= 0 && ((e.z >> 24) & 3) != 2;
+        const int ee = k + 1;
+        const uint2 pe = make_uint2((uint32_t)e.w, ((uint32_t)(e.z & 0xFFFFFF) << 8) | (uint32_t)(ee - (int)pos));
+        q0 = hv && c == 0 ? pe : q0;
+        q1 = hv && c == 1 ? pe : q1;
+        q2 = hv && c == 2 ? pe : q2;
+        q3 = hv && c == 3 ? pe : q3;
+        ovf = ovf || (hv && c >= 4);
+        c += hv ? 1u : 0u;
+        hs = hs || (hv && k == (int)pos);
+        node = ok ? t : node;
+        nb = ok ? e.y : nb;
+        k = ok ? ee : k;
+        const uint32_t vn = M.w[k < S_W ? k : S_W - 1];
+        walk = ok && (vn & W_CODED) && vn != m.ws_code;
+        v = vn;
+        // walks that ended: their pieces to the pool, then the next start
+        const bool done = act && !walk;
+        const uint32_t cc = done ? (c < 4u ? c : 4u) : 0u;
+        uint32_t tot;
+        const uint32_t base = pool_n + w_exscan(cc, &tot);
+        const bool fits = base + cc <= (uint32_t)S_POOL;
+        ovf = ovf || (done && !fits);
+        if (done && fits) {
+            if (cc > 0) M.pool[base] = q0;
+            if (cc > 1) M.pool[base + 1] = q1;
+            if (cc > 2) M.pool[base + 2] = q2;
+            if (cc > 3) M.pool[base + 3] = q3;
+            M.sidx[pos] = (uint16_t)(base | (cc << 12) | (hs ? 0x8000u : 0u));
+        }
+        pool_n += tot;
+        const uint64_t DM = w_ballot(done);
+        const uint32_t mine = next_item + w_rank(DM);
+        next_item += (uint32_t)w_popc(DM);
+        pos = done ? mine : pos;
+        act = done ? mine < wlen : act;
+        const uint32_t vs = M.w[act ? pos : 0];
+        v = done ? vs : v;
+        walk = done ? (act && (vs & W_CODED)) : walk;
+        k = done ? (int)pos : k;
+        node = done ? 0 : node;
+        nb = done ? m.root_base : nb;
+        c = done ? 0u : c;
+        hs = hs && !done;
+    }
+    w_sync();
+    return !w_ballot(ovf);
+}
+
+// The lattice of one word (W positions [p0, p1)) from base 0 over the pieces spm_walk_starts found,
+// in word_dp_flat's order; LDS only, one piece per iteration. back[] of (p0, p1] must be BK_NONE on
+// entry. Inactive lanes pass p1 <= p0. Returns the margin (as word_dp_flat).
+__device__ __forceinline__ float word_dp_starts(SpmWaveMemS &M, const SpmDev &m, int p0, int p1) {
+    float minm = 3.0e38f;
+    bool act = p0 < p1;
+    int s = p0, reach = p0;
+    float till = 0.0f;
+    uint32_t si = M.sidx[act ? p0 : 0];
+    uint32_t i = 0;
+    const bool may_rebase = w_ballot(act && (float)(p1 - p0) * m.abs_score_max >= 0.5f * SPM_REBASE) != 0;
+    const uint32_t bk_unk = ((uint32_t)m.unk_id << 8) | 1u;
+    while (w_ballot(act)) {
+        const uint32_t cnt = (si >> 12) & 7u;
+        const bool hasp = act && i < cnt;
+        const uint2 pe = M.pool[hasp ? (si & 0xFFFu) + i : 0];
+        {
+            const int ee = s + (int)(pe.y & 0xFFu);
+            const int es = hasp ? ee : S_W;
+            const uint32_t bk = M.back[es];
+            const float bb = M.best[es];
+            const float cand = __uint_as_float(pe.x) + till;
+            const bool none = bk == BK_NONE;
+            const bool take = none || cand > bb;
+            const float gap = take ? cand - bb : bb - cand;
+            minm = hasp && !none ? fminf(minm, gap) : minm;
+            M.best[es] = take ? cand : bb;
+            M.back[es] = take ? pe.y : bk;
+            reach = hasp && ee > reach ? ee : reach;
+        }
+        const bool ends = act && i + 1 >= cnt;  // this start's last piece (or none): then its unk node
+        {
+            const bool unk = ends && !(si & 0x8000u);
+            const int es = unk ? s + 1 : S_W;
+            const uint32_t bk = M.back[es];
+            const float bb = M.best[es];
+            const float cand = m.unk_score + till;
+            const bool none = bk == BK_NONE;
+            const bool take = none || cand > bb;
+            const float gap = take ? cand - bb : bb - cand;
+            minm = unk && !none ? fminf(minm, gap) : minm;
+            M.best[es] = take ? cand : bb;
+            M.back[es] = take ? bk_unk : bk;
+            reach = unk && s + 1 > reach ? s + 1 : reach;
+        }
+        const int sn = s + 1;
+        const bool fin = ends && sn >= p1;
+        const bool next = ends && !fin;
+        const int sc = next ? sn : S_W;
+        const float tn = M.best[sc];
+        const uint32_t sin_ = M.sidx[next ? sn : 0];
+        s = next ? sn : s;
+        till = next ? tn : till;
+        si = next ? sin_ : si;
+        i = ends ? 0u : i + 1u;
+        act = act && !fin;
+        if (may_rebase) {
+            if (w_ballot(next && (till < -SPM_REBASE || till > SPM_REBASE))) {  // rare: sentencepiece's rebase
+                if (next && (till < -SPM_REBASE || till > SPM_REBASE)) {
+                    for (int q = s + 1; q <= reach; ++q)
+                        if (M.back[q] != BK_NONE) M.best[q] -= till;
+                    till = 0.0f;
+                }
+            }
+        }
+    }
+    return minm;
+}
 
 // backtrack a solved word into forward links nxt[s] = chars of the piece at s; returns its id
 // count (byte fallback: one id per UTF-8 byte of an unk char)
@@ -835,6 +993,12 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     w_sync();
     pc.mark(TP_C);
     if constexpr (!PL) {
+    bool walked = false;  // SpmWaveMemS: every start walked at once, the words solved over the pool
+    if constexpr (MemT::ST) {
+        walked = nmiss > 0 && spm_walk_starts(M, m, wlen);
+        pc.count(TC_PROBES, 1);                // (SpmWaveMemS: tiles, and those whose starts fit the pool)
+        pc.count(TC_HITS, walked ? 1 : 0);
+    }
     for (uint32_t ib = 0; ib < nmiss; ib += 64) {
         const uint32_t i = ib + (uint32_t)lane;
         const bool act = i < nmiss;
@@ -846,7 +1010,9 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
         float minm = 3.0e38f;
         word_dp<true>(M, m, p0, p1, 0.0f, minm);
 #else
-        const float minm = word_dp_flat(M, m, p0, p1);
+        float minm;
+        if constexpr (MemT::ST) minm = walked ? word_dp_starts(M, m, p0, p1) : word_dp_flat(M, m, p0, p1);
+        else minm = word_dp_flat(M, m, p0, p1);
 #endif
         if (act) {
             if (!spm_margin_ok(M, m, row, p0, p1, minm)) M.mfail[row] = 1;

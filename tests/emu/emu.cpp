@@ -433,6 +433,9 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     if (m->sdev.pool_ok && !m->sdev.wc) {  // as the launcher: the pooled variant when the pool is on
         std::vector<SpmWaveMemP> MP(g_waves);
         run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMemP>(ta, hot_tab, scode, MP[w], (uint32_t)w, (uint32_t)g_waves); });
+    } else if (getenv("AK_EMU_SPM_STARTS")) {  // the per-call path's tile (k_spm_small): start-parallel walks
+        std::vector<SpmWaveMemS> MS(g_waves);
+        run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMemS>(ta, hot_tab, scode, MS[w], (uint32_t)w, (uint32_t)g_waves); });
     } else {
         run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMem>(ta, hot_tab, scode, M[w], (uint32_t)w, (uint32_t)g_waves); });
     }

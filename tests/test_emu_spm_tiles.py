@@ -176,3 +176,36 @@ def test_fallback_rows_through_the_wave_nfc(golden, spm_model, monkeypatch):
     ids, oo, _ = emu.spm_tiles(m, buf, offs, rows=4)
     assert emu.last_nfc_rows() == 0
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+@pytest.mark.parametrize("rows", [1, 4])
+def test_start_parallel_tile_is_the_same(golden, spm_model, monkeypatch, rows):
+    """The per-call path's tile (k_spm_small's SpmWaveMemS: every start's trie walk at once into an
+    LDS piece pool, the lattice over the pool) gives the oracle's ids: the golden sample, synthetic
+    Devanagari / Hinglish / fuzz rows, a 31-char word, and scores scaled x2000 so the carried score
+    crosses the rebase bound."""
+    import copy
+    from akshar_amd import synth
+    from tests.test_emu_tiles import emu_sample
+    monkeypatch.setenv("AK_SPM_POOL", "0")
+    monkeypatch.setenv("AK_EMU_SPM_STARTS", "1")
+    em = emu.Model(spm=spm_model)
+    short = [r for r in emu_sample(golden) if r["set"] != "long"]
+    ids, oo, _ = emu.spm_tiles(em, *O.pack([r["text"] for r in short]), rows=rows)
+    assert [(r["set"], r["text"]) for r, g in zip(short, rows_ints(ids, oo)) if g != r["spm"]] == []
+    for kind in (0, 1, 2):
+        texts = synth.lines(kind, 300, seed=60 + kind)
+        texts[5] = texts[5] + " " + "क" * 30 + " end"
+        buf, offs = O.pack(texts)
+        ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=rows)
+        ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
+        assert np.array_equal(oo, ro) and np.array_equal(ids, ref), kind
+        tiles, walked = emu.last_counters()[:2]
+        assert walked > (0.8 * tiles if rows == 1 else 0), (kind, tiles, walked)
+    m = copy.copy(spm_model)
+    m.scores = (np.asarray(spm_model.scores, dtype=np.float32) * np.float32(2000.0)).astype(np.float32)
+    em = emu.Model(spm=m)
+    buf, offs = synth.generate(1, 200, seed=78)
+    ids, oo, _ = emu.spm_tiles(em, buf, offs, rows=rows)
+    ref, ro = O.OracleSPM(m).encode_batch(buf, offs)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)

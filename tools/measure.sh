@@ -5,13 +5,14 @@
 #   nccl     bench --workload cfg5 under torchrun (nccl, world 1)
 #   trace    rocprofv3 kernel trace + stats of the cfg4 bench command
 #   pmc      PMC passes over the cfg4 (10 M-row BPE) and cfg5 (25 M-row SPM) launch shapes (tools/pmc_op.sh)
+#   pmcrows  PMC passes over the cfg2 (1 M Devanagari rows, segment) and cfg3 (1 M Hinglish, fused analyze) launches
 #   fallback tools/fallback_realism.py
 #   waves    tools/wave_split.py (the fallback waves' per-pass split, fuzz / alphabet sets)
 #   tools/measure.sh TAG [STEP...]      (no steps: all of them, in this order)
 set -e
 TAG=${1:?tag}
 shift || true
-STEPS=${*:-tests smoke bench nccl trace pmc fallback waves}
+STEPS=${*:-tests smoke bench nccl trace pmc pmcrows fallback waves}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -30,6 +31,8 @@ for s in $STEPS; do
              python3 bench.py --no-cpu --no-e2e --no-others --no-single --steps 5 > $OUT/trace.log 2>&1 ;;
     pmc) bash tools/pmc_op.sh $OUT/pmc_cfg4 bpe 10000000
          bash tools/pmc_op.sh $OUT/pmc_cfg5 spm 25000000 ;;
+    pmcrows) bash tools/pmc_op.sh $OUT/pmc_cfg2 segment3 1000000 0
+             bash tools/pmc_op.sh $OUT/pmc_cfg3 analyze 1000000 1 ;;
     fallback) timeout -k 10 400 python -u tools/fallback_realism.py > $OUT/fallback_realism.json 2> $OUT/fallback_realism.err ;;
     waves) timeout -k 10 300 python -u tools/wave_split.py > $OUT/wave_split.jsonl 2> $OUT/wave_split.err ;;
     *) echo "unknown step $s"; exit 2 ;;
