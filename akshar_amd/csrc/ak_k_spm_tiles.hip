@@ -35,6 +35,10 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     __shared__ uint32_t hot_tab[HOT_N];
     __shared__ uint16_t scode[HOT_N];
     __shared__ MemT wm[SPM_TILE_BLOCK / 64];
+#if AK_SPM_ROOT_LDS
+    __shared__ int4 rt[POOLED ? SPM_RT_N : 1];  // (the pooled variant's word batches: the root step from LDS)
+    if constexpr (POOLED) spm_root_table(ta.ra.spm, rt, (int)threadIdx.x, SPM_TILE_BLOCK);
+#endif
     for (uint32_t i = threadIdx.x; i < HOT_N; i += SPM_TILE_BLOCK) {
         const uint32_t cp = hot_cp(i);
         hot_tab[i] = hot_word(cp);
@@ -43,8 +47,13 @@ __global__ __launch_bounds__(SPM_TILE_BLOCK) void k_spm_tiles(TileArgs ta) {
     }
     __syncthreads();
     const uint32_t wave = threadIdx.x >> 6;
+#if AK_SPM_ROOT_LDS
+    const int4 *rtp = POOLED ? rt : nullptr;
+#else
+    const int4 *rtp = nullptr;
+#endif
     spm_tiles_wave<FLAGS, MemT>(ta, hot_tab, scode, wm[wave], blockIdx.x * (SPM_TILE_BLOCK / 64) + wave,
-                                gridDim.x * (SPM_TILE_BLOCK / 64));
+                                gridDim.x * (SPM_TILE_BLOCK / 64), rtp);
 }
 
 // The SentencePiece kernels' LDS code table entry of hot_cp(i): W_CODED | code for chars some piece

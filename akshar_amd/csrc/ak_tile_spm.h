@@ -641,6 +641,18 @@ __device__ __forceinline__ bool spm_margin_ok(const SpmWaveMem &M, const SpmDev 
 // unit's fallback mask gets the row (the copy then takes the row from its fallback slot and skips
 // its run entries, k_unit_copy_spm) and the first such word appends it to the fallback list.
 
+#ifndef AK_SPM_ROOT_LDS
+#define AK_SPM_ROOT_LDS 0
+#endif
+constexpr int SPM_RT_N = 128;  // root children held in LDS (codes 0..127: the 24k model's 113 piece chars all fit)
+// the block's root table: rt[c] = trie[root_base + c] (a node that fails the root check past the array)
+__device__ __forceinline__ void spm_root_table(const SpmDev &m, int4 *rt, int tid, int nthreads) {
+    for (int c = tid; c < SPM_RT_N; c += nthreads) {
+        const int64_t t = (int64_t)m.root_base + c;
+        rt[c] = t >= 0 && t < (int64_t)m.n_nodes ? m.trie[t] : make_int4(-1, 0, -1, 0);
+    }
+}
+
 // Position-major batch arrays: slot (pos, lane) at pos * B + lane
 template <int B, int CAPL>
 struct SpBatch {
@@ -659,8 +671,11 @@ struct SpBatch {
 // word_dp_flat over one lane's pooled word (positions 0..L, "▁" at 0), from base 0: the same
 // candidates in the same order, first arrival wins, the same margin bookkeeping; no rebase (pool_ok:
 // a pooled word cannot reach the bound from base 0). Lanes with act false pass L = 0.
+// rt (AK_SPM_ROOT_LDS, or null): the root's children of codes < SPM_RT_N in LDS (spm_root_table): a
+// start's first trie step reads them there and only the deeper steps gather from the trie in HBM / L2.
 template <int B, int CAPL>
-__device__ __forceinline__ float word_dp_pool(const SpBatch<B, CAPL> &P, const SpmDev &m, int lane, int L) {
+__device__ __forceinline__ float word_dp_pool(const SpBatch<B, CAPL> &P, const SpmDev &m, int lane, int L,
+                                              const int4 *rt = nullptr) {
     float minm = 3.0e38f;
     bool act = L > 0;
     int s = 0, k = 0, node = 0, nb = m.root_base;
@@ -671,7 +686,15 @@ __device__ __forceinline__ float word_dp_pool(const SpBatch<B, CAPL> &P, const S
     while (w_ballot(act)) {
         const bool coded = act && (v & W_CODED);
         const int t = coded ? nb + (int)(v & 0x7FFFu) : m.root_base;  // idle lanes read a node in range
+#if AK_SPM_ROOT_LDS
+        int4 e;
+        const bool hot = rt != nullptr && coded && node == 0 && (v & 0x7FFFu) < (uint32_t)SPM_RT_N;
+        if (hot) e = rt[v & 0x7FFFu];
+        else e = m.trie[t];  // (exec-masked: the hot lanes issue no gather)
+#else
+        (void)rt;
         const int4 e = m.trie[t];
+#endif
         const bool ok = coded && e.x == node;
         const int value = e.z;
         const bool hv = ok && value >= 0 && ((value >> 24) & 3) != 2;
@@ -729,7 +752,7 @@ __device__ __forceinline__ float word_dp_pool(const SpBatch<B, CAPL> &P, const S
 // One batch of ring c: its first cnt (<= B) entries, lane l the l-th.
 template <int B, int CAPL, class MemT>
 __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint4 *pool, uint32_t c, uint32_t cnt,
-                                            PassClock &pc) {
+                                            PassClock &pc, const int4 *rt = nullptr) {
     const SpmDev &m = ta.ra.spm;
     const int lane = w_lane();
     const bool act = (uint32_t)lane < cnt;  // cnt <= B
@@ -767,7 +790,7 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint
 #pragma unroll
     for (int pos = 0; pos <= CAPL; ++pos)
         if (pos <= Lmax && lane < B) P.back[pos * B + ln] = BK_NONE;
-    const float minm = word_dp_pool<B, CAPL>(P, m, lane, L);
+    const float minm = word_dp_pool<B, CAPL>(P, m, lane, L, rt);
     // the margin test of spm_margin_ok with the word's position in its row (M = mpos x max |score|)
     const float Mb = fminf((float)mpos * m.abs_score_max, SPM_REBASE + m.abs_score_max) + 1.0f;
     const float tau = (float)(L + 3) * Mb * 2.384185791015625e-07f;  // 2^-22
@@ -822,22 +845,23 @@ __device__ __forceinline__ void spm_pool_flush(const TileArgs &ta, MemT &M, uint
 #endif
 // every ring holding a full batch (minc = 1 at the wave's end: every word), a batch at a time
 template <class MemT>
-__device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, MemT &M, uint4 *pool, bool all, PassClock &pc) {
+__device__ __forceinline__ void spm_pool_drain(const TileArgs &ta, MemT &M, uint4 *pool, bool all, PassClock &pc,
+                                               const int4 *rt = nullptr) {
 #pragma unroll 1
     for (uint32_t c = 0; c < (uint32_t)SP_NCLASS; ++c) {
         const uint32_t bw = sp_batch(c);
         for (;;) {
             const uint32_t k = w_bcast(M.pcnt[c], 0);
             if (k == 0 || (!all && k < (bw < (uint32_t)AK_SP_FLUSH_MIN ? bw : (uint32_t)AK_SP_FLUSH_MIN))) break;
-            if (c == (uint32_t)(SP_NCLASS - 1)) spm_pool_flush<32, SP_MAXL, MemT>(ta, M, pool, c, k < bw ? k : bw, pc);
-            else spm_pool_flush<64, SP_SHORT, MemT>(ta, M, pool, c, k < bw ? k : bw, pc);
+            if (c == (uint32_t)(SP_NCLASS - 1)) spm_pool_flush<32, SP_MAXL, MemT>(ta, M, pool, c, k < bw ? k : bw, pc, rt);
+            else spm_pool_flush<64, SP_SHORT, MemT>(ta, M, pool, c, k < bw ? k : bw, pc, rt);
         }
     }
 }
 
 template <int FLAGS, class MemT, bool NFCD = false>
 __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *scode,
-                        MemT &M, uint4 *pool, PassClock &pc, bool redo_mode = false) {
+                        MemT &M, uint4 *pool, PassClock &pc, bool redo_mode = false, const int4 *rt = nullptr) {
     constexpr int BCAP = MemT::BC, WN = MemT::WN;
     constexpr bool PL = MemT::PL;
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
@@ -1170,13 +1194,14 @@ __device__ int spm_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const ui
     }
     w_sync();
     pc.mark(TP_F);
-    if constexpr (PL) spm_pool_drain(ta, M, pool, false, pc);  // full batches (the tile's buffers are free now)
+    if constexpr (PL) spm_pool_drain(ta, M, pool, false, pc, rt);  // full batches (the tile's buffers are free now)
     pc.mark(TP_FBE);
     return nr;
 }
 
 template <int FLAGS, class MemT>
-__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, MemT &M, uint32_t wave_gid, uint32_t nwaves) {
+__device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint16_t *scode, MemT &M, uint32_t wave_gid, uint32_t nwaves,
+                               const int4 *rt = nullptr) {
     PassClock pc;
     pc.init(ta.passprof != nullptr, M.passacc);
     uint4 *pool = ta.pool + (uint64_t)wave_gid * SP_CAP;  // this wave's rings
@@ -1200,14 +1225,15 @@ __device__ void spm_tiles_wave(const TileArgs &ta, const uint32_t *H, const uint
         }
         w_sync();
         for (uint64_t r = r0; r < r1;)
-            r += (uint64_t)spm_tile<FLAGS, MemT>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, M, pool, pc);
+            r += (uint64_t)spm_tile<FLAGS, MemT>(ta, r, r + (uint64_t)ta.rows < r1 ? r + (uint64_t)ta.rows : r1, H, scode, M, pool, pc,
+                                                 false, rt);
         if (w_lane() == 0) {
             // OR: a pooled word of this unit may already have sent a row to the fallback kernels
             if (M.ufbm) atomicOr((unsigned long long *)(ta.unit_fb + t), (unsigned long long)M.ufbm);
             ta.unit_len[t] = (uint32_t)(M.unext - run0);
         }
     }
-    if constexpr (MemT::PL) spm_pool_drain(ta, M, pool, true, pc);  // the rest: every pooled word solved before the wave leaves
+    if constexpr (MemT::PL) spm_pool_drain(ta, M, pool, true, pc, rt);  // the rest: every pooled word solved before the wave leaves
     pc.mark(TP_FBE);
     pc.flush(ta.passprof);
 }

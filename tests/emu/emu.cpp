@@ -432,7 +432,14 @@ extern "C" int64_t emu_spm_tiles(void *model, int flags, const uint8_t *in, cons
     std::vector<SpmWaveMem> M(g_waves);
     if (m->sdev.pool_ok && !m->sdev.wc) {  // as the launcher: the pooled variant when the pool is on
         std::vector<SpmWaveMemP> MP(g_waves);
-        run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMemP>(ta, hot_tab, scode, MP[w], (uint32_t)w, (uint32_t)g_waves); });
+#if AK_SPM_ROOT_LDS
+        static int4 rt[SPM_RT_N];
+        spm_root_table(m->sdev, rt, 0, 1);
+        const int4 *rtp = rt;
+#else
+        const int4 *rtp = nullptr;
+#endif
+        run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMemP>(ta, hot_tab, scode, MP[w], (uint32_t)w, (uint32_t)g_waves, rtp); });
     } else if (getenv("AK_EMU_SPM_STARTS")) {  // the per-call path's tile (k_spm_small): start-parallel walks
         std::vector<SpmWaveMemS> MS(g_waves);
         run_waves([&](int w) { spm_tiles_wave<3, SpmWaveMemS>(ta, hot_tab, scode, MS[w], (uint32_t)w, (uint32_t)g_waves); });
