@@ -76,7 +76,10 @@ def _deps(src, seen=None):
 # with no scratch spills (with it: 20 VGPRs spilled to scratch in every tile's prologue). The SPM
 # and row-tile kernels measured faster WITH machine LICM (A/B on MI355X, tools/gpu_iter.sh AB_VARIANTS: cfg3
 # fused analyze 66.8 vs 60.9 GB/s), so only the BPE TU takes the flag.
-TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"]}
+# ak_k_spm_tiles.hip: passes D2 / N's per-char predicates as bitwise expressions (AK_D2_BITWISE,
+# ak_tile.h): -1.2 % SentencePiece kernel time, but +2.7 % for the BPE TU (A/B on MI355X,
+# profiles/r06l_ab_d2_bitwise.jsonl), so only the SPM TU takes it.
+TU_FLAGS = {"ak_k_bpe_tiles.hip": ["-mllvm", "-disable-machine-licm"], "ak_k_spm_tiles.hip": ["-DAK_D2_BITWISE=1"]}
 
 
 def build_hip(force=False, jobs=None):

@@ -277,6 +277,23 @@ __device__ __forceinline__ bool nfc_trig(uint32_t m, uint32_t p) {
     // (a starter after p never moves, and one after p's trailing mark is blocked from p's base)
     return (cm == 0 && !(m & H_SECOND)) || ((p & H_DECOMP) && (p & H_STABLE) && cm != 0u && cm < (p >> H_CCC_SHIFT));
 }
+#ifndef AK_D2_BITWISE  // the per-char predicates of passes D2 and N as bitwise & / | of comparisons
+#define AK_D2_BITWISE 0   // (no short-circuit branches, no exec-mask bookkeeping around them)
+#endif
+// nfc_trig as one expression of comparisons (the same truth table, no early returns)
+template <bool HF>
+__device__ __forceinline__ bool nfc_trig_bf(uint32_t m, uint32_t p) {
+    const bool dec = (m & H_DECOMP) != 0u;
+    const bool rs = p == H_ROWSTART;
+    const uint32_t cm = HF && (m & H_HC0) ? 0u : (m >> H_CCC_SHIFT);
+    const bool pst = HF ? (p & H_HFST) != 0u : (p & H_STABLE) != 0u;
+    const uint32_t cpv = HF && (p & H_HC0) ? 0u : (p >> H_CCC_SHIFT);
+    const bool sec = (m & H_SECOND) != 0u;
+    const bool a = (cm != 0u) & ((cm < cpv) | (sec & (cpv != 0u) & (cm > cpv)));
+    const bool b = ((cm == 0u) & !sec) |
+                   (((p & H_DECOMP) != 0u) & ((p & H_STABLE) != 0u) & (cm != 0u) & (cm < (p >> H_CCC_SHIFT)));
+    return dec | (!rs & (pst ? b : a));
+}
 // nfc_trig fires only because m, a composition second, may compose with the starter before the
 // single mark p (m is not reordered before p): the caller checks that starter (the char two back)
 __device__ __forceinline__ bool nfc_l_cand(uint32_t m, uint32_t p) {
@@ -640,10 +657,18 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             // the next lead (or the row end) must sit right after this char: else stray bytes
             const uint32_t nent = c + 1 < np ? nent0 : 0x8000u;
             const int nxt = (nent & 0x8000u) ? rend : (int)nent;
+#if AK_D2_BITWISE
+            const bool bad = chr & ((cp == 0xFFFFFFFFu) | (pos + utf8_len(cp) != nxt));
+#else
             const bool bad = chr && (cp == 0xFFFFFFFFu || pos + utf8_len(cp) != nxt);
+#endif
             const uint32_t ci = cp < HOT_LO ? cp : (cp - 0x900u < 0x100u ? cp - 0x900u + HOT_LO : 0u);
             uint32_t hw = H[ci];
+#if AK_D2_BITWISE
+            const bool cold = chr & !bad & (ci == 0u) & (cp != 0u);
+#else
             const bool cold = chr && !bad && ci == 0u && cp != 0u;
+#endif
             if (w_ballot(cold)) {
                 if (cold) hw = hot_word(cp);
             }
@@ -659,9 +684,15 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             // exact clauses (d2_exact: in-tile composition, a second after one mark, a mark moved into
             // a base + mark decomposition) decide, and the rows still unproven are marked for the
             // fallback kernels.
+#if AK_D2_BITWISE
+            const bool ok = chr & !bad & !xp;
+            const bool t0 = !NFCD && (ok & ((h & H_STABLE) == 0u) & nfc_trig_bf<false>(h, hprev));
+            const bool pc = !NFCD && (ok & (hprev != H_ROWSTART) & ((h & H_SECOND) != 0u) & ((hprev & H_FIRST) != 0u));
+#else
             const bool ok = chr && !bad && !xp;
             const bool t0 = !NFCD && ok && !(h & H_STABLE) && nfc_trig<false>(h, hprev);
             const bool pc = !NFCD && ok && nfc_pair_cand(h, hprev);
+#endif
             uint32_t cmp_hi = 0;
             if (w_ballot(bad || t0 || pc)) {
                 bool pfb = false, lok = false;
@@ -1075,8 +1106,13 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
             const uint16_t pb = in && kk >= 2 ? pb0 : V_DEAD;
             const uint16_t nx = in && kk + 1 < vlen ? nx0 : V_DEAD;
             const bool special = x >= V_SPECIAL;
+#if AK_D2_BITWISE
+            const bool drop = in & !special & (x != (uint16_t)'\n') & (x == pa) & ((pa == pb) | (nx == x));
+            const bool keep = in & !drop;
+#else
             const bool drop = in && !special && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
             const bool keep = in && !drop;
+#endif
             // hot word: LDS for U+0000..017F / U+0900..09FF, the global trie for the rest (rare)
             const uint32_t xi = x < HOT_LO ? x : ((uint32_t)x - 0x900u < 0x100u ? (uint32_t)x - 0x900u + HOT_LO : 0u);
             uint32_t h = H[xi];
@@ -1103,15 +1139,25 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
             // HF's tables compose the pair (the previous kept char is its word's map field: a char of
             // normalize_text's output maps to itself).
             const uint64_t RM = w_ballot(keep && (x == V_B || x == V_FB));
+#if AK_D2_BITWISE
+            const bool hfc = keep & !special & ((h & H_HFST) == 0u);
+            const bool trig = hfc & nfc_trig_bf<true>(h, hprev);
+            const bool hpc = hfc & (hprev != H_ROWSTART) & ((h & H_SECOND) != 0u) & ((hprev & H_FIRST) != 0u);
+#else
             const bool hfc = keep && !special && !(h & H_HFST);
             const bool trig = hfc && nfc_trig<true>(h, hprev);
             const bool hpc = hfc && nfc_pair_cand(h, hprev);
+#endif
             if (w_ballot(trig || hpc)) {
                 const uint32_t rrow = rs + w_rank_incl(RM) - 1;
                 if (trig || (hpc && compose_pair<NF_HFK>(hprev & 0xFFFFu, x))) M.fb[rrow] = 1;
             }
             // pre-tokenizer + ids
+#if AK_D2_BITWISE
+            const bool wordchar = keep & !special & (cls != HF_S);
+#else
             const bool wordchar = keep && !special && cls != HF_S;
+#endif
             const uint64_t SM = w_ballot(wordchar && cls != cprev);
             const uint32_t word = carry_word + w_rank_incl(SM);  // inclusive
             const uint32_t si = sfast_index(x);
