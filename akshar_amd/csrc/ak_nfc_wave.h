@@ -191,6 +191,11 @@ __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n,
     return w;
 }
 
+#ifndef AK_NFC_SORT  // the non-trivial segments' NFC in rounds of their own (1), or every segment in
+#define AK_NFC_SORT 1    // order, 64 per round (0)
+#endif
+
+#if !AK_NFC_SORT
 // NFC of the batch's segments, a lane each (64 per round, whatever rows they belong to): a lone char
 // that does not decompose is itself, any other segment runs the exact sequential nfc_full; its
 // UTF-8 goes to out[tout ...) (segments in order, so rows stay back to back), its byte count to its
@@ -238,6 +243,119 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
     nc = 0;
     ns = 0;
 }
+
+#else
+// NFC of the batch's segments. A lone char that does not decompose (a trivial segment, most of them)
+// is itself; any other runs the exact sequential nfc_seg on a lane. A round of 64 lanes lasts as long
+// as its slowest lane, so the non-trivial segments get rounds of their own: the batch is cut into
+// chunks holding at most 64 of them; per chunk, (1) the non-trivial segments are listed in order
+// (their indices in the spent byte buffer), (2) lane k runs the k-th one's NFC into its dec slot,
+// (3) every segment of the chunk, 64 at a time and in order, emits its UTF-8 — a trivial one its
+// char, a non-trivial one its lane's dec slot — at the exclusive scan of the byte counts, so rows stay
+// back to back in the epoch's text, and adds its bytes to its row's vbytes. A segment whose NFC passes
+// NW_DCAP code points marks its row failed (vfail). Empties the batch.
+__device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &nc, int &ns, uint8_t *out, uint32_t &tout,
+                                                uint32_t out_cap, const uint2 *fast, const uint4 *chash) {
+    const int lane = w_lane();
+    if (lane == 0) W.seg[ns] = (uint16_t)nc;
+    w_sync();
+    // the spent byte buffer: the chunk's non-trivial segment indices and their NFC lengths
+    uint16_t *ntl = (uint16_t *)W.bytes;
+    int8_t *ntw = (int8_t *)(W.bytes + 128);
+    static_assert(NW_DCAP <= 127 && sizeof(W.bytes) >= 192, "ntl / ntw fit the byte buffer");
+    // classify every segment: row tag | non-trivial << 7 (rows of a failed row count as trivial: no text)
+    for (int base = 0; base < ns; base += 64) {
+        const int j = base + lane;
+        if (j < ns) {
+            const int s0 = (int)W.seg[j], e0 = (int)W.seg[j + 1];
+            const uint32_t r = W.segrow[j] & 0x7Fu;
+            const uint32_t c0 = W.cps[s0];
+            const bool trivial = R.vfail[r] || (e0 - s0 == 1 && !p_decomp(prop(fast, c0)) && c0 - H_SBASE >= H_SCOUNT);
+            W.segrow[j] = (uint8_t)(r | (trivial ? 0u : 0x80u));
+        }
+    }
+    w_sync();
+    uint32_t *mydec = W.dec + lane * NW_DCAP;
+    for (int c0 = 0; c0 < ns;) {
+        // (1) the chunk: up to the 64th non-trivial segment
+        int nt = 0, c1 = ns;
+        for (int base = c0; base < ns; base += 64) {
+            const int j = base + lane;
+            const bool ntv = j < ns && (W.segrow[j] & 0x80u);
+            const uint64_t M = w_ballot(ntv);
+            const int k = nt + (int)w_rank(M);
+            if (ntv && k < 64) ntl[k] = (uint16_t)j;
+            const int add = w_popc(M);
+            if (nt + add > 64) {  // the 65th non-trivial segment opens the next chunk
+                uint64_t mm = M;
+                for (int q = 0; q < 64 - nt; ++q) mm &= mm - 1;  // drop the ones this chunk takes
+                c1 = base + __builtin_ctzll(mm);
+                nt = 64;
+                break;
+            }
+            nt += add;
+        }
+        w_sync();
+        // (2) lane k: the k-th non-trivial segment's NFC into its dec slot
+        {
+            int w = 0;
+            if (lane < nt) {
+                const int j = (int)ntl[lane];
+                const int s0 = (int)W.seg[j], e0 = (int)W.seg[j + 1];
+                w = nfc_seg(W.cps + s0, mydec, e0 - s0, fast, chash);
+                ntw[lane] = (int8_t)(w < 0 ? -1 : w);
+            }
+        }
+        w_sync();
+        // (3) the chunk's segments in order, 64 at a time
+        int kseen = 0;
+        for (int base = c0; base < c1; base += 64) {
+            const int j = base + lane;
+            const bool act = j < c1;
+            const uint32_t sr = act ? W.segrow[j] : 0u;
+            const bool ntv = (sr & 0x80u) != 0u;
+            const uint64_t M = w_ballot(ntv);
+            const int slot = kseen + (int)w_rank(M);
+            kseen += w_popc(M);
+            const uint32_t r = sr & 0x7Fu;
+            const bool live = act && !R.vfail[r];  // (a row found invalid while decoding has no text)
+            int w = 0;
+            const uint32_t *src = nullptr;
+            uint32_t one = 0;
+            if (live) {
+                if (ntv) {
+                    w = (int)ntw[slot];
+                    src = W.dec + slot * NW_DCAP;
+                } else {
+                    one = W.cps[W.seg[j]];
+                    w = 1;
+                }
+            }
+            uint32_t nb = 0;
+            for (int k = 0; k < w; ++k) nb += (uint32_t)utf8_len(src ? src[k] : one);
+            uint32_t t;
+            const uint32_t at = tout + w_exscan(nb, &t);
+            if (live && w >= 0) {
+                uint32_t o = at;
+                for (int k = 0; k < w; ++k) {
+                    uint32_t by[4];
+                    const uint32_t cl = utf8_bytes_of(src ? src[k] : one, by);
+                    for (uint32_t q = 0; q < cl; ++q)
+                        if (o + q < out_cap) out[o + q] = (uint8_t)by[q];  // (never short: the caller reserves 3 bytes per byte)
+                    o += cl;
+                }
+                if (nb) atomicAdd(&R.vbytes[r], nb);
+            }
+            if (live && w < 0) R.vfail[r] = 1;  // (it writes nothing: its row goes on, the text stays intact)
+            tout += t;
+            w_sync();
+        }
+        c0 = c1;
+    }
+    nc = 0;
+    ns = 0;
+}
+#endif
 
 // The fallback kernels' waves (k_bpe_nfc, k_spm_nfc) take the tile kernel's fallback rows
 // i = wave_gid, + nwaves, ... of ta.fb_list in epochs: each row NFC-normalized by the wave
