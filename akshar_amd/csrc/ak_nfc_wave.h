@@ -14,7 +14,8 @@
 //            the row is the concatenation of NFC of its segments
 //   NFC      lane per segment, the segments of several rows together: a lone char that does not
 //            decompose is itself; any other segment runs the exact sequential algorithm (ak_dev.h
-//            nfc_full: full canonical decomposition, stable ccc sort, canonical composition)
+//            nfc_full: full canonical decomposition, stable ccc sort, canonical composition), the
+//            non-trivial segments listed and run 64 at a time ahead of the in-order output
 //   encode   UTF-8 byte counts per lane, a scan, and each lane writes its bytes
 // Rows over NW_MAXB bytes, a segment whose NFC passes NW_DCAP code points, or invalid UTF-8 go on
 // to the one-lane path.
