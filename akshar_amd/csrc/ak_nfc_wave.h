@@ -123,9 +123,13 @@ __device__ __forceinline__ uint32_t compose_hashed(const uint4 *ch, uint32_t a, 
 // only when the starter is a composition first and the char a second, unblocked — the pairs the
 // table holds (tools/gen_tables.py: comp_first / comp_second, Hangul L, LV, V, T). Inlined, so its
 // LDS accesses stay LDS accesses. Returns the length, or -1 past NW_DCAP.
+// HF: the same with HF's ccc (ak_dev.h nfc_full<NF_HF>: HF's NFKC over the normalize_text alphabet).
+template <bool HF = false>
 __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n, const uint2 *fast, const uint4 *chash) {
     constexpr uint32_t CP = 0x1FFFFFu, SECOND = 1u << 22;
-    auto ent = [&](uint32_t cp, uint2 pr) { return cp | (p_second(pr) ? SECOND : 0u) | ((uint32_t)p_ccc(pr) << 24); };
+    auto ent = [&](uint32_t cp, uint2 pr) {
+        return cp | (p_second(pr) ? SECOND : 0u) | ((uint32_t)(HF ? p_ccc_hf(pr) : p_ccc(pr)) << 24);
+    };
     int m = 0;
     for (int i = 0; i < n; ++i) {
         const uint32_t cp = in[i];
@@ -202,6 +206,7 @@ __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n,
 // UTF-8 goes to out[tout ...) (segments in order, so rows stay back to back), its byte count to its
 // row's vbytes. A segment whose NFC passes NW_DCAP code points marks its row failed (vfail). Empties
 // the batch.
+template <bool HF = false>
 __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &nc, int &ns, uint8_t *out, uint32_t &tout,
                                                 uint32_t out_cap, const uint2 *fast, const uint4 *chash) {
     const int lane = w_lane();
@@ -219,7 +224,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
                 dec[0] = c0;
                 w = 1;
             } else {
-                w = nfc_seg(W.cps + s, dec, e - s, fast, chash);
+                w = nfc_seg<HF>(W.cps + s, dec, e - s, fast, chash);
             }
         }
         uint32_t nb = 0;
@@ -255,6 +260,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
 // char, a non-trivial one its lane's dec slot — at the exclusive scan of the byte counts, so rows stay
 // back to back in the epoch's text, and adds its bytes to its row's vbytes. A segment whose NFC passes
 // NW_DCAP code points marks its row failed (vfail). Empties the batch.
+template <bool HF = false>
 __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &nc, int &ns, uint8_t *out, uint32_t &tout,
                                                 uint32_t out_cap, const uint2 *fast, const uint4 *chash) {
     const int lane = w_lane();
@@ -303,7 +309,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
             if (lane < nt) {
                 const int j = (int)ntl[lane];
                 const int s0 = (int)W.seg[j], e0 = (int)W.seg[j + 1];
-                w = nfc_seg(W.cps + s0, mydec, e0 - s0, fast, chash);
+                w = nfc_seg<HF>(W.cps + s0, mydec, e0 - s0, fast, chash);
                 ntw[lane] = (int8_t)(w < 0 ? -1 : w);
             }
         }
@@ -375,7 +381,7 @@ constexpr uint64_t NE_TEXT_B = NE_TCAP + 64;              // + slack: the tile's
 constexpr uint64_t NE_OFFS_B = ((NE_VMAX + 1) * 8 + 15) / 16 * 16;
 constexpr uint64_t NE_CNT_B = NE_VMAX * 4, NE_FB_B = NE_VMAX * 4 + 16;
 constexpr uint64_t NE_REG_B = (NE_RCAP + 64) * 4;         // + slack: pool_flush's 16-entry windows
-constexpr uint64_t NE_BYTES = (NE_TEXT_B + NE_OFFS_B + NE_CNT_B + NE_FB_B + NE_REG_B + 255) / 256 * 256;  // per wave
+constexpr uint64_t NE_BYTES = (2 * (NE_TEXT_B + NE_OFFS_B) + NE_CNT_B + NE_FB_B + NE_REG_B + 255) / 256 * 256;  // per wave
 
 struct NfcEpoch {
     uint8_t *text;     // NE_TCAP (+ slack)
@@ -384,6 +390,8 @@ struct NfcEpoch {
     uint32_t *vfb;     // the tile's own fallback list (unused: its M.fb says the same), NE_VMAX
     uint32_t *vfbc;    // ... and length
     uint32_t *region;  // NE_RCAP (+ slack)
+    uint8_t *htext;    // BPE: the HF NFKC text of the epoch's rows HF's NFKC changes (hf_epoch_gather)
+    uint64_t *hoffs;   // ... its offsets
 };
 
 __device__ __forceinline__ NfcEpoch nfc_epoch(uint8_t *ebuf, uint32_t wave_gid) {
@@ -395,6 +403,8 @@ __device__ __forceinline__ NfcEpoch nfc_epoch(uint8_t *ebuf, uint32_t wave_gid) 
     E.vfb = (uint32_t *)(b + NE_TEXT_B + NE_OFFS_B + NE_CNT_B);
     E.vfbc = E.vfb + NE_VMAX;
     E.region = (uint32_t *)(b + NE_TEXT_B + NE_OFFS_B + NE_CNT_B + NE_FB_B);
+    E.htext = b + NE_TEXT_B + NE_OFFS_B + NE_CNT_B + NE_FB_B + NE_REG_B;
+    E.hoffs = (uint64_t *)(E.htext + NE_TEXT_B);
     return E;
 }
 
@@ -574,6 +584,162 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
 }
 static_assert(3 * NW_MAXB + 16 < NE_TCAP, "an empty epoch takes any row the wave normalizes");
 
+// The HF rows a round did not take, R.vrow / vstart / vlen [from, from + n), down to [0, n) for the next
+// round (n <= NE_VMAX: every lane reads its two entries before any is written).
+__device__ __forceinline__ void hf_rest_down(NfcRows &R, uint32_t from, uint32_t n) {
+    const uint32_t k0 = (uint32_t)w_lane(), k1 = k0 + 64u;
+    const bool a0 = k0 < n, a1 = k1 < n;
+    const uint32_t r0 = a0 ? R.vrow[from + k0] : 0u, s0 = a0 ? R.vstart[from + k0] : 0u, l0 = a0 ? R.vlen[from + k0] : 0u;
+    const uint32_t r1 = a1 ? R.vrow[from + k1] : 0u, s1 = a1 ? R.vstart[from + k1] : 0u, l1 = a1 ? R.vlen[from + k1] : 0u;
+    w_sync();
+    if (a0) { R.vrow[k0] = r0; R.vstart[k0] = s0; R.vlen[k0] = l0; }
+    if (a1) { R.vrow[k1] = r1; R.vstart[k1] = s1; R.vlen[k1] = l1; }
+    w_sync();
+}
+static_assert(NE_VMAX <= 128, "hf_rest_down: two entries per lane");
+
+// BPE: the rows of an epoch the tile sent on because HF's NFKC changes their normalize_text output
+// (pass N's HF-NFC check; nfc_epoch_finish kept them: R.vrow / vstart / vlen [0, nh), their NFC text
+// in E.text). Their text as the reference's HF tokenizer sees it, by the wave, into E.htext as
+// virtual rows 0..v-1 (E.hoffs), for the tile to encode with normalize_text and the HF check off
+// (bpe_tile<.., RAW>): per batch of rows (<= NW_MAXB bytes, as nfc_epoch_gather) the bytes are
+// copied and decoded, then
+//   map        normalize_text's per-char map (semantic_normalize + filter_garbage: p_normmap, 0 =
+//              dropped), compacted in place
+//   elongation remove_elongations over the mapped chars: x dropped when x == prev, x != '\n' and
+//              (prev == prev2 or next == x) (runs >= 3 -> 1), the row tag in the comparison so runs
+//              never cross rows; then HF's compat spaces -> ' ' (ak_dev.h BpeSink<false>::push)
+//   HF NFC     segments at a row's first char and every HF-stable char (HF ccc 0, not a composition
+//              second), each segment's NFC with HF's ccc (nfc_flush_batch<true>: ak_dev.h
+//              nfc_full<NF_HF>), UTF-8 into E.htext
+// Takes the longest prefix of the rows that fits the text reserve (at least one row: any row fits an
+// empty one); returns its length v. A row with a segment over NW_DCAP is marked failed (vfail).
+__device__ __forceinline__ uint32_t hf_epoch_gather(const TileArgs &ta, const NfcEpoch &E, NfcWaveMem &S, NfcRows &R,
+                                                    uint32_t nh, const uint2 *fast) {
+    const int lane = w_lane();
+    uint32_t v = 0, tout = 0, reserve = 0;
+    if (lane == 0) atomicExch(E.vfbc, 0u);  // (the tile's own list: at most one entry per row of the round)
+    while (v < nh) {
+        const uint32_t j = v + (uint32_t)lane;
+        const bool valid = j < nh;
+        const uint32_t a = valid ? R.vlen[j] : 0u;
+        const uint32_t o0 = valid ? R.vstart[j] : 0u;
+        uint32_t tt;
+        const uint32_t B = w_exscan(a, &tt) + a;  // inclusive
+        const bool ok = valid && B <= (uint32_t)NW_MAXB && reserve + 3 * B + 16 <= NE_TCAP;
+        const uint64_t OK = w_ballot(ok);
+        const uint32_t kstop = ~OK ? (uint32_t)__builtin_ctzll(~OK) : 64u;
+        if (kstop == 0) break;  // the reserve is full: the rest wait for the next round
+        const bool take = (uint32_t)lane < kstop;
+        const uint32_t start = B - a;
+        const uint32_t key = take ? start : 0xFFFFFFFFu;
+        const uint32_t blen = w_bcast(B, (int)kstop - 1);
+        w_sync();  // (every lane has read its row's vstart / vlen)
+        if (take) {
+            R.vbytes[j] = 0;
+            R.vfail[j] = 0;
+        }
+        for (uint32_t base = 0; base < blen + 8; base += 64) {
+            const uint32_t p = base + (uint32_t)lane;
+            const int k = w_last_le(key, p < blen ? p : 0u);
+            const uint32_t src = w_shfl(o0, k) + (p - w_shfl(start, k));
+            if (p < blen) S.bytes[p] = E.text[src];  // (this wave's own stores: same-CU L1)
+            else if (p < (uint32_t)NW_MAXB + 32) S.bytes[p] = 0;
+        }
+        w_sync();
+        // decode: chars tagged with their virtual row (bits 24-30); the text is the wave's own UTF-8
+        int nc = 0;
+        for (uint32_t base = 0; base < blen; base += 64) {
+            const uint32_t p = base + (uint32_t)lane;
+            const bool inb = p < blen;
+            const uint32_t b = inb ? S.bytes[p] : 0u;
+            const bool lead = inb && (b & 0xC0u) != 0x80u;
+            const uint32_t cp = lead ? decode_word(lds_word(S.bytes, p), (int)p, (int)blen) : 0u;
+            const int k = w_last_le(key, inb ? p : 0u);
+            const uint32_t rv = w_shfl(j, k);
+            if (lead && cp == 0xFFFFFFFFu) R.vfail[rv] = 1;
+            const uint64_t LMk = w_ballot(lead);
+            if (lead) S.cps[nc + (int)w_rank(LMk)] = (cp == 0xFFFFFFFFu ? 0xFFFDu : cp) | (rv << 24);
+            nc += w_popc(LMk);
+        }
+        w_sync();
+        // normalize_text's map, compacted in place (a step's writes land below its reads)
+        int nm = 0;
+        for (int base = 0; base < nc; base += 64) {
+            const int ci = base + lane;
+            const uint32_t x = ci < nc ? S.cps[ci] : 0u;
+            const uint32_t mp = ci < nc ? p_normmap(prop(fast, x & 0xFFFFFFu)) : 0u;
+            const uint64_t KM = w_ballot(mp != 0u);
+            if (mp) S.cps[nm + (int)w_rank(KM)] = mp | (x & 0x7F000000u);
+            nm += w_popc(KM);
+        }
+        w_sync();
+        // remove_elongations, then compat spaces -> ' ' (prev / prev2 of lanes 0 and 1 carried: the
+        // step before may have compacted over them)
+        int ne = 0;
+        uint32_t c1 = 0xFFFFFFFFu, c2 = 0xFFFFFFFFu;
+        for (int base = 0; base < nm; base += 64) {
+            const int ci = base + lane;
+            const bool in = ci < nm;
+            const uint32_t x = in ? S.cps[ci] : 0xFFFFFFFEu;
+            const uint32_t nx = ci + 1 < nm ? S.cps[ci + 1] : 0xFFFFFFFFu;
+            const uint32_t pa = w_prev(x, c1), pb = w_prev(pa, c2);
+            c2 = w_bcast(x, 62);
+            c1 = w_bcast(x, 63);
+            const uint32_t cp = x & 0xFFFFFFu;
+            const bool drop = in && x == pa && cp != (uint32_t)'\n' && (pa == pb || nx == x);
+            const bool keep = in && !drop;
+            const uint32_t y = keep && p_hfspace(prop(fast, cp)) ? 0x20u : cp;
+            const uint64_t KM = w_ballot(keep);
+            w_sync();  // (every lane has read its neighbours)
+            if (keep) S.cps[ne + (int)w_rank(KM)] = y | (x & 0x7F000000u);
+            ne += w_popc(KM);
+        }
+        w_sync();
+        // segments: a row's first char and every HF-stable char
+        int ns = 0;
+        uint32_t carry_tag = 0xFFFFFFFFu;
+        for (int base = 0; base < ne; base += 64) {
+            const int ci = base + lane;
+            const bool in = ci < ne;
+            const uint32_t x = in ? S.cps[ci] : 0u;
+            const uint32_t cp = x & 0xFFFFFFu;
+            const uint32_t tag = (x >> 24) & 0x7Fu;
+            const bool first = tag != w_prev(tag, carry_tag);
+            carry_tag = w_bcast(tag, 63);
+            const uint2 pr = prop(fast, cp);
+            const bool st = in && (first || (p_ccc_hf(pr) == 0 && !p_second(pr)));
+            const uint64_t SM = w_ballot(st);
+            if (st) {
+                S.seg[ns + (int)w_rank(SM)] = (uint16_t)ci;
+                S.segrow[ns + (int)w_rank(SM)] = (uint8_t)tag;
+            }
+            if (in) S.cps[ci] = cp;
+            ns += w_popc(SM);
+        }
+        w_sync();
+        nfc_flush_batch<true>(S, R, ne, ns, E.htext, tout, NE_TCAP, fast, ta.comp_hash);
+        v += kstop;
+        reserve += 3 * blen;
+    }
+    // offsets: the scan of the rows' bytes
+    uint32_t pos = 0;
+    for (uint32_t b = 0; b < v; b += 64) {
+        const uint32_t k = b + (uint32_t)lane;
+        const uint32_t nb = k < v ? R.vbytes[k] : 0u;
+        uint32_t t;
+        const uint32_t at = pos + w_exscan(nb, &t);
+        if (k < v) E.hoffs[k] = at;
+        pos += t;
+    }
+    if (lane == 0) E.hoffs[v] = pos;
+#ifndef AK_HOST_EMU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the text and offsets have landed (the tile reads them)
+#endif
+    w_sync();
+    return v;
+}
+
 // The same epoch for rows that need no NFC (SentencePiece's send-backs, k_spm_redo): list[i], +
 // nwaves, ... copied back to back (a row over NW_MAXB bytes, which no tile buffer holds, goes
 // straight to fbl).
@@ -609,38 +775,57 @@ __device__ __forceinline__ uint32_t copy_epoch_gather(const TileArgs &ta, const 
 }
 
 // Virtual rows [r, r + took) of one tile: their runs in the region (lane l: row r + l; sb: the tile's
-// first position; first: the row's run from there, n: its length; fb: the tile sent the row on).
-__device__ __forceinline__ void nfc_epoch_runs(NfcRows &R, uint32_t r, int took, uint64_t sb, bool fb, uint32_t first,
+// first position; first: the row's run from there, n: its length; fb: the tile's M.fb of the row:
+// 0 = encoded, 2 = sent on for HF's NFKC alone (BPE pass N), else sent on for another reason).
+constexpr uint32_t VL_FB = 0xFFFFFFFFu, VL_HF = 0xFFFFFFFEu;  // vlen of a row the tile sent on
+__device__ __forceinline__ void nfc_epoch_runs(NfcRows &R, uint32_t r, int took, uint64_t sb, uint32_t fb, uint32_t first,
                                                uint32_t n) {
     const int lane = w_lane();
     if (lane < took) {
         R.vstart[r + lane] = (uint32_t)sb + (fb ? 0u : first);
-        R.vlen[r + lane] = fb ? 0xFFFFFFFFu : n;
+        R.vlen[r + lane] = fb == 0u ? n : (fb == 2u ? VL_HF : VL_FB);
     }
     w_sync();
 }
 
 // Each encoded virtual row's ids (its run without STAGE_DEAD entries) -> its fallback slot and count,
 // if they fit the slot; else -> fb3. BPE: slot = offs[r] + 2 r, len + 2 entries (mul 1); SentencePiece
-// 2 offs[r] + 2 r, 2 len + 2 (mul 2).
-__device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEpoch &E, NfcRows &R, uint32_t v,
-                                                 uint32_t mul, uint32_t *fb3, uint32_t *fb3_count, uint32_t *also = nullptr) {
+// 2 offs[r] + 2 r, 2 len + 2 (mul 2). With hf, a row the tile sent on for HF's NFKC alone is kept
+// for hf_epoch_gather instead: R.vrow / vstart / vlen [0, nh) = the row, its text in E.text (offset,
+// bytes); returns nh.
+__device__ __forceinline__ uint32_t nfc_epoch_finish(const TileArgs &ta, const NfcEpoch &E, NfcRows &R, uint32_t v,
+                                                     uint32_t mul, uint32_t *fb3, uint32_t *fb3_count,
+                                                     uint32_t *also = nullptr, bool hf = false) {
     const int lane = w_lane();
 #ifndef AK_HOST_EMU
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the region's ids, merges and counts have landed
 #endif
     uint32_t *stage = (uint32_t *)ta.ra.out;
+    uint32_t nh = 0;
     for (uint32_t j = 0; j < v; ++j) {
         const uint64_t r = R.vrow[j];
         const uint32_t rl = R.vlen[j];
+        const bool sent = rl >= VL_HF;
+        if (hf && rl == VL_HF && !R.vfail[j]) {  // (nh <= j: entries already read)
+            const uint64_t t0 = E.voffs[j], t1 = E.voffs[j + 1];
+            w_sync();
+            if (lane == 0) {
+                R.vrow[nh] = (uint32_t)r;
+                R.vstart[nh] = (uint32_t)t0;
+                R.vlen[nh] = (uint32_t)(t1 - t0);
+            }
+            w_sync();
+            ++nh;
+            continue;
+        }
         const uint64_t o0 = ta.ra.offs[r], len = ta.ra.offs[r + 1] - o0;
         // (an agent-scope load: pool_flush's atomicSub on the count ran at L2, past this CU's L1)
 #ifdef AK_HOST_EMU
-        const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : E.vcnt[j];
+        const uint32_t cnt = sent ? 0u : E.vcnt[j];
 #else
-        const uint32_t cnt = rl == 0xFFFFFFFFu ? 0u : __hip_atomic_load(E.vcnt + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t cnt = sent ? 0u : __hip_atomic_load(E.vcnt + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
-        if (rl == 0xFFFFFFFFu || R.vfail[j] || (uint64_t)cnt > mul * len + 2) {
+        if (sent || R.vfail[j] || (uint64_t)cnt > mul * len + 2) {
             nfc_fb3(fb3, fb3_count, r, also);
             continue;
         }
@@ -660,10 +845,16 @@ __device__ __forceinline__ void nfc_epoch_finish(const TileArgs &ta, const NfcEp
             if (ta.ra.row_status) ta.ra.row_status[r] = 0;
         }
     }
+    w_sync();
+    return nh;
 }
 
+#ifndef AK_NO_HF_WAVE
+#define AK_NO_HF_WAVE 0  // 1: rows HF's NFKC changes go on to the one-lane kernel (as before round 6)
+#endif
 // The kernel k_bpe_nfc's wave (ak_k_bpe_tiles.hip): epochs as above; the merge pool drained at each
-// epoch's end (its entries point into the region).
+// epoch's end (its entries point into the region); then the epoch's rows HF's NFKC changes
+// (hf_epoch_gather) through the tile once more, normalize_text off (bpe_tile<.., RAW>).
 template <int FLAGS>
 __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count, const uint32_t *H,
                              const uint16_t *sfast, const uint2 *fast, NfcWaveLds<TileWaveMem> &L, uint32_t wave_gid,
@@ -674,37 +865,60 @@ __device__ void bpe_nfc_wave(const TileArgs &ta, uint8_t *ebuf, uint32_t *fb3, u
     const bool prof = !AK_NFC_SPLIT && ta.passprof != nullptr;  // (level 2: the NFC and the slot copies count as "loop")
     uint4 *pool = ta.pool + (uint64_t)wave_gid * POOL_U4;
     const NfcEpoch E = nfc_epoch(ebuf, wave_gid);
-    const TileArgs tl = nfc_epoch_args(ta, E);
+    TileArgs tl = nfc_epoch_args(ta, E);
     for (uint32_t i = wave_gid; i < nl;) {
         const uint64_t g0 = prof ? clock64() : 0;
-        const uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, L.n, L.rows, fast, fb3, fb3_count);
+        uint32_t v = nfc_epoch_gather(ta, i, nl, nwaves, E, L.n, L.rows, fast, fb3, fb3_count);
         if (v == 0) continue;
-        // the tile's buffers over the NFC scratch: its lasting fields set again (the pool is empty)
         PassClock pc;
         pc.init(prof, M.passacc);
-        if (lane < POOL_NCLASS) {
-            M.phead[lane] = 0;
-            M.pcnt[lane] = 0;
+        if (lane == 0 && prof) M.passacc[TP_LOOP] = pc.last - g0;
+        // round 0: the epoch's NFC text; rounds 1, 2, ...: the HF text of its rows HF's NFKC changes
+        // (the same tile code, normalize_text and the HF check off)
+        bool raw = false;
+        uint32_t nh_left = 0;
+        for (;;) {
+            tl.ra.in = raw ? E.htext : E.text;
+            tl.ra.offs = raw ? E.hoffs : E.voffs;
+            // the tile's buffers over the NFC scratch: its lasting fields set again (the pool is empty)
+            if (lane < POOL_NCLASS) {
+                M.phead[lane] = 0;
+                M.pcnt[lane] = 0;
+            }
+            if (lane == 0) {
+                M.unext = 0;
+                M.ufbm = 0;
+            }
+            w_sync();
+            for (uint32_t r = 0; r < v;) {
+                const uint64_t sb = M.unext;
+                const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
+                const int took = bpe_tile<FLAGS, true>(tl, r, re, H, sfast, M, pool, pc, raw);
+                const bool in = lane < took;
+                nfc_epoch_runs(L.rows, r, took, sb, in ? (uint32_t)M.fb[lane] : 0u, in ? M.rowop[lane] : 0u,
+                               in ? M.rowop[lane + 1] - M.rowop[lane] : 0u);
+                r += (uint32_t)took;
+            }
+            pool_drain(tl, M, pool, 1u, pc);  // every miss of the round merged
+            pc.mark(TP_FBE);
+            const uint32_t nh = nfc_epoch_finish(ta, E, L.rows, v, 1u, fb3, fb3_count, nullptr, !raw && !AK_NO_HF_WAVE);
+            pc.mark(TP_LOOP);
+            if (!raw) {
+                nh_left = nh;
+            } else {
+                nh_left -= v;
+                if (nh_left) hf_rest_down(L.rows, v, nh_left);
+            }
+            if (nh_left == 0) break;
+            pc.flush(ta.passprof);  // (the gather's scratch overlays the accumulators)
+            v = hf_epoch_gather(ta, E, L.n, L.rows, nh_left, fast);
+            pc.init(prof, M.passacc);
+            if (v == 0) {  // (cannot happen: a row over NW_MAXB bytes never reaches the tile) the one-lane kernel
+                for (uint32_t j = 0; j < nh_left; ++j) nfc_fb3(fb3, fb3_count, L.rows.vrow[j]);
+                break;
+            }
+            raw = true;
         }
-        if (lane == 0) {
-            M.unext = 0;
-            M.ufbm = 0;
-            if (prof) M.passacc[TP_LOOP] = pc.last - g0;
-        }
-        w_sync();
-        for (uint32_t r = 0; r < v;) {
-            const uint64_t sb = M.unext;
-            const uint32_t re = r + (uint32_t)tl.rows < v ? r + (uint32_t)tl.rows : v;
-            const int took = bpe_tile<FLAGS, true>(tl, r, re, H, sfast, M, pool, pc);
-            const bool in = lane < took;
-            nfc_epoch_runs(L.rows, r, took, sb, in && M.fb[lane], in ? M.rowop[lane] : 0u,
-                           in ? M.rowop[lane + 1] - M.rowop[lane] : 0u);
-            r += (uint32_t)took;
-        }
-        pool_drain(tl, M, pool, 1u, pc);  // every miss of the epoch merged
-        pc.mark(TP_FBE);
-        nfc_epoch_finish(ta, E, L.rows, v, 1u, fb3, fb3_count);
-        pc.mark(TP_LOOP);
         pc.flush(ta.passprof);
     }
 }

@@ -572,8 +572,13 @@ __device__ AK_D2_INLINE D2Exact d2_exact(MemT &M, const uint16_t *P, const uint3
 // A row whose NFC quick check trips or that holds invalid UTF-8 is marked in M.fb (the caller sends
 // it to the fallback kernels).
 // NFCD: the rows are NFC already (k_bpe_nfc normalized them): only invalid UTF-8 is checked in D2.
+// raw (with NFCD; a wave-uniform value, so the fallback wave inlines one copy of the tile for both
+// its texts): the rows are HF NFKC text already (hf_epoch_gather): V holds the chars themselves (no
+// normalize_text map, no nukta expansion); a char past U+FFFB is invalid here.
 template <int BCAP, class Mem, bool NFCD = false>
-__device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, uint64_t rend, const uint32_t *H, Mem &M) {
+__device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, uint64_t rend, const uint32_t *H, Mem &M,
+                                               bool raw = false) {
+    const bool RAW = NFCD && raw;
     const int lane = w_lane();
     const int nr0 = (int)(rend - r0);
     const uint64_t myoff = lane <= nr0 ? a.offs[r0 + lane] : 0ull;
@@ -658,9 +663,9 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             const uint32_t nent = c + 1 < np ? nent0 : 0x8000u;
             const int nxt = (nent & 0x8000u) ? rend : (int)nent;
 #if AK_D2_BITWISE
-            const bool bad = chr & ((cp == 0xFFFFFFFFu) | (pos + utf8_len(cp) != nxt));
+            const bool bad = chr & ((cp == 0xFFFFFFFFu) | (pos + utf8_len(cp) != nxt) | (RAW & (cp >= V_SPECIAL)));
 #else
-            const bool bad = chr && (cp == 0xFFFFFFFFu || pos + utf8_len(cp) != nxt);
+            const bool bad = chr && (cp == 0xFFFFFFFFu || pos + utf8_len(cp) != nxt || (RAW && cp >= V_SPECIAL));
 #endif
             const uint32_t ci = cp < HOT_LO ? cp : (cp - 0x900u < 0x100u ? cp - 0x900u + HOT_LO : 0u);
             uint32_t hw = H[ci];
@@ -675,10 +680,10 @@ __device__ __forceinline__ TileRows tile_front(const RowArgs &a, uint64_t r0, ui
             const uint32_t h = chr ? (bad ? 0u : hw) : H_ROWSTART;
             // a precomposed nukta letter (H_EXP) is base + nukta: the next char is checked against the
             // nukta, and the letter itself never needs the full NFC (see hot_word)
-            const bool xp = chr && (h & H_EXP);
+            const bool xp = !RAW && chr && (h & H_EXP);
             uint32_t hp = xp ? ((h & 0xFFFFu) < 0x0980u ? hn_deva : hn_beng) : h;
             uint32_t hprev = w_prev(hp, carry_h);  // DPP wave_shr:1, lane 0 takes the carry
-            uint32_t mv = chr ? (h & 0xFFFFu) : 0u;
+            uint32_t mv = RAW ? (chr && !bad ? cp : 0u) : (chr ? (h & 0xFFFFu) : 0u);
             // NFC proof (rare work behind ONE ballot): nfc_trig on the non-stable chars, and the pair
             // candidates (a second right after a first). Where either holds, or the char is bad, the
             // exact clauses (d2_exact: in-tile composition, a second after one mark, a mark moved into
@@ -1062,13 +1067,14 @@ __device__ __forceinline__ void pool_drain(const TileArgs &ta, TileWaveMem &M, u
 
 template <int FLAGS, bool NFCD = false>
 __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_t rend, const uint32_t *H, const uint16_t *sfast,
-                        TileWaveMem &M, uint4 *pool, PassClock &pc) {
+                        TileWaveMem &M, uint4 *pool, PassClock &pc, bool raw = false) {
+    const bool RAW = NFCD && raw;  // (the HF text: normalize_text and the HF check off)
     static_assert(FLAGS == 3, "the tile path implements normalize_text with its defaults");
     const int lane = w_lane();
     const RowArgs &a = ta.ra;
     const BpeDev &m = a.bpe;
     pc.mark(TP_STAGE);
-    const TileRows tr = tile_front<T_BCAP, TileWaveMem, NFCD>(a, r0, rend, H, M);
+    const TileRows tr = tile_front<T_BCAP, TileWaveMem, NFCD>(a, r0, rend, H, M, raw);
     const int nr = tr.nr;
     const uint32_t vlen = tr.vlen;
     if (AK_KNOCKOUT == 10) return nr;
@@ -1107,10 +1113,10 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
             const uint16_t nx = in && kk + 1 < vlen ? nx0 : V_DEAD;
             const bool special = x >= V_SPECIAL;
 #if AK_D2_BITWISE
-            const bool drop = in & !special & (x != (uint16_t)'\n') & (x == pa) & ((pa == pb) | (nx == x));
+            const bool drop = !RAW & in & !special & (x != (uint16_t)'\n') & (x == pa) & ((pa == pb) | (nx == x));
             const bool keep = in & !drop;
 #else
-            const bool drop = in && !special && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
+            const bool drop = !RAW && in && !special && x != (uint16_t)'\n' && x == pa && (pa == pb || nx == x);
             const bool keep = in && !drop;
 #endif
             // hot word: LDS for U+0000..017F / U+0900..09FF, the global trie for the rest (rare)
@@ -1148,9 +1154,9 @@ __device__ __forceinline__ int bpe_tile(const TileArgs &ta, uint64_t r0, uint64_
             const bool trig = hfc && nfc_trig<true>(h, hprev);
             const bool hpc = hfc && nfc_pair_cand(h, hprev);
 #endif
-            if (w_ballot(trig || hpc)) {
+            if (!RAW && w_ballot(trig || hpc)) {  // (fb bit 1: sent on for HF's NFKC, ak_nfc_wave.h)
                 const uint32_t rrow = rs + w_rank_incl(RM) - 1;
-                if (trig || (hpc && compose_pair<NF_HFK>(hprev & 0xFFFFu, x))) M.fb[rrow] = 1;
+                if (trig || (hpc && compose_pair<NF_HFK>(hprev & 0xFFFFu, x))) M.fb[rrow] |= 2;
             }
             // pre-tokenizer + ids
 #if AK_D2_BITWISE

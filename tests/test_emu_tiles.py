@@ -319,3 +319,59 @@ def test_wave_nfc_epoch_edges(bpe_model, spm_model):
     ids, oo, _ = emu.spm_tiles(emu.Model(spm=spm_model), buf, offs, rows=8)
     ref, ro = O.OracleSPM(spm_model).encode_batch(buf, offs)
     assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_hf_nfkc_rows_through_the_wave(golden, bpe_model):
+    """Rows whose normalize_text output HF's NFKC changes (the golden fuzz rows where HF's ccc
+    reorders marks, and chars normalize_text drops between a letter and a nukta, which HF then
+    composes: U+0928 U+0001 U+093C -> U+0929) are sent on by the tile's pass N; the fallback wave
+    rebuilds their HF text (hf_epoch_gather: normalize_text's map, remove_elongations, compat
+    spaces, NFC with HF's ccc) and encodes it with normalize_text off (bpe_tile<.., RAW>): every one
+    finishes in the wave (none left for the one-lane kernel) and equals the oracle."""
+    import unicodedata
+    hf = []
+    for r in golden:
+        if r["set"] != "fuzz":
+            continue
+        t = "".join(" " if c.isspace() and unicodedata.normalize("NFKC", c) == " " else c for c in r["norm"])
+        if unicodedata.normalize("NFKC", t) != t:
+            hf.append(r["text"])
+    assert len(hf) >= 5
+    extra = ["न\x01़", "नननन\x01़ x", "ab न\u0007़़़ cd", "x़॒॓", "NAAAAN\x01़   ok"]
+    texts = [t for t in hf + extra for _ in range(3)]
+    buf, offs = O.pack(texts)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    ids, oo, _ = emu.bpe_tiles(emu.Model(bpe=bpe_model), buf, offs, rows=8)
+    fb, nfc = emu.last_fallback_rows(), emu.last_nfc_rows()
+    assert fb >= 3 * len(hf) and nfc == fb, (fb, nfc)
+    assert np.array_equal(oo, ro) and np.array_equal(ids, ref)
+
+
+def test_hf_nfkc_rounds_and_edges(bpe_model):
+    """HF rows past one round's text reserve (rows of 300-760 bytes: several rounds per epoch, the
+    rest moved down), mixed with rows NFC changes, invalid rows and empty rows; elongation runs at
+    row edges (a row ending in "aa" before a row opening with "a": runs never cross rows), dropped
+    chars inside runs, compat spaces (U+00A0, U+3000) and newlines: every row equals the oracle."""
+    rng = np.random.default_rng(41)
+    hf_seeds = ["न\x01़", "ab न\u0007़़़ cd", "ड\x02़ ok", "aaa\x01a न\x03़", "x 　न\x01़\n\n\nyy"]
+    other = ["ạ́", "é ऩि", "plain ascii row", "", "क़ ড় x"]
+    raw = []
+    for i in range(260):
+        k = rng.random()
+        if k < 0.55:
+            t = hf_seeds[rng.integers(len(hf_seeds))]
+            r = rng.random()
+            if r < 0.4:
+                t = t + " " + "x" * int(rng.integers(280, 700))
+            elif r < 0.6:
+                t = "a" * int(rng.integers(1, 5)) + t + "a" * int(rng.integers(1, 5))
+            raw.append(t.encode())
+        elif k < 0.9:
+            raw.append(other[rng.integers(len(other))].encode())
+        else:
+            raw.append([b"\xe0\xa4", b"\x80lead", b"a\x80b"][rng.integers(3)])
+    buf, offs = _raw_rows(raw)
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(buf, offs)
+    ids, oo, _ = emu.bpe_tiles(emu.Model(bpe=bpe_model), buf, offs, rows=8)
+    assert emu.last_nfc_rows() > 120
+    assert rows_ints(ids, oo) == rows_ints(ref, ro)

@@ -635,6 +635,34 @@ def test_bpe_fallback_rows_through_the_wave_nfc(golden, golden_nfkc, eng, bpe_mo
     assert torch.equal(oo2, oo) and torch.equal(ids2, ids)
 
 
+def test_bpe_hf_nfkc_rows_finish_in_the_wave(golden, eng, bpe_model, monkeypatch):
+    """Rows whose normalize_text output HF's NFKC changes (the golden fuzz rows where HF's ccc
+    reorders marks; a char normalize_text drops between a letter and a nukta HF then composes),
+    replicated so every fallback wave holds some, long ones past a round's text reserve: the
+    fallback waves rebuild their HF text and encode it with normalize_text off, none is left for the
+    one-lane kernel, and the ids equal the oracle and the one-lane path alone (AK_NO_NFC_WAVE)."""
+    import unicodedata
+    hf = []
+    for r in golden:
+        if r["set"] != "fuzz":
+            continue
+        t = "".join(" " if c.isspace() and unicodedata.normalize("NFKC", c) == " " else c for c in r["norm"])
+        if unicodedata.normalize("NFKC", t) != t:
+            hf.append(r["text"])
+    extra = ["न\x01़", "नननन\x01़ x", "ab न\u0007़़़ cd", "x 　न\x01़\n\n\nyy", "ड\x02़ " + "x" * 600]
+    texts = (hf + extra) * 400
+    gb, go = eng.pack(texts)
+    m = eng.BPE(bpe_model)
+    ids, oo = m.encode_batch(gb, go)
+    d = eng.fallback_detail()
+    assert d["rows"] >= len(hf) * 400 and d["one_lane"] == 0, d
+    ref, ro = O.OracleBPE(bpe_model).encode_batch(*O.pack(texts))
+    assert np.array_equal(_cpu(oo).astype(np.uint64), ro) and np.array_equal(_cpu(ids).astype(np.uint32), ref)
+    monkeypatch.setenv("AK_NO_NFC_WAVE", "1")
+    ids2, oo2 = m.encode_batch(gb, go)
+    assert torch.equal(oo2, oo) and torch.equal(ids2, ids)
+
+
 def test_spm_fallback_rows_through_the_wave_nfc(golden, eng, spm_model, monkeypatch):
     """As above for SentencePiece (k_spm_nfc after k_spm_redo): the fallback rows of the golden
     alphabet / fuzz / adversarial sets, replicated 40 times, mostly finish in the wave path and
