@@ -124,15 +124,21 @@ __device__ __forceinline__ uint32_t compose_hashed(const uint4 *ch, uint32_t a, 
 // table holds (tools/gen_tables.py: comp_first / comp_second, Hangul L, LV, V, T). Inlined, so its
 // LDS accesses stay LDS accesses. Returns the length, or -1 past NW_DCAP.
 // HF: the same with HF's ccc (ak_dev.h nfc_full<NF_HF>: HF's NFKC over the normalize_text alphabet).
+// The input chars come as entries (nfc_ent, made where the segment pass looked the char up): only a
+// char that decomposes, and a composite the segment makes, are looked up again.
+constexpr uint32_t NE_CP = 0x1FFFFFu, NE_DECOMP = 1u << 21, NE_SECOND = 1u << 22, NE_FIRST = 1u << 23;
+template <bool HF = false>
+__device__ __forceinline__ uint32_t nfc_ent(uint32_t cp, uint2 pr) {  // cp | decomposes | second | first | ccc << 24
+    return cp | (p_decomp(pr) ? NE_DECOMP : 0u) | (p_second(pr) ? NE_SECOND : 0u) | (((pr.x >> 23) & 1u) ? NE_FIRST : 0u) |
+           ((uint32_t)(HF ? p_ccc_hf(pr) : p_ccc(pr)) << 24);
+}
 template <bool HF = false>
 __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n, const uint2 *fast, const uint4 *chash) {
-    constexpr uint32_t CP = 0x1FFFFFu, SECOND = 1u << 22;
-    auto ent = [&](uint32_t cp, uint2 pr) {
-        return cp | (p_second(pr) ? SECOND : 0u) | ((uint32_t)(HF ? p_ccc_hf(pr) : p_ccc(pr)) << 24);
-    };
+    constexpr uint32_t CP = NE_CP, SECOND = NE_SECOND;
     int m = 0;
     for (int i = 0; i < n; ++i) {
-        const uint32_t cp = in[i];
+        const uint32_t xi = in[i];
+        const uint32_t cp = xi & CP;
         if (cp - H_SBASE < H_SCOUNT) {  // Hangul syllable: L V (T), algorithmically
             const uint32_t x = cp - H_SBASE;
             if (m + 3 > NW_DCAP) return -1;
@@ -141,16 +147,17 @@ __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n,
             if (x % H_TCOUNT) dec[m++] = (H_TBASE + x % H_TCOUNT) | SECOND;
             continue;
         }
+        if (!(xi & NE_DECOMP)) {
+            if (m + 1 > NW_DCAP) return -1;
+            dec[m++] = xi;
+            continue;
+        }
         const uint2 pr = prop(fast, cp);
         const uint32_t len = (pr.y >> 16) & 7, idx = pr.y >> 19;
-        if (m + (int)(len ? len : 1) > NW_DCAP) return -1;
-        if (!len) {
-            dec[m++] = ent(cp, pr);
-        } else {
-            for (uint32_t k = 0; k < len; ++k) {
-                const uint32_t d = AK_UT_DECOMP[idx + k];
-                dec[m++] = ent(d, prop(fast, d));
-            }
+        if (m + (int)len > NW_DCAP) return -1;
+        for (uint32_t k = 0; k < len; ++k) {
+            const uint32_t d = AK_UT_DECOMP[idx + k];
+            dec[m++] = nfc_ent<HF>(d, prop(fast, d));  // (a full decomposition: d does not decompose)
         }
     }
     for (int i = 1; i < m; ++i) {  // canonical ordering: stable insertion sort of non-starter runs
@@ -188,7 +195,7 @@ __device__ __forceinline__ int nfc_seg(const uint32_t *in, uint32_t *dec, int n,
             starter = w;
             st = ch;
             first = ch - H_SBASE < H_SCOUNT ? (ch - H_SBASE) % H_TCOUNT == 0
-                                            : (ch - H_LBASE < H_LCOUNT || ((prop(fast, ch).x >> 23) & 1u));
+                                            : (ch - H_LBASE < H_LCOUNT || (x & NE_FIRST) != 0u);
         }
         lastc = c;
         dec[w++] = ch;
@@ -220,8 +227,8 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
         int w = 0;
         if (act && !R.vfail[W.segrow[j]]) {  // (a row found invalid while decoding has no text)
             const uint32_t c0 = W.cps[s];
-            if (e - s == 1 && !p_decomp(prop(fast, c0)) && c0 - H_SBASE >= H_SCOUNT) {
-                dec[0] = c0;
+            if (e - s == 1 && !(c0 & NE_DECOMP) && (c0 & NE_CP) - H_SBASE >= H_SCOUNT) {
+                dec[0] = c0 & NE_CP;
                 w = 1;
             } else {
                 w = nfc_seg<HF>(W.cps + s, dec, e - s, fast, chash);
@@ -277,7 +284,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
             const int s0 = (int)W.seg[j], e0 = (int)W.seg[j + 1];
             const uint32_t r = W.segrow[j] & 0x7Fu;
             const uint32_t c0 = W.cps[s0];
-            const bool trivial = R.vfail[r] || (e0 - s0 == 1 && !p_decomp(prop(fast, c0)) && c0 - H_SBASE >= H_SCOUNT);
+            const bool trivial = R.vfail[r] || (e0 - s0 == 1 && !(c0 & NE_DECOMP) && (c0 & NE_CP) - H_SBASE >= H_SCOUNT);
             W.segrow[j] = (uint8_t)(r | (trivial ? 0u : 0x80u));
         }
     }
@@ -334,7 +341,7 @@ __device__ __forceinline__ void nfc_flush_batch(NfcWaveMem &W, NfcRows &R, int &
                     w = (int)ntw[slot];
                     src = W.dec + slot * NW_DCAP;
                 } else {
-                    one = W.cps[W.seg[j]];
+                    one = W.cps[W.seg[j]] & NE_CP;
                     w = 1;
                 }
             }
@@ -548,13 +555,14 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             const uint32_t tag = (x >> 24) & 0x7Fu;
             const bool first = tag != w_prev(tag, carry_tag);
             carry_tag = w_bcast(tag, 63);
-            const bool st = in && ((x >> 31) || first || p_stable(prop(fast, cp)));
+            const uint2 pr = prop(fast, cp);
+            const bool st = in && ((x >> 31) || first || p_stable(pr));
             const uint64_t SM = w_ballot(st);
             if (st) {
                 S.seg[ns + (int)w_rank(SM)] = (uint16_t)ci;
                 S.segrow[ns + (int)w_rank(SM)] = (uint8_t)((x >> 24) & 0x7Fu);
             }
-            if (in) S.cps[ci] = cp;
+            if (in) S.cps[ci] = nfc_ent<false>(cp, pr);
             ns += w_popc(SM);
         }
         w_sync();
@@ -714,7 +722,7 @@ __device__ __forceinline__ uint32_t hf_epoch_gather(const TileArgs &ta, const Nf
                 S.seg[ns + (int)w_rank(SM)] = (uint16_t)ci;
                 S.segrow[ns + (int)w_rank(SM)] = (uint8_t)tag;
             }
-            if (in) S.cps[ci] = cp;
+            if (in) S.cps[ci] = nfc_ent<true>(cp, pr);
             ns += w_popc(SM);
         }
         w_sync();
