@@ -437,6 +437,9 @@ __device__ __forceinline__ void nfc_fb3(uint32_t *fb3, uint32_t *fb3_count, uint
     }
 }
 
+#ifndef AK_NFC_CHUNKS
+#define AK_NFC_CHUNKS 1  // the gather copies 16-byte blocks, a lane each (0: a lane per byte, each byte's row searched)
+#endif
 #ifndef AK_NFC_SPLIT
 #define AK_NFC_SPLIT 0  // development aid (a build variant): the gather's phases' wave-cycles into the
 #endif              // tile counters (profiling level 2; the waves' own pass clocks off)
@@ -508,6 +511,37 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             R.vfail[vi] = 0;
         }
         NFC_SPLIT_MARK(0);
+#if AK_NFC_CHUNKS
+        // the batch's bytes by 16-byte blocks: block q of a row is the aligned block (o0 & ~15) + 16 q
+        // of the input; a lane per block (its row found once per 64 blocks, not per 64 bytes: each
+        // search is 6 dependent shuffles) loads it and stores the row's bytes in it, each with its
+        // virtual row in segrow (bit 7: the row's first byte) for the decode
+        (void)key;
+        const uint32_t nq = row_in && a ? (uint32_t)(((o0 + a + 15) >> 4) - (o0 >> 4)) : 0u;
+        uint32_t tq;
+        const uint32_t Q = w_exscan(nq, &tq);
+        const uint32_t qkey = take ? Q : 0xFFFFFFFFu;
+        for (uint32_t qb = 0; qb < tq; qb += 64) {
+            const uint32_t q = qb + (uint32_t)lane;
+            const bool act = q < tq;
+            const int j = w_last_le(qkey, act ? q : 0u);
+            const uint64_t ro0 = w_shfl(o0, j);
+            const uint32_t rst = w_shfl(start, j), ra = w_shfl(a, j), rq = w_shfl(Q, j), rvi = w_shfl(vi, j);
+            const uint64_t blk = (ro0 & ~15ull) + 16ull * (uint64_t)(q - rq);
+            const uint4 d = act ? load_x4((const uint4 *)(ta.ra.in + blk)) : make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const uint64_t at = blk + (uint64_t)t;
+                if (act && at >= ro0 && at < ro0 + ra) {
+                    const uint32_t pp = rst + (uint32_t)(at - ro0);
+                    S.bytes[pp] = (uint8_t)(dw[t >> 2] >> (8 * (t & 3)));
+                    S.segrow[pp] = (uint8_t)(rvi | (at == ro0 ? 0x80u : 0u));
+                }
+            }
+        }
+        if (lane < 16 && blen + (uint32_t)lane < (uint32_t)NW_MAXB + 32) S.bytes[blen + lane] = 0;  // decode reads 4-byte windows
+#else
         // the batch's bytes (+ zero slack: decode reads 4-byte windows)
         for (uint32_t base = 0; base < blen + 8; base += 64) {
             const uint32_t p = base + (uint32_t)lane;
@@ -516,6 +550,7 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             if (p < blen) S.bytes[p] = ta.ra.in[src];
             else if (p < (uint32_t)NW_MAXB + 32) S.bytes[p] = 0;
         }
+#endif
         w_sync();
         NFC_SPLIT_MARK(1);
         // decode: chars tagged with their virtual row (bits 24-30) and row start (bit 31)
@@ -526,8 +561,13 @@ __device__ __forceinline__ uint32_t nfc_epoch_gather(const TileArgs &ta, uint32_
             const uint32_t b = inb ? S.bytes[p] : 0u;
             const bool lead = inb && (b & 0xC0u) != 0x80u;
             const uint32_t cp = lead ? decode_word(lds_word(S.bytes, p), (int)p, (int)blen) : 0u;
+#if AK_NFC_CHUNKS
+            const uint32_t sr = inb ? S.segrow[p] : 0u;
+            const uint32_t rv = sr & 0x7Fu, rs = (sr & 0x80u) ? p : 0xFFFFFFFFu;
+#else
             const int j = w_last_le(key, inb ? p : 0u);
             const uint32_t rv = w_shfl(vi, j), rs = w_shfl(start, j);
+#endif
             if (lead) {
                 if (cp == 0xFFFFFFFFu) R.vfail[rv] = 1;
                 else atomicAdd(&R.vbytes[rv], (uint32_t)utf8_len(cp));
