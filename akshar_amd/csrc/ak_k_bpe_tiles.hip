@@ -53,7 +53,10 @@ __global__ __launch_bounds__(TILE_BLOCK, AK_BPE_TILE_WPE) void k_bpe_tiles(TileA
 // to its fallback slot (ta.ra.out is the second staging half). A row this cannot take (invalid
 // UTF-8, over NW_MAXB bytes, a segment past NW_DCAP, a fallback again in the tile: HF's NFKC changes
 // the text, or ids past its slot) goes on to k_tile_fb through the second list (fb3).
-constexpr int NFC_BLOCK = 512;  // 8 waves share the tables (NfcWaveLds: 16.5 KB each)
+#ifndef AK_NFC_BLOCK
+#define AK_NFC_BLOCK 640
+#endif
+constexpr int NFC_BLOCK = AK_NFC_BLOCK;  // 10 waves share the tables (NfcWaveLds: 12.2 KB each)
 
 template <int FLAGS>
 __global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count) {

@@ -25,7 +25,10 @@
 namespace ak {
 
 constexpr int NW_MAXB = T_BCAP;  // rows the tile kernel could take (a longer NFC text falls back anyway)
-constexpr int NW_DCAP = 32;      // code points of one segment's NFC
+#ifndef AK_NW_DCAP
+#define AK_NW_DCAP 16
+#endif
+constexpr int NW_DCAP = AK_NW_DCAP;  // code points of one segment's NFC
 
 // An epoch: the fallback rows a wave NFC-normalizes back to back before encoding them together
 constexpr uint32_t NE_TCAP = 8192;  // their NFC text, bytes
@@ -46,8 +49,9 @@ struct NfcRows {              // the epoch's rows, through its three phases
     uint8_t vfail[NE_VMAX];   // a segment's NFC failed (the row goes on to fb3)
 };
 // A fallback wave's LDS: the NFC scratch and the tile's buffers in one place (the phases alternate:
-// every tile field is set again at each epoch's first tile), the rows beside them. 16.5 KB for BPE
-// instead of 20 KB: eight waves per CU (one 512-thread block) where four fitted.
+// every tile field is set again at each epoch's first tile), the rows beside them. 12.2 KB for BPE
+// (16-code-point segment slots; 16.5 KB with 32, 20 KB without the union): ten waves per CU (one
+// 640-thread block) where eight fitted (fuzz BPE waves -13 %, profiles/r06t_*), four before the union.
 template <class TM>
 struct NfcWaveLds {
     union {
