@@ -54,9 +54,9 @@ __global__ __launch_bounds__(TILE_BLOCK, AK_BPE_TILE_WPE) void k_bpe_tiles(TileA
 // UTF-8, over NW_MAXB bytes, a segment past NW_DCAP, a fallback again in the tile: HF's NFKC changes
 // the text, or ids past its slot) goes on to k_tile_fb through the second list (fb3).
 #ifndef AK_NFC_BLOCK
-#define AK_NFC_BLOCK 640
+#define AK_NFC_BLOCK 704
 #endif
-constexpr int NFC_BLOCK = AK_NFC_BLOCK;  // 10 waves share the tables (NfcWaveLds: 12.2 KB each)
+constexpr int NFC_BLOCK = AK_NFC_BLOCK;  // 11 waves share the tables (NfcWaveLds: 12.2 KB each; 157 KB of LDS in all)
 
 template <int FLAGS>
 __global__ __launch_bounds__(NFC_BLOCK) void k_bpe_nfc(TileArgs ta, uint8_t *ebuf, uint32_t *fb3, uint32_t *fb3_count) {

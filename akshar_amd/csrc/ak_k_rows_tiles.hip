@@ -39,9 +39,9 @@ __global__ __launch_bounds__(RT_BLOCK) void k_rows_tiles(TileArgs ta, RowsOut o)
 // segments, rows_tile<OPS, NFCD> over the NFC text, the outputs to the rows' fallback slots; the
 // rows it cannot take go on to k_rows_tile_fb through fb3.
 #ifndef AK_RT_NFC_BLOCK
-#define AK_RT_NFC_BLOCK 640
+#define AK_RT_NFC_BLOCK 704
 #endif
-constexpr int RT_NFC_BLOCK = AK_RT_NFC_BLOCK;  // 10 waves (NfcWaveLds<RowsWaveMem>)
+constexpr int RT_NFC_BLOCK = AK_RT_NFC_BLOCK;  // 11 waves (NfcWaveLds<RowsWaveMem>)
 template <int OPS>
 __global__ __launch_bounds__(RT_NFC_BLOCK) void k_rows_nfc(TileArgs ta, RowsOut ofb, uint8_t *ebuf, uint32_t *fb3,
                                                            uint32_t *fb3_count) {

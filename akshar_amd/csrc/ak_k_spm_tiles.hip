@@ -124,7 +124,7 @@ int small_call_spm(AkWs *w, const RowArgs &a, const uint16_t *scode, const Small
 
 // rows the word pool sent back (ak_tile_spm.h spm_redo_wave): the waves' epochs, the tile variant
 #ifndef AK_SPM_NFC_BLOCK
-#define AK_SPM_NFC_BLOCK 640
+#define AK_SPM_NFC_BLOCK 704
 #endif
 constexpr int SPM_REDO_BLOCK = AK_SPM_NFC_BLOCK;  // the grid's waves = k_spm_nfc's (the same epoch buffers)
 template <int FLAGS>
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(SPM_REDO_BLOCK) void k_spm_redo(TileArgs ta, uint8_
 
 // the tile kernel's fallback rows in each wave's epochs (ak_tile_spm.h spm_nfc_wave): NFC, the tile
 // variant over the NFC text, the ids to the rows' fallback slots; the rest go on in fb3 (k_spm_tile_fb)
-constexpr int SPM_NFC_BLOCK = AK_SPM_NFC_BLOCK;  // 10 waves (NfcWaveLds: 12.5 KB each)
+constexpr int SPM_NFC_BLOCK = AK_SPM_NFC_BLOCK;  // 11 waves (NfcWaveLds: 12.2 KB each)
 template <int FLAGS>
 __global__ __launch_bounds__(SPM_NFC_BLOCK) void k_spm_nfc(TileArgs ta, uint8_t *ebuf, uint32_t *fb3,
                                                           uint32_t *fb3_count) {

@@ -50,8 +50,9 @@ struct NfcRows {              // the epoch's rows, through its three phases
 };
 // A fallback wave's LDS: the NFC scratch and the tile's buffers in one place (the phases alternate:
 // every tile field is set again at each epoch's first tile), the rows beside them. 12.2 KB for BPE
-// (16-code-point segment slots; 16.5 KB with 32, 20 KB without the union): ten waves per CU (one
-// 640-thread block) where eight fitted (fuzz BPE waves -13 %, profiles/r06t_*), four before the union.
+// (16-code-point segment slots; 16.5 KB with 32, 20 KB without the union): eleven waves per CU (one
+// 704-thread block, 157 KB of LDS; ten at 640 threads) where eight fitted (fuzz BPE waves -13 % and
+// -8 %, profiles/r06t_*, r06zb_*), four before the union.
 template <class TM>
 struct NfcWaveLds {
     union {
